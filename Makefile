@@ -1,0 +1,37 @@
+# Builds the product library (HIP, gfx950) and the CPU oracle (test infrastructure).
+#   make            -> kmer-ml_amd/kmerml/_lib/libkmerhip.so + oracle/build/liboracle.so
+#   make lib        -> product library only
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+CSRC     := kmer-ml_amd/csrc
+OUTDIR   := kmer-ml_amd/kmerml/_lib
+OBJDIR   := $(CSRC)/build
+LIB      := $(OUTDIR)/libkmerhip.so
+OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o
+HDRS     := $(CSRC)/kmh_internal.h include/kmerhip.h
+
+all: lib oracle
+
+lib: $(LIB)
+
+$(LIB): $(OBJS)
+	@mkdir -p $(OUTDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(OBJDIR) $(OUTDIR)/libkmerhip.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib oracle clean

@@ -1,0 +1,229 @@
+"""Benchmark: bases/s counted into the genomes x k-mers count matrix on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--k 12] [--genomes 64]
+                  [--genome-len 100000000] [--assemble auto|allgather|none]
+
+Workload (BASELINE.json configs): N = 1 is config 3 -- 64 synthetic 100 Mbp genomes,
+k = 12, dense 4^12 histogram per genome on one MI355X.  N > 1 is config 4 -- the same 64
+genomes sharded in contiguous blocks of 64/N per GPU (one process per GPU, launched by
+torch.distributed.run) with an RCCL all-gather that assembles the [64, 4^12] matrix on
+every rank inside each step.  A step is one pass of the count path over every genome
+(plus the all-gather for N > 1); the genomes are generated on the device before timing,
+so inputs are resident in HBM when the timed region starts.
+
+Printed by rank 0: one JSON line with the driver's fields plus
+  roofline      the dominant kernel: algorithmic bytes per launch / mean launch time
+                (HIP events on the launch stream) against 8 TB/s;
+  step_roofline the whole step: (sum L * 1 B + G * 4^k * 4 B) / step time / 8 TB/s;
+  cpu_baseline  the reference's algorithm (oracle/kmers.py, the same pure-Python window
+                loop as generate.py:49-58) timed on one host core over a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "kmer-ml_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from kmerml import _native  # noqa: E402
+
+METRIC = "bases/s counted into k-mer feature matrix (1/2/4/8 GPU) + % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+SEED_BASE = 0x6B6D65724D4C0000
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--k", type=int, default=12)
+    p.add_argument("--genomes", type=int, default=64, help="total genomes over all ranks")
+    p.add_argument("--genome-len", type=int, default=100_000_000)
+    p.add_argument("--assemble", choices=["auto", "allgather", "none"], default="auto")
+    p.add_argument("--cpu-sample", type=int, default=4_000_000,
+                   help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
+    p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(sample, k):
+    """Time the reference's per-window loop (oracle restatement) on one core."""
+    sys.path.insert(0, HERE)
+    from oracle import kmers as okmers
+    from oracle import synth as osynth
+    seq = osynth.synth_bases(sample, osynth.genome_seed(0)).tobytes().decode()
+    t0 = time.perf_counter()
+    table = okmers.count_sequence(seq, k)
+    dt = time.perf_counter() - t0
+    assert sum(table.values()) == sample - k + 1
+    return {"value": sample / dt, "unit": "bases/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} bases of synthetic genome 0, k={k}: the count loop of "
+                      f"generate.py:49-58 restated in pure Python (oracle/kmers.py), "
+                      f"{dt:.2f} s on one core",
+            "seconds": dt, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def load_traffic(path, config_key):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this command."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    entry = d.get(config_key)
+    return entry if isinstance(entry, dict) else None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    k, G, L = a.k, a.genomes, a.genome_len
+    lo, hi = (G * rank) // world, (G * (rank + 1)) // world
+    g_local = hi - lo
+    B = -(-G // world)
+    assemble = (world > 1) if a.assemble == "auto" else (a.assemble == "allgather")
+    bins = 1 << (2 * k)
+
+    # CPU baseline first (rank 0, N = 1 only), so it never overlaps GPU timing.
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        cpu = cpu_baseline(a.cpu_sample, k)
+
+    ctx = _native.context(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    stride = (L + 15) // 16 * 16   # genome starts 16-byte aligned; any gap is 'N' (not a base)
+    d_seq = torch.empty(max(g_local, 1) * stride, dtype=torch.uint8, device=dev)
+    if stride != L:
+        d_seq.fill_(ord("N"))
+    if g_local:
+        ctx.synth_dev(d_seq.data_ptr(), L, stride, g_local, SEED_BASE + lo, s)
+    offsets = np.arange(g_local + 1, dtype=np.uint64) * np.uint64(stride)
+    local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
+    full = torch.empty((world * B, bins), dtype=torch.int32, device=dev) if assemble else None
+    t_count = []
+
+    def step(record=False):
+        e0 = torch.cuda.Event(enable_timing=True) if record else None
+        e1 = torch.cuda.Event(enable_timing=True) if record else None
+        if record:
+            e0.record(stream)
+        if g_local:
+            ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, local.data_ptr(), s)
+        if record:
+            e1.record(stream)
+            t_count.append((e0, e1))
+        if assemble:
+            dist.all_gather_into_tensor(full, local)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(record=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernels = ctx.timing_report()
+    ctx.timing(False)
+    count_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in t_count]))
+    if world > 1:
+        t = torch.tensor([elapsed, count_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, count_ms = float(t[0]), float(t[1])
+
+    # sanity: every row sums to the number of valid windows (all-ACGT genomes)
+    rows = full[:G] if (assemble and G % world == 0) else local[:g_local]
+    ok = bool(torch.all(rows.sum(1, dtype=torch.int64) == max(L - k + 1, 0)).item())
+
+    if rank == 0:
+        ms = elapsed / a.steps * 1e3
+        total_bases = G * L if (assemble or world == 1) else g_local * L * world
+        value = total_bases / (elapsed / a.steps)
+        algo_step = G * L + G * bins * 4
+        budget = int(os.environ.get("KMH_SUF_BUDGET_MB", "256")) << 20   # kmh_dense.hip batching
+        genomes_per_batch = max(1, min(g_local, budget // max(1, ((L - k + 1 + 16383) // 16384) * 32768)))
+        dom = max(kernels.items(), key=lambda kv: kv[1][1]) if kernels else None
+        roof = None
+        if dom:
+            name, (launches, tot) = dom
+            per_launch_ms = tot / launches
+            if name == "k_partition":
+                algo = genomes_per_batch * L                 # bases read once (1 B each)
+            elif name == "k_bucket_count":
+                algo = genomes_per_batch * bins * 4          # count row slice written once
+            else:
+                algo = g_local * (L + bins * 4) / max(1, launches / a.steps)
+            achieved = algo / (per_launch_ms * 1e-3) / 1e9
+            traffic = load_traffic(a.pmc_summary, f"{name}:k{k}:L{L}")
+            roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                    "algorithmic_bytes_per_launch": algo, "mean_launch_ms": round(per_launch_ms, 4),
+                    "launches_per_step": launches / a.steps}
+        count_rate = g_local * L / (count_ms * 1e-3)
+        out = {
+            "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": (f"config{3 if world == 1 else 4}: {G} synthetic {L // 1_000_000} Mbp "
+                                    f"genomes, k={k} dense 4^{k} count matrix"
+                                    + ("" if world == 1 else f", sharded {G}/{world} per GPU + RCCL all-gather")),
+                       "genomes": G, "genome_len": L, "k": k,
+                       "parallelism": f"genome-sharded x{world}" + (" + allgather" if assemble else "")},
+            "roofline": roof,
+            "step_roofline": {"algorithmic_bytes": algo_step, "achieved_GBs": round(algo_step / (ms * 1e-3) / 1e9, 1),
+                              "frac": round(algo_step / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "count_ms_per_step_rank_max": round(count_ms, 4),
+            "count_only_bases_per_s_per_gpu": count_rate,
+            "kernels": {n: {"launches": l, "total_ms": round(t, 4), "mean_ms": round(t / l, 4)}
+                        for n, (l, t) in kernels.items()},
+            "rows_checked": ok,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("row-sum check failed")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * kmerhip.h -- C ABI of libkmerhip.so, the MI355X (gfx950) k-mer counting library
+ * that replaces the hot path of Masthetheus/kmer-ml.
+ *
+ * The reference has no FFI: its boundary is the Python class API.  Each entry point
+ * below replaces one piece of /root/reference/kmerml/kmers/generate.py; the Python
+ * host mirror (kmer-ml_amd/kmerml/kmers/generate.py) binds them with ctypes so that
+ * scripts/extract_kmers.py runs unchanged.  See INTEGRATION.md for the binding.
+ *
+ * Conventions
+ *   - Plain C types only; every int-returning call returns KMH_OK (0) or a negative
+ *     KMH_ERR_* code; the message is available from kmh_last_error(ctx) (or
+ *     kmh_last_error(NULL) for calls without a context).  No C++ exception crosses
+ *     this boundary.
+ *   - The caller owns every host buffer; the library owns the device buffers of a
+ *     context.  Functions with a _dev suffix take DEVICE pointers (hipMalloc /
+ *     torch tensors on the context's device) and a hipStream_t passed as void*
+ *     (NULL = the context's own stream); they only enqueue work.
+ *   - One context per (thread, device).  Calls on one context are serialised by the
+ *     caller; different contexts may be used concurrently.
+ *   - Base alphabet: A/C/G/T in either case are bases (generate.py:41 upper()s the
+ *     record, :55 keeps windows whose characters are all in "ACGT"); every other
+ *     byte breaks windows.  k-mer codes are 2 bits per base, A=0 C=1 G=2 T=3, first
+ *     base most significant, so code order = lexicographic order of the strings.
+ *   - Counts are exact 32-bit integers: a sequence handed to a count call must be
+ *     shorter than 2^32 - 1 bytes (KMH_ERR_INVALID otherwise).
+ */
+#ifndef KMERHIP_H
+#define KMERHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMH_OK               0
+#define KMH_ERR_INVALID     -1  /* bad argument                        */
+#define KMH_ERR_HIP         -2  /* HIP runtime error                    */
+#define KMH_ERR_NOMEM       -3  /* host or device allocation failed     */
+#define KMH_ERR_UNSUPPORTED -4  /* k outside the supported range        */
+#define KMH_ERR_IO          -5  /* file could not be read               */
+
+#define KMH_MAX_DENSE_K  12     /* dense 4^k tables: 1 <= k <= 12        */
+#define KMH_MAX_SPARSE_K 32     /* sorted sparse path: 13 <= k <= 32     */
+
+typedef struct kmh_ctx kmh_ctx;
+typedef struct kmh_fasta kmh_fasta;
+typedef struct kmh_kmers kmh_kmers;
+
+/* ---- library / context ------------------------------------------------------ */
+
+/* Version string, e.g. "kmerhip 0.1.0 gfx950". */
+const char* kmh_version(void);
+
+/* Create a context on HIP device `device`: selects the device, creates a stream and
+ * an empty device workspace.  Replaces nothing in the reference (it has no device). */
+int kmh_ctx_create(int device, kmh_ctx** out);
+void kmh_ctx_destroy(kmh_ctx* ctx);
+
+/* Last error message of `ctx`, or of the calling thread's context-free calls when
+ * ctx == NULL.  Never NULL; "" when there was no error. */
+const char* kmh_last_error(const kmh_ctx* ctx);
+
+/* Per-kernel timing with HIP events on the launch stream (bench / profiling).
+ * enable != 0 starts recording; kmh_timing_report fills up to `cap` entries of
+ * name/launches/total_ms and returns the number of distinct kernels. */
+int kmh_timing_enable(kmh_ctx* ctx, int enable);
+int kmh_timing_report(kmh_ctx* ctx, const char** names, uint64_t* launches,
+                      double* total_ms, int cap);
+
+/* ---- FASTA ingest (host) ----------------------------------------------------- */
+/* Replaces `for record in SeqIO.parse(fasta_file, "fasta")` + `str(record.seq)`
+ * (generate.py:39-41; Biopython 1.85 SimpleFastaParser semantics): universal newlines,
+ * text before the first '>' skipped, id = first whitespace token of the title,
+ * sequence lines rstrip()-ed and joined with every ' ' and '\r' removed. */
+int kmh_fasta_read(const char* path, kmh_fasta** out);
+uint64_t kmh_fasta_count(const kmh_fasta* f);
+/* Record i: id bytes, sequence bytes (case preserved) and the sequence length in
+ * characters (UTF-8 code points; equals the byte length for ASCII input), the value
+ * generate.py:44 compares with max(k_values). */
+int kmh_fasta_record(const kmh_fasta* f, uint64_t i, const char** id, uint64_t* id_len,
+                     const uint8_t** seq, uint64_t* seq_len, uint64_t* char_len);
+/* Concatenate the sequences of the records whose char_len >= min_len (the record
+ * filter of generate.py:44-46), each followed by one '\n' separator byte, into `out`
+ * (capacity `cap`).  kept (nullable, kmh_fasta_count bytes) receives 1/0 per record.
+ * With out == NULL only *out_len is computed. */
+int kmh_fasta_pack(const kmh_fasta* f, uint64_t min_len, uint8_t* out, uint64_t cap,
+                   uint64_t* out_len, uint8_t* kept);
+void kmh_fasta_free(kmh_fasta* f);
+
+/* ---- counting, host buffers (the drop-in path) -------------------------------- */
+/* Replaces the counting loop generate.py:36-58 for one k: counts every window of
+ * `seq` whose k bytes are all bases.  Result = distinct k-mers in FIRST-OCCURRENCE
+ * order (the insertion order of the reference's dict, which fixes the line order of
+ * k{k}.txt, generate.py:89-91), with exact counts and the first window start.
+ * 1 <= k <= 12: dense 4^k table on the GPU; 13 <= k <= 32: GPU sort + run-length.
+ * canonical != 0 counts min(forward, reverse complement) codes (not in the reference,
+ * which is forward-strand only; used for BASELINE config 5). */
+int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int canonical,
+                   kmh_kmers** out);
+uint64_t kmh_kmers_size(const kmh_kmers* r);
+/* Copy the result out; any pointer may be NULL.  codes/counts/first: size() entries. */
+int kmh_kmers_export(const kmh_kmers* r, uint64_t* codes, uint32_t* counts, uint64_t* first);
+void kmh_kmers_free(kmh_kmers* r);
+
+/* Dense 4^k count vector of one host sequence (1 <= k <= 12), counts[4^k]
+ * caller-owned.  Same counting rule as kmh_count_host. */
+int kmh_count_dense_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k,
+                         uint32_t* counts);
+
+/* ---- counting, device-resident batch (feature matrix; bench; multi-GPU) ------- */
+/* G genomes in one device buffer: genome g = d_seq[offsets[g] .. offsets[g+1]),
+ * offsets (HOST array, G+1 entries, non-decreasing) must be multiples of 16 bytes.
+ * Writes the G x 4^k u32 count matrix (row g = genome g, column = k-mer code) to
+ * d_matrix.  This is the per-rank block of the genomes x k-mers feature matrix that
+ * the reference assembles in features.py:85-117 (kmerml.ml.features.KmerFeatureBuilder)
+ * from the per-organism files; rows are all-gathered across ranks by the host. */
+int kmh_count_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets,
+                        int G, int k, uint32_t* d_matrix, void* stream);
+
+/* First window start of every k-mer per genome (0xFFFFFFFF = absent), G x 4^k u32,
+ * same layout and arguments as kmh_count_dense_dev.  Used to rebuild the
+ * first-occurrence line order of k{k}.txt. */
+int kmh_first_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets,
+                        int G, int k, uint32_t* d_first, void* stream);
+
+/* Synthetic genomes on the device: G genomes of `len` bases written
+ * at d_seq + g * stride; base i of genome g is
+ * "ACGT"[(splitmix64(s_g + (i >> 5)) >> (2 * (i & 31))) & 3] with
+ * s_g = splitmix64(seed0 + g) (seed0 = 0x6B6D65724D4C0000 for the bench genomes). */
+int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G,
+                  uint64_t seed0, void* stream);
+
+/* ---- k{k}.txt text (host) ----------------------------------------------------- */
+/* Replaces the writer loop of _save_kmers_to_file (generate.py:89-91): one line
+ * "<digits>\t<count>\n" per k-mer, digits A=0 T=1 C=2 G=3 (generate.py:71).
+ * Writes at most `cap` bytes; returns the number of bytes the full text needs (so a
+ * call with out == NULL sizes the buffer), or a negative error code. */
+int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, uint64_t n,
+                         char* out, uint64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KMERHIP_H */

@@ -1,0 +1,347 @@
+// kmh_api.cpp -- the C ABI of libkmerhip.so (include/kmerhip.h): contexts, device
+// workspace, kernel timing, and the host-buffer counting entry points that replace the
+// counting loop of /root/reference/kmerml/kmers/generate.py:36-58.
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "kmh_internal.h"
+
+struct kmh_ctx : kmh::Ctx {};
+
+struct kmh_kmers {
+    std::vector<uint64_t> codes;   // first-occurrence order
+    std::vector<uint32_t> counts;
+    std::vector<uint64_t> first;
+};
+
+namespace kmh {
+
+namespace {
+thread_local std::string t_err;
+}
+
+void set_thread_error(const std::string& msg) { t_err = msg; }
+
+int fail(Ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    else t_err = msg;
+    return code;
+}
+
+int hip_fail(Ctx* ctx, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(ctx, e == hipErrorOutOfMemory ? KMH_ERR_NOMEM : KMH_ERR_HIP, m);
+}
+
+int ensure(Ctx* ctx, DevBuf& b, size_t bytes) {
+    if (bytes <= b.bytes) return KMH_OK;
+    if (b.ptr) {
+        // the buffer may still be read by queued work on the context stream
+        KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        KMH_HIP(ctx, hipDeviceSynchronize());
+        KMH_HIP(ctx, hipFree(b.ptr));
+        b.ptr = nullptr;
+        b.bytes = 0;
+    }
+    const size_t sz = std::max<size_t>(bytes, 4096);
+    KMH_HIP(ctx, hipMalloc(&b.ptr, sz));
+    b.bytes = sz;
+    return KMH_OK;
+}
+
+int upload(Ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (ctx->pinned_ready) KMH_HIP(ctx, hipEventSynchronize(ctx->pinned_ready));
+    if (bytes > ctx->pinned_bytes) {
+        if (ctx->pinned) KMH_HIP(ctx, hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        const size_t sz = std::max<size_t>(bytes, 1 << 16);
+        KMH_HIP(ctx, hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault));
+        ctx->pinned_bytes = sz;
+    }
+    memcpy(ctx->pinned, src, bytes);
+    KMH_HIP(ctx, hipMemcpyAsync(dst, ctx->pinned, bytes, hipMemcpyHostToDevice, s));
+    if (!ctx->pinned_ready) KMH_HIP(ctx, hipEventCreateWithFlags(&ctx->pinned_ready, hipEventDisableTiming));
+    KMH_HIP(ctx, hipEventRecord(ctx->pinned_ready, s));
+    return KMH_OK;
+}
+
+static hipEvent_t take_event(Ctx* ctx) {
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void time_begin(Ctx* ctx, hipStream_t s, const char* name) {
+    if (!ctx->timing) return;
+    TimedLaunch t{name, take_event(ctx), take_event(ctx)};
+    if (t.start) (void)hipEventRecord(t.start, s);
+    ctx->launches.push_back(t);
+}
+
+void time_end(Ctx* ctx, hipStream_t s) {
+    if (!ctx->timing || ctx->launches.empty()) return;
+    TimedLaunch& t = ctx->launches.back();
+    if (t.stop) (void)hipEventRecord(t.stop, s);
+}
+
+}  // namespace kmh
+
+using kmh::fail;
+
+static hipStream_t pick_stream(kmh_ctx* ctx, void* stream) {
+    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+extern "C" {
+
+const char* kmh_version(void) { return "kmerhip 0.1.0 gfx950"; }
+
+int kmh_ctx_create(int device, kmh_ctx** out) {
+    if (!out) {
+        kmh::set_thread_error("kmh_ctx_create: out is NULL");
+        return KMH_ERR_INVALID;
+    }
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) {
+        kmh::set_thread_error(std::string("no HIP device available: ") + hipGetErrorString(e));
+        return KMH_ERR_HIP;
+    }
+    if (device < 0 || device >= ndev) {
+        kmh::set_thread_error("kmh_ctx_create: device index out of range");
+        return KMH_ERR_INVALID;
+    }
+    std::unique_ptr<kmh_ctx> c(new (std::nothrow) kmh_ctx);
+    if (!c) return KMH_ERR_NOMEM;
+    c->device = device;
+    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        kmh::set_thread_error(std::string("kmh_ctx_create: ") + hipGetErrorString(e));
+        return KMH_ERR_HIP;
+    }
+    *out = c.release();
+    return KMH_OK;
+}
+
+void kmh_ctx_destroy(kmh_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (kmh::DevBuf* b : {&ctx->seq, &ctx->suf, &ctx->toff, &ctx->meta, &ctx->out, &ctx->out2})
+        if (b->ptr) (void)hipFree(b->ptr);
+    for (auto& b : ctx->sparse)
+        if (b.ptr) (void)hipFree(b.ptr);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->pinned_ready) (void)hipEventDestroy(ctx->pinned_ready);
+    for (auto& t : ctx->launches) {
+        if (t.start) (void)hipEventDestroy(t.start);
+        if (t.stop) (void)hipEventDestroy(t.stop);
+    }
+    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* kmh_last_error(const kmh_ctx* ctx) {
+    return ctx ? ctx->err.c_str() : kmh::t_err.c_str();
+}
+
+int kmh_timing_enable(kmh_ctx* ctx, int enable) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->timing = enable != 0;
+    for (auto& t : ctx->launches) {
+        if (t.start) ctx->event_pool.push_back(t.start);
+        if (t.stop) ctx->event_pool.push_back(t.stop);
+    }
+    ctx->launches.clear();
+    return KMH_OK;
+}
+
+int kmh_timing_report(kmh_ctx* ctx, const char** names, uint64_t* launches, double* total_ms,
+                      int cap) {
+    if (!ctx) return KMH_ERR_INVALID;
+    (void)hipSetDevice(ctx->device);
+    std::map<std::string, std::pair<uint64_t, double>> acc;
+    std::vector<std::string> order;
+    for (auto& t : ctx->launches) {
+        float ms = 0.f;
+        if (t.start && t.stop) {
+            if (hipEventSynchronize(t.stop) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "timing: event sync failed");
+            (void)hipEventElapsedTime(&ms, t.start, t.stop);
+        }
+        auto it = acc.find(t.name);
+        if (it == acc.end()) {
+            order.push_back(t.name);
+            acc[t.name] = {1, (double)ms};
+        } else {
+            it->second.first += 1;
+            it->second.second += ms;
+        }
+    }
+    ctx->report_names = order;
+    const int n = (int)order.size();
+    for (int i = 0; i < n && i < cap; ++i) {
+        if (names) names[i] = ctx->report_names[i].c_str();
+        if (launches) launches[i] = acc[order[i]].first;
+        if (total_ms) total_ms[i] = acc[order[i]].second;
+    }
+    return n;
+}
+
+int kmh_count_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
+                        int k, uint32_t* d_matrix, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::dense_count(ctx, d_seq, offsets, G, k, d_matrix, pick_stream(ctx, stream));
+}
+
+int kmh_first_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
+                        int k, uint32_t* d_first, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::dense_first(ctx, d_seq, offsets, G, k, d_first, pick_stream(ctx, stream));
+}
+
+int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G,
+                  uint64_t seed0, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::synth(ctx, d_seq, len, stride, G, seed0, pick_stream(ctx, stream));
+}
+
+// Host sequence -> device (padded with one non-base byte so loads past the end are safe).
+static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t** d_seq) {
+    int rc = kmh::ensure(ctx, ctx->seq, (size_t)n + 64);
+    if (rc) return rc;
+    uint8_t* d = static_cast<uint8_t*>(ctx->seq.ptr);
+    if (n) KMH_HIP(ctx, hipMemcpyAsync(d, seq, n, hipMemcpyHostToDevice, ctx->stream));
+    KMH_HIP(ctx, hipMemsetAsync(d + n, 0, 64, ctx->stream));
+    *d_seq = d;
+    return KMH_OK;
+}
+
+int kmh_count_dense_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, uint32_t* counts) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (!counts || (n && !seq)) return fail(ctx, KMH_ERR_INVALID, "NULL argument");
+    if (k < 1 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "dense counting needs 1 <= k <= 12");
+    if (n >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "sequence must be shorter than 2^32 - 1 bytes");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    const size_t bins = (size_t)1 << (2 * k);
+    uint8_t* d_seq = nullptr;
+    int rc = stage_sequence(ctx, seq, n, &d_seq);
+    if (rc) return rc;
+    if ((rc = kmh::ensure(ctx, ctx->out, bins * sizeof(uint32_t)))) return rc;
+    const uint64_t off[2] = {0, n};
+    uint32_t* d_counts = static_cast<uint32_t*>(ctx->out.ptr);
+    if ((rc = kmh::dense_count(ctx, d_seq, off, 1, k, d_counts, ctx->stream))) return rc;
+    KMH_HIP(ctx, hipMemcpyAsync(counts, d_counts, bins * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return KMH_OK;
+}
+
+int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int canonical,
+                   kmh_kmers** out) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (!out || (n && !seq)) return fail(ctx, KMH_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (k < 1 || k > KMH_MAX_SPARSE_K)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "k must be in [1, 32] (k = " + std::to_string(k) + ")");
+    if (n >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "sequence must be shorter than 2^32 - 1 bytes");
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    std::unique_ptr<kmh_kmers> r(new (std::nothrow) kmh_kmers);
+    if (!r) return fail(ctx, KMH_ERR_NOMEM, "out of host memory");
+    uint8_t* d_seq = nullptr;
+    int rc = stage_sequence(ctx, seq, n, &d_seq);
+    if (rc) return rc;
+    try {
+        if (k <= KMH_MAX_DENSE_K && !canonical) {
+            const size_t bins = (size_t)1 << (2 * k);
+            if ((rc = kmh::ensure(ctx, ctx->out, bins * sizeof(uint32_t)))) return rc;
+            if ((rc = kmh::ensure(ctx, ctx->out2, bins * sizeof(uint32_t)))) return rc;
+            uint32_t* d_counts = static_cast<uint32_t*>(ctx->out.ptr);
+            uint32_t* d_first = static_cast<uint32_t*>(ctx->out2.ptr);
+            const uint64_t off[2] = {0, n};
+            if ((rc = kmh::dense_count(ctx, d_seq, off, 1, k, d_counts, ctx->stream))) return rc;
+            if ((rc = kmh::dense_first(ctx, d_seq, off, 1, k, d_first, ctx->stream))) return rc;
+            std::vector<uint32_t> counts(bins), first(bins);
+            KMH_HIP(ctx, hipMemcpyAsync(counts.data(), d_counts, bins * 4, hipMemcpyDeviceToHost, ctx->stream));
+            KMH_HIP(ctx, hipMemcpyAsync(first.data(), d_first, bins * 4, hipMemcpyDeviceToHost, ctx->stream));
+            KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            // First-occurrence order: every window start is the first occurrence of at
+            // most one k-mer, so scatter codes to their first position and scan.
+            std::vector<uint32_t> at(n ? n : 1, 0xFFFFFFFFu);
+            uint64_t distinct = 0;
+            for (size_t c = 0; c < bins; ++c) {
+                if (counts[c]) {
+                    if (first[c] >= n) return fail(ctx, KMH_ERR_HIP, "inconsistent first-occurrence table");
+                    at[first[c]] = (uint32_t)c;
+                    ++distinct;
+                }
+            }
+            r->codes.reserve(distinct);
+            r->counts.reserve(distinct);
+            r->first.reserve(distinct);
+            for (uint64_t p = 0; p < n; ++p) {
+                const uint32_t c = at[p];
+                if (c != 0xFFFFFFFFu) {
+                    r->codes.push_back(c);
+                    r->counts.push_back(counts[c]);
+                    r->first.push_back(p);
+                }
+            }
+            if (r->codes.size() != distinct) return fail(ctx, KMH_ERR_HIP, "duplicate first occurrence");
+        } else {
+            std::vector<uint64_t> codes, first;
+            std::vector<uint32_t> counts;
+            if ((rc = kmh::sparse_count(ctx, d_seq, n, k, canonical, codes, counts, first, ctx->stream)))
+                return rc;
+            std::vector<uint64_t> idx(codes.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+            std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return first[a] < first[b]; });
+            r->codes.resize(idx.size());
+            r->counts.resize(idx.size());
+            r->first.resize(idx.size());
+            for (size_t i = 0; i < idx.size(); ++i) {
+                r->codes[i] = codes[idx[i]];
+                r->counts[i] = counts[idx[i]];
+                r->first[i] = first[idx[i]];
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        return fail(ctx, KMH_ERR_NOMEM, "out of host memory");
+    }
+    *out = r.release();
+    return KMH_OK;
+}
+
+uint64_t kmh_kmers_size(const kmh_kmers* r) { return r ? r->codes.size() : 0; }
+
+int kmh_kmers_export(const kmh_kmers* r, uint64_t* codes, uint32_t* counts, uint64_t* first) {
+    if (!r) return KMH_ERR_INVALID;
+    const size_t n = r->codes.size();
+    if (codes && n) memcpy(codes, r->codes.data(), n * sizeof(uint64_t));
+    if (counts && n) memcpy(counts, r->counts.data(), n * sizeof(uint32_t));
+    if (first && n) memcpy(first, r->first.data(), n * sizeof(uint64_t));
+    return KMH_OK;
+}
+
+void kmh_kmers_free(kmh_kmers* r) { delete r; }
+
+}  // extern "C"

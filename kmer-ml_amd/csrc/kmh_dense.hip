@@ -1,0 +1,560 @@
+// kmh_dense.hip -- dense k-mer counting on MI355X (gfx950): 1 <= k <= 12.
+//
+// Replaces the window loop of /root/reference/kmerml/kmers/generate.py:49-58 (slide a
+// k-window over each record, drop windows with a non-ACGT byte, count) for a batch of
+// genomes resident in HBM.  Design and rooflines: DESIGN.md, "Kernels".
+//
+//   k <= 9   k_direct:     each workgroup counts a span of one genome into an LDS table
+//                          (4^k bins, or 32768-bin slices in 4^k/32768 passes for k = 8, 9)
+//                          and adds it into the genome's row.
+//   k >= 10  k_partition:  one 16384-window tile per workgroup; k-mers are bucketed by
+//                          their top 2k-15 bits with an LDS counting sort and each tile
+//                          writes its bucket-ordered 15-bit suffixes + bucket offsets.
+//            k_bucket_count: one workgroup per (genome, bucket) gathers that bucket's
+//                          segments from every tile of the genome into a 32768-bin LDS
+//                          histogram and stores the row slice once.
+//
+// Bases: A/C/G/T in either case (generate.py:41 upper()s the record; :55 keeps windows of
+// "ACGT" only).  Any other byte -- including the '\n' the host puts between records and
+// bytes past a genome's end -- breaks windows, so windows never span records or genomes.
+#include <algorithm>
+#include <cstdlib>
+
+#include "kmh_internal.h"
+
+namespace kmh {
+namespace {
+
+constexpr int kDirectThreads = kTileThreads;
+constexpr int kTargetWorkgroups = 512;
+
+struct GenomeMap {
+    const uint64_t* goff;   // genome byte offsets, G + 1 (device)
+    const uint64_t* tbase;  // cumulative tile counts, G + 1 (device), tbase[0] = 0
+    int g0, g1;             // genomes covered by this launch
+    uint64_t tile_lo;       // tbase[g0]
+};
+
+template <int K>
+constexpr int num_buckets() { return 1 << (2 * K - kSubBits); }
+
+template <int K>
+constexpr int toff_stride() { return ((num_buckets<K>() + 1 + 7) / 8) * 8; }
+
+// Largest g in [g0, g1) with tbase[g] <= gt (genomes without tiles are skipped).
+__device__ __forceinline__ int find_genome(const GenomeMap& m, uint64_t gt) {
+    int lo = m.g0, hi = m.g1 - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (m.tbase[mid] <= gt) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// 16 bytes at pos; bytes at or past `end` read as 0 (not a base).
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ seq, uint64_t pos,
+                                        uint64_t end) {
+    if (pos + 16 <= end) return *reinterpret_cast<const uint4*>(seq + pos);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (pos + i < end) w[i >> 2] |= (uint32_t)seq[pos + i] << (8 * (i & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Four ASCII bytes (byte 0 first) -> 8 bits of 2-bit codes (byte 0 in bits 7:6) and a
+// 4-bit invalid mask (byte 0 in bit 3).  code = ((c >> 1) ^ (c >> 2)) & 3 maps A/a->0,
+// C/c->1, G/g->2, T/t->3; a byte is a base iff (c & 0xDF) == "ACGT"[code].
+__device__ __forceinline__ void enc4(uint32_t w, uint32_t& c8, uint32_t& i4) {
+    const uint32_t cb = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
+    const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, cb);  // "ACGT"[cb]
+    const uint32_t e = (w & 0xDFDFDFDFu) ^ expect;                       // 0 byte = base
+    const uint32_t nz = (((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e) & 0x80808080u;
+    i4 = ((nz >> 7) * 0x08040201u) >> 24;
+    c8 = (cb * 0x40100401u) >> 24;
+}
+
+// 16 bytes -> 32-bit code word (first base in bits 31:30) + 16-bit invalid mask (first
+// base in bit 15).
+__device__ __forceinline__ void enc16(uint4 v, uint32_t& code, uint32_t& inv) {
+    uint32_t c0, c1, c2, c3, i0, i1, i2, i3;
+    enc4(v.x, c0, i0);
+    enc4(v.y, c1, i1);
+    enc4(v.z, c2, i2);
+    enc4(v.w, c3, i3);
+    code = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
+    inv = (i0 << 12) | (i1 << 8) | (i2 << 4) | i3;
+}
+
+// Visit the 32 windows that start at tstart + 32 * threadIdx.x + j, j = 0..31, of a
+// kTileThreads-thread workgroup: f(j, code, is_valid).  The k - 1 <= 15 bases past a
+// thread's 32 come from the next lane's first 16 (lane 63 loads them).
+template <int K, typename F>
+__device__ __forceinline__ void walk_tile(const uint8_t* __restrict__ seq, uint64_t tstart,
+                                          uint64_t gend, F&& f) {
+    static_assert(K >= 1 && K <= 16, "dense windows need k <= 16");
+    const int lane = threadIdx.x & 63;
+    const uint64_t base = tstart + (uint64_t)threadIdx.x * kTileBpt;
+    uint32_t cA, iA, cB, iB;
+    enc16(load16(seq, base, gend), cA, iA);
+    enc16(load16(seq, base + 16, gend), cB, iB);
+    uint32_t cN = __shfl_down(cA, 1);
+    uint32_t iN = __shfl_down(iA, 1);
+    if (lane == 63) enc16(load16(seq, base + 32, gend), cN, iN);
+    constexpr uint32_t KM = (K == 16) ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
+    constexpr uint32_t VM = (1u << K) - 1u;
+    const uint64_t wAB = ((uint64_t)cA << 32) | cB;
+    const uint32_t vAB = (iA << 16) | iB;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t code = (uint32_t)(wAB >> (64 - 2 * (j + K))) & KM;
+        f(j, code, ((vAB >> (32 - (j + K))) & VM) == 0u);
+    }
+    const uint64_t wBN = ((uint64_t)cB << 32) | cN;
+    const uint32_t vBN = (iB << 16) | iN;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t code = (uint32_t)(wBN >> (64 - 2 * (j + K))) & KM;
+        f(16 + j, code, ((vBN >> (32 - (j + K))) & VM) == 0u);
+    }
+}
+
+// XCD-aware work order: blocks b and b+8 share an XCD under the observed round-robin
+// placement, so hand each XCD a contiguous range of work items (speed only).
+__device__ __forceinline__ uint32_t xcd_work_id() {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    return (nb % 8u == 0u) ? (b % 8u) * (nb / 8u) + b / 8u : b;
+}
+
+// ---------------------------------------------------------------- k <= 9: direct
+template <int K>
+__global__ __launch_bounds__(kDirectThreads) void k_direct(const uint8_t* __restrict__ seq,
+                                                           GenomeMap m, int S,
+                                                           uint32_t* __restrict__ out) {
+    constexpr uint32_t BINS = 1u << (2 * K);
+    constexpr uint32_t SLICE = BINS < (uint32_t)kSubBins ? BINS : (uint32_t)kSubBins;
+    constexpr int NPASS = (int)(BINS / SLICE);
+    constexpr int REP0 = (int)(16384u / SLICE);  // replicas that fit in 64 KiB
+    constexpr int REP = REP0 < 1 ? 1 : (REP0 > 8 ? 8 : REP0);
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[REP * SLICE];
+
+    const uint32_t w = xcd_work_id();
+    const int gl = (int)(w / (uint32_t)S), s = (int)(w % (uint32_t)S);
+    const int g = m.g0 + gl;
+    const uint64_t gs = m.goff[g], ge = m.goff[g + 1];
+    const uint64_t nt = m.tbase[g + 1] - m.tbase[g];
+    const uint64_t ta = nt * (uint64_t)s / (uint64_t)S, tb = nt * (uint64_t)(s + 1) / (uint64_t)S;
+    uint32_t* tab = tbl + ((threadIdx.x >> 6) % REP) * SLICE;
+    uint32_t* orow = out + (uint64_t)g * BINS;
+
+    for (int p = 0; p < NPASS; ++p) {
+        for (uint32_t i = threadIdx.x; i < REP * SLICE; i += kDirectThreads) tbl[i] = 0u;
+        __syncthreads();
+        for (uint64_t t = ta; t < tb; ++t) {
+            walk_tile<K>(seq, gs + t * (uint64_t)kTile, ge, [&](int, uint32_t code, bool ok) {
+                if (NPASS == 1) {
+                    if (ok) atomicAdd(&tab[code], 1u);
+                } else if (ok && (code / SLICE) == (uint32_t)p) {
+                    atomicAdd(&tab[code % SLICE], 1u);
+                }
+            });
+        }
+        __syncthreads();
+        if (ta < tb) {
+            for (uint32_t i = threadIdx.x; i < SLICE; i += kDirectThreads) {
+                uint32_t v = 0u;
+#pragma unroll
+                for (int r = 0; r < REP; ++r) v += tbl[r * SLICE + i];
+                if (v) atomicAdd(&orow[(uint64_t)p * SLICE + i], v);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- k >= 10: partition
+template <int K>
+__global__ __launch_bounds__(kTileThreads) void k_partition(const uint8_t* __restrict__ seq,
+                                                            GenomeMap m,
+                                                            uint16_t* __restrict__ suf,
+                                                            uint16_t* __restrict__ toff) {
+    constexpr int NBK = num_buckets<K>();
+    constexpr int TS = toff_stride<K>();
+    static_assert(NBK <= kTileThreads, "one scan element per thread");
+    __shared__ __attribute__((aligned(16))) uint16_t sorted[kTile];
+    __shared__ uint32_t cnt[NBK];
+    __shared__ uint32_t cur[NBK];
+    __shared__ uint32_t wsum[kTileThreads / 64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = blockIdx.x;
+    const uint64_t gt = m.tile_lo + lt;
+    const int g = find_genome(m, gt);
+    const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)kTile;
+    const uint64_t ge = m.goff[g + 1];
+
+    for (int b = tid; b < NBK; b += kTileThreads) cnt[b] = 0u;
+    __syncthreads();
+
+    uint32_t km[kTileBpt];
+    walk_tile<K>(seq, tstart, ge, [&](int j, uint32_t code, bool ok) {
+        km[j] = ok ? code : 0xFFFFFFFFu;
+        if (ok) atomicAdd(&cnt[code >> kSubBits], 1u);
+    });
+    __syncthreads();
+
+    // Exclusive scan of the bucket histogram -> bucket starts.
+    const uint32_t v = tid < NBK ? cnt[tid] : 0u;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t pre = 0u, total = 0u;
+#pragma unroll
+    for (int w = 0; w < kTileThreads / 64; ++w) {
+        pre += (w < wave) ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    uint16_t* trow = toff + lt * (uint64_t)TS;
+    if (tid < NBK) {
+        cur[tid] = pre + incl - v;
+        trow[tid] = (uint16_t)(pre + incl - v);
+    }
+    if (tid == 0) trow[NBK] = (uint16_t)total;
+    __syncthreads();
+
+    // Scatter 15-bit suffixes into bucket order.
+#pragma unroll
+    for (int j = 0; j < kTileBpt; ++j) {
+        const uint32_t c = km[j];
+        if (c != 0xFFFFFFFFu) {
+            const uint32_t slot = atomicAdd(&cur[c >> kSubBits], 1u);
+            sorted[slot] = (uint16_t)(c & (kSubBins - 1));
+        }
+    }
+    __syncthreads();
+
+    uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)kTile);
+    const uint4* src = reinterpret_cast<const uint4*>(sorted);
+    const uint32_t nchunk = (total + 7u) >> 3;
+    for (uint32_t c = tid; c < nchunk; c += kTileThreads) dst[c] = src[c];
+}
+
+template <int K, int GS>
+__global__ __launch_bounds__(kCountThreads) void k_bucket_count(
+    const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, GenomeMap m, int S,
+    uint32_t* __restrict__ out) {
+    constexpr int NBK = num_buckets<K>();
+    constexpr int TS = toff_stride<K>();
+    constexpr int NGRP = kCountThreads / GS;
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[kSubBins];
+
+    const uint32_t w = xcd_work_id();
+    const int s = (int)(w % (uint32_t)S);
+    const uint32_t b = (w / (uint32_t)S) % NBK;
+    const int g = m.g0 + (int)(w / ((uint32_t)S * NBK));
+    const uint64_t t0 = m.tbase[g] - m.tile_lo, nt = m.tbase[g + 1] - m.tbase[g];
+    const uint64_t ta = t0 + nt * (uint64_t)s / (uint64_t)S;
+    const uint64_t tb = t0 + nt * (uint64_t)(s + 1) / (uint64_t)S;
+
+    uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
+    for (int i = threadIdx.x; i < kSubBins / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+
+    const int grp = threadIdx.x / GS, r = threadIdx.x % GS;
+    for (uint64_t t = ta + grp; t < tb; t += NGRP) {
+        const uint16_t* row = toff + t * (uint64_t)TS;
+        const uint32_t s0 = row[b], e0 = row[b + 1];
+        const uint16_t* p = suf + t * (uint64_t)kTile;
+        for (uint32_t c = (s0 & ~7u) + (uint32_t)r * 8u; c < e0; c += GS * 8u) {
+            const uint4 q = *reinterpret_cast<const uint4*>(p + c);
+            const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t idx = c + (uint32_t)i;
+                if (idx >= s0 && idx < e0) atomicAdd(&tbl[(wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu], 1u);
+            }
+        }
+    }
+    __syncthreads();
+
+    uint32_t* orow = out + (uint64_t)g * (1ull << (2 * K)) + (uint64_t)b * kSubBins;
+    if (S == 1) {
+        uint4* o4 = reinterpret_cast<uint4*>(orow);
+        for (int i = threadIdx.x; i < kSubBins / 4; i += kCountThreads) o4[i] = tbl4[i];
+    } else if (ta < tb) {
+        for (int i = threadIdx.x; i < kSubBins; i += kCountThreads) {
+            const uint32_t x = tbl[i];
+            if (x) atomicAdd(&orow[i], x);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- first occurrence
+template <int K>
+__global__ __launch_bounds__(kTileThreads) void k_first(const uint8_t* __restrict__ seq,
+                                                        GenomeMap m,
+                                                        uint32_t* __restrict__ first) {
+    const uint64_t gt = m.tile_lo + blockIdx.x;
+    const int g = find_genome(m, gt);
+    const uint64_t gs = m.goff[g];
+    const uint64_t rel = (gt - m.tbase[g]) * (uint64_t)kTile + (uint64_t)threadIdx.x * kTileBpt;
+    uint32_t* frow = first + (uint64_t)g * (1ull << (2 * K));
+    walk_tile<K>(seq, gs + (gt - m.tbase[g]) * (uint64_t)kTile, m.goff[g + 1],
+                 [&](int j, uint32_t code, bool ok) {
+                     if (ok) atomicMin(&frow[code], (uint32_t)(rel + (uint64_t)j));
+                 });
+}
+
+// ---------------------------------------------------------------- synthetic genomes
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, uint64_t len,
+                                               uint64_t stride, uint64_t seed0, int G) {
+    const uint64_t wpg = (len + 31) / 32;
+    const uint64_t total = wpg * (uint64_t)G;
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = idx / wpg, wi = idx % wpg;
+        const uint64_t r = splitmix64(splitmix64(seed0 + g) + wi);
+        uint8_t* dst = out + g * stride + wi * 32;
+        if (wi * 32 + 32 <= len && ((uintptr_t)dst & 15u) == 0u) {
+            uint32_t q[8];
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                const uint32_t x = (uint32_t)(r >> (8 * d)) & 0xFFu;
+                const uint32_t sel = (x | (x << 6) | (x << 12) | (x << 18)) & 0x03030303u;
+                q[d] = __builtin_amdgcn_perm(0u, 0x54474341u, sel);
+            }
+            reinterpret_cast<uint4*>(dst)[0] = make_uint4(q[0], q[1], q[2], q[3]);
+            reinterpret_cast<uint4*>(dst)[1] = make_uint4(q[4], q[5], q[6], q[7]);
+        } else {
+            for (int i = 0; i < 32 && wi * 32 + i < len; ++i)
+                dst[i] = "ACGT"[(r >> (2 * i)) & 3u];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- host side
+struct Layout {
+    std::vector<uint64_t> goff, tbase;
+    uint64_t ntiles = 0;
+};
+
+int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, Layout& L) {
+    if (G < 1) return fail(ctx, KMH_ERR_INVALID, "G must be >= 1");
+    if (!offsets) return fail(ctx, KMH_ERR_INVALID, "offsets is NULL");
+    L.goff.assign(offsets, offsets + G + 1);
+    L.tbase.assign(G + 1, 0);
+    for (int g = 0; g < G; ++g) {
+        const uint64_t a = offsets[g], b = offsets[g + 1];
+        if (b < a) return fail(ctx, KMH_ERR_INVALID, "offsets must be non-decreasing");
+        if (a % 16 != 0) return fail(ctx, KMH_ERR_INVALID, "genome start offsets must be multiples of 16");
+        if (b - a >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "a genome must be shorter than 2^32 - 1 bytes");
+        const uint64_t nwin = (b - a >= (uint64_t)k) ? (b - a - (uint64_t)k + 1) : 0;
+        L.tbase[g + 1] = L.tbase[g] + (nwin + kTile - 1) / kTile;
+    }
+    L.ntiles = L.tbase[G];
+    return KMH_OK;
+}
+
+int upload_layout(Ctx* ctx, const Layout& L, hipStream_t s, const uint64_t** d_goff,
+                  const uint64_t** d_tbase) {
+    const size_t n = L.goff.size();
+    int rc = ensure(ctx, ctx->meta, 2 * n * sizeof(uint64_t));
+    if (rc) return rc;
+    std::vector<uint64_t> both(2 * n);
+    std::copy(L.goff.begin(), L.goff.end(), both.begin());
+    std::copy(L.tbase.begin(), L.tbase.end(), both.begin() + n);
+    rc = upload(ctx, ctx->meta.ptr, both.data(), both.size() * sizeof(uint64_t), s);
+    if (rc) return rc;
+    *d_goff = static_cast<const uint64_t*>(ctx->meta.ptr);
+    *d_tbase = *d_goff + n;
+    return KMH_OK;
+}
+
+size_t env_mb(const char* name, size_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    const long x = std::atol(v);
+    return x > 0 ? (size_t)x : dflt;
+}
+
+template <int K>
+int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
+               const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
+    const size_t row = (size_t)1 << (2 * K);
+    KMH_HIP(ctx, hipMemsetAsync(d_out, 0, row * (size_t)G * sizeof(uint32_t), s));
+    // Spans per genome: fill ~kTargetWorkgroups*2 workgroups, at most one per tile.
+    uint64_t maxt = 0;
+    for (int g = 0; g < G; ++g) maxt = std::max<uint64_t>(maxt, L.tbase[g + 1] - L.tbase[g]);
+    if (maxt == 0) return KMH_OK;
+    const uint64_t want = (2 * (uint64_t)kTargetWorkgroups + G - 1) / G;
+    const int S = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, maxt));
+    GenomeMap m{d_goff, d_tbase, 0, G, 0};
+    time_begin(ctx, s, "k_direct");
+    hipLaunchKernelGGL(k_direct<K>, dim3((unsigned)(G * S)), dim3(kDirectThreads), 0, s, d_seq,
+                       m, S, d_out);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+template <int K>
+int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
+                    const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
+    constexpr int NBK = num_buckets<K>();
+    constexpr int TS = toff_stride<K>();
+    constexpr int GS0 = kTile / NBK / 8;
+    constexpr int GS = GS0 < 1 ? 1 : (GS0 > 64 ? 64 : GS0);
+    const size_t row = (size_t)1 << (2 * K);
+    // Genomes per batch: keep the suffix buffer of one batch within the budget (it is
+    // written and re-read, so a budget inside the 256 MiB Infinity Cache can keep it
+    // on-die).  KMH_SUF_BUDGET_MB overrides.
+    const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 256) << 20;
+    const size_t tile_bytes = (size_t)kTile * sizeof(uint16_t);
+    uint64_t max_batch_tiles = 0;
+    {
+        int g = 0;
+        while (g < G) {
+            int h = g;
+            uint64_t tiles = 0;
+            do {
+                tiles += L.tbase[h + 1] - L.tbase[h];
+                ++h;
+            } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget);
+            max_batch_tiles = std::max(max_batch_tiles, tiles);
+            g = h;
+        }
+    }
+    int rc = ensure(ctx, ctx->suf, std::max<uint64_t>(max_batch_tiles, 1) * tile_bytes);
+    if (rc) return rc;
+    rc = ensure(ctx, ctx->toff, std::max<uint64_t>(max_batch_tiles, 1) * TS * sizeof(uint16_t));
+    if (rc) return rc;
+    uint16_t* suf = static_cast<uint16_t*>(ctx->suf.ptr);
+    uint16_t* toff = static_cast<uint16_t*>(ctx->toff.ptr);
+
+    int g = 0;
+    while (g < G) {
+        int h = g;
+        uint64_t tiles = 0;
+        do {
+            tiles += L.tbase[h + 1] - L.tbase[h];
+            ++h;
+        } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget);
+        const int nG = h - g;
+        GenomeMap m{d_goff, d_tbase, g, h, L.tbase[g]};
+        uint64_t maxt = 0;
+        for (int q = g; q < h; ++q) maxt = std::max<uint64_t>(maxt, L.tbase[q + 1] - L.tbase[q]);
+        const uint64_t want = ((uint64_t)kTargetWorkgroups + (uint64_t)nG * NBK - 1) / ((uint64_t)nG * NBK);
+        const int S = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxt, 1)));
+        if (S > 1) KMH_HIP(ctx, hipMemsetAsync(d_out + (size_t)g * row, 0, (size_t)nG * row * sizeof(uint32_t), s));
+        if (tiles) {
+            time_begin(ctx, s, "k_partition");
+            hipLaunchKernelGGL(k_partition<K>, dim3((unsigned)tiles), dim3(kTileThreads), 0, s,
+                               d_seq, m, suf, toff);
+            time_end(ctx, s);
+            KMH_HIP(ctx, hipGetLastError());
+        }
+        time_begin(ctx, s, "k_bucket_count");
+        hipLaunchKernelGGL((k_bucket_count<K, GS>), dim3((unsigned)(nG * NBK * S)),
+                           dim3(kCountThreads), 0, s, suf, toff, m, S, d_out);
+        time_end(ctx, s);
+        KMH_HIP(ctx, hipGetLastError());
+        g = h;
+    }
+    return KMH_OK;
+}
+
+template <int K>
+int count_k(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
+            const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
+    if constexpr (K <= 9) return run_direct<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+    else return run_partitioned<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+}
+
+template <int K>
+int first_k(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
+            const uint64_t* d_tbase, int G, uint32_t* d_first, hipStream_t s) {
+    const size_t row = (size_t)1 << (2 * K);
+    KMH_HIP(ctx, hipMemsetAsync(d_first, 0xFF, row * (size_t)G * sizeof(uint32_t), s));
+    if (L.ntiles == 0) return KMH_OK;
+    GenomeMap m{d_goff, d_tbase, 0, G, 0};
+    time_begin(ctx, s, "k_first");
+    hipLaunchKernelGGL(k_first<K>, dim3((unsigned)L.ntiles), dim3(kTileThreads), 0, s, d_seq, m,
+                       d_first);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+#define KMH_DISPATCH_K(fn, k, ...)                      \
+    switch (k) {                                        \
+    case 1: return fn<1>(__VA_ARGS__);                  \
+    case 2: return fn<2>(__VA_ARGS__);                  \
+    case 3: return fn<3>(__VA_ARGS__);                  \
+    case 4: return fn<4>(__VA_ARGS__);                  \
+    case 5: return fn<5>(__VA_ARGS__);                  \
+    case 6: return fn<6>(__VA_ARGS__);                  \
+    case 7: return fn<7>(__VA_ARGS__);                  \
+    case 8: return fn<8>(__VA_ARGS__);                  \
+    case 9: return fn<9>(__VA_ARGS__);                  \
+    case 10: return fn<10>(__VA_ARGS__);                \
+    case 11: return fn<11>(__VA_ARGS__);                \
+    case 12: return fn<12>(__VA_ARGS__);                \
+    default: break;                                     \
+    }
+
+}  // namespace
+
+int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                uint32_t* d_out, hipStream_t s) {
+    if (k < 1 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "dense counting needs 1 <= k <= 12");
+    if (!d_seq || !d_out) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    Layout L;
+    int rc = make_layout(ctx, offsets, G, k, L);
+    if (rc) return rc;
+    const uint64_t *d_goff, *d_tbase;
+    rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+    if (rc) return rc;
+    KMH_DISPATCH_K(count_k, k, ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+    return fail(ctx, KMH_ERR_UNSUPPORTED, "unsupported k");
+}
+
+int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                uint32_t* d_first, hipStream_t s) {
+    if (k < 1 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "dense counting needs 1 <= k <= 12");
+    if (!d_seq || !d_first) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    Layout L;
+    int rc = make_layout(ctx, offsets, G, k, L);
+    if (rc) return rc;
+    const uint64_t *d_goff, *d_tbase;
+    rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+    if (rc) return rc;
+    KMH_DISPATCH_K(first_k, k, ctx, d_seq, L, d_goff, d_tbase, G, d_first, s);
+    return fail(ctx, KMH_ERR_UNSUPPORTED, "unsupported k");
+}
+
+int synth(Ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G, uint64_t seed0,
+          hipStream_t s) {
+    if (!d_seq || G < 1 || stride < len) return fail(ctx, KMH_ERR_INVALID, "bad synth arguments");
+    const uint64_t words = (len + 31) / 32 * (uint64_t)G;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((words + 255) / 256, 65536);
+    if (blocks == 0) return KMH_OK;
+    time_begin(ctx, s, "k_synth");
+    hipLaunchKernelGGL(k_synth, dim3(blocks), dim3(256), 0, s, d_seq, len, stride, seed0, G);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+}  // namespace kmh

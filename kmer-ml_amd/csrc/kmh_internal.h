@@ -1,0 +1,90 @@
+// Internal declarations shared by the host runtime (kmh_api.cpp, kmh_fasta.cpp) and the
+// HIP translation units (kmh_dense.hip, kmh_sparse.hip).  Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/kmerhip.h"
+
+namespace kmh {
+
+// Geometry of the dense path ("Kernels").
+constexpr int kTileThreads = 512;                      // threads of a tile workgroup
+constexpr int kTileBpt = 32;                           // window starts per thread
+constexpr int kTile = kTileThreads * kTileBpt;         // 16384 window starts per tile
+constexpr int kSubBits = 15;                           // bins owned by one count workgroup
+constexpr int kSubBins = 1 << kSubBits;                // 32768 u32 = 128 KiB of LDS
+constexpr int kCountThreads = 1024;                    // threads of a bucket-count workgroup
+constexpr int kDirectMaxK = 7;                         // k <= 7: whole table in LDS
+
+// A growable device allocation owned by a context.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct TimedLaunch {
+    const char* name;
+    hipEvent_t start;
+    hipEvent_t stop;
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // device workspace
+    DevBuf seq, suf, toff, meta, out, out2, sparse[8];
+    // pinned staging for small host->device tables
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
+    hipEvent_t pinned_ready = nullptr;
+    // per-kernel timing
+    bool timing = false;
+    std::vector<TimedLaunch> launches;
+    std::vector<hipEvent_t> event_pool;
+    std::vector<std::string> report_names;
+};
+
+// Error helpers: set ctx->err (or the thread-local message when ctx == nullptr).
+int fail(Ctx* ctx, int code, const std::string& msg);
+int hip_fail(Ctx* ctx, hipError_t e, const char* what);
+void set_thread_error(const std::string& msg);
+
+#define KMH_HIP(ctx, call)                                   \
+    do {                                                     \
+        hipError_t e_ = (call);                              \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
+    } while (0)
+
+// Grow-only device buffer.
+int ensure(Ctx* ctx, DevBuf& b, size_t bytes);
+// Copy a small host table to device through the pinned staging buffer (async on s).
+int upload(Ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s);
+
+// Kernel timing brackets (no-ops unless ctx->timing).
+void time_begin(Ctx* ctx, hipStream_t s, const char* name);
+void time_end(Ctx* ctx, hipStream_t s);
+
+// ---- dense path (kmh_dense.hip) ----
+// offsets: host, G+1 entries.  d_out: G x 4^k u32.
+int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                uint32_t* d_out, hipStream_t s);
+int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                uint32_t* d_first, hipStream_t s);
+int synth(Ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G, uint64_t seed0,
+          hipStream_t s);
+
+// ---- sparse path (kmh_sparse.hip) ----
+// Counts the windows of d_seq[0, n) for 13 <= k <= 32 (works for any 1 <= k <= 32).
+// On return the host vectors hold the distinct codes in ascending order, their counts
+// and their first window start.
+int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
+                 std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
+                 std::vector<uint64_t>& first, hipStream_t s);
+
+}  // namespace kmh

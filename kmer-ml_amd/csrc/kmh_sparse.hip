@@ -1,0 +1,143 @@
+// kmh_sparse.hip -- sorted sparse k-mer counting for 13 <= k <= 32 on MI355X.
+//
+// Replaces generate.py:49-58 for k where a dense 4^k table is impractical (the
+// reference's dict is a hash table, generate.py:36,58).  Every valid window emits its
+// 2k-bit code and start position; the pairs are compacted, radix-sorted by code (stable,
+// so equal codes keep ascending positions), and run-length encoded: each run gives one
+// distinct k-mer, its count and its first position.  canonical != 0 emits
+// min(forward, reverse complement) (BASELINE config 5; not a reference feature).
+#include <hipcub/hipcub.hpp>
+
+#include "kmh_internal.h"
+
+namespace kmh {
+namespace {
+
+__device__ __forceinline__ int base_code(uint8_t c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return -1;
+    }
+}
+
+// One thread per window start.  The k <= 32 bytes of a window are read byte-wise; the
+// vector L1 serves the 32x overlap between neighbouring threads.
+__global__ __launch_bounds__(256) void k_window_codes(const uint8_t* __restrict__ seq,
+                                                      uint64_t nwin, int k, int canonical,
+                                                      uint64_t* __restrict__ codes,
+                                                      uint8_t* __restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nwin) return;
+    uint64_t fwd = 0, rc = 0;
+    bool ok = true;
+    for (int j = 0; j < k; ++j) {
+        const int b = base_code(seq[i + j]);
+        ok &= b >= 0;
+        const uint64_t bb = (uint64_t)(b & 3);
+        fwd = (fwd << 2) | bb;
+        rc |= (3ull - bb) << (2 * j);
+    }
+    codes[i] = (canonical && rc < fwd) ? rc : fwd;
+    flags[i] = ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_run_first(const uint32_t* __restrict__ pos_sorted,
+                                                   const uint32_t* __restrict__ run_start,
+                                                   const uint64_t* __restrict__ nruns,
+                                                   uint64_t* __restrict__ first) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < *nruns) first[r] = pos_sorted[run_start[r]];
+}
+
+void* carve(char*& p, size_t bytes) {
+    void* r = p;
+    p += (bytes + 255) & ~(size_t)255;
+    return r;
+}
+
+}  // namespace
+
+int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
+                 std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
+                 std::vector<uint64_t>& first, hipStream_t s) {
+    codes.clear();
+    counts.clear();
+    first.clear();
+    if (k < 1 || k > KMH_MAX_SPARSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "sparse counting needs 1 <= k <= 32");
+    if (n >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "sequence must be shorter than 2^32 - 1 bytes");
+    if (n < (uint64_t)k) return KMH_OK;
+    const uint64_t nwin = n - (uint64_t)k + 1;
+    const int N = (int)nwin;  // hipcub item counts are int here; n < 2^31 enforced below
+    if (nwin > 0x7FFFFFFFull) return fail(ctx, KMH_ERR_UNSUPPORTED, "sparse path supports < 2^31 windows per call");
+
+    // Scratch sizes of the hipcub passes.
+    size_t t_sel = 0, t_sort = 0, t_rle = 0, t_scan = 0;
+    uint64_t *kin = nullptr, *kout = nullptr, *nsel = nullptr;
+    uint32_t *vin = nullptr, *vout = nullptr;
+    uint8_t* flags = nullptr;
+    hipcub::CountingInputIterator<uint32_t> iota(0u);
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(nullptr, t_sel, kin, flags, kout, nsel, N, s));
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, kin, kout, vin, vout, N, 0, 2 * k, s));
+    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, kin, kout, vin, nsel, N, s));
+    KMH_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, vin, vout, N, s));
+    const size_t temp = std::max(std::max(t_sel, t_sort), std::max(t_rle, t_scan));
+
+    const size_t bytes = 4 * (((size_t)nwin * 8 + 255) & ~(size_t)255) +
+                         3 * (((size_t)nwin * 4 + 255) & ~(size_t)255) +
+                         (((size_t)nwin + 255) & ~(size_t)255) + temp + 4096;
+    int rc = ensure(ctx, ctx->sparse[0], bytes);
+    if (rc) return rc;
+    char* p = static_cast<char*>(ctx->sparse[0].ptr);
+    uint64_t* codes_all = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* keys_a = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* keys_b = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* first_d = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint32_t* pos_a = static_cast<uint32_t*>(carve(p, nwin * 4));
+    uint32_t* pos_b = static_cast<uint32_t*>(carve(p, nwin * 4));
+    uint32_t* cnt_d = static_cast<uint32_t*>(carve(p, nwin * 4));
+    flags = static_cast<uint8_t*>(carve(p, nwin));
+    uint64_t* small = static_cast<uint64_t*>(carve(p, 64));
+    void* tmp = carve(p, temp);
+    uint64_t* nvalid_d = small;
+    uint64_t* nruns_d = small + 1;
+
+    time_begin(ctx, s, "k_window_codes");
+    hipLaunchKernelGGL(k_window_codes, dim3((unsigned)((nwin + 255) / 256)), dim3(256), 0, s,
+                       d_seq, nwin, k, canonical, codes_all, flags);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    size_t t = temp;
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(tmp, t, codes_all, flags, keys_a, nvalid_d, N, s));
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(tmp, t, iota, flags, pos_a, nvalid_d, N, s));
+    uint64_t nvalid = 0;
+    KMH_HIP(ctx, hipMemcpyAsync(&nvalid, nvalid_d, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    if (nvalid == 0) return KMH_OK;
+    const int M = (int)nvalid;
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t, keys_a, keys_b, pos_a, pos_b, M, 0, 2 * k, s));
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(tmp, t, keys_b, keys_a, cnt_d, nruns_d, M, s));
+    uint64_t nruns = 0;
+    KMH_HIP(ctx, hipMemcpyAsync(&nruns, nruns_d, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceScan::ExclusiveSum(tmp, t, cnt_d, pos_a, (int)nruns, s));
+    hipLaunchKernelGGL(k_run_first, dim3((unsigned)((nruns + 255) / 256)), dim3(256), 0, s,
+                       pos_b, pos_a, nruns_d, first_d);
+    KMH_HIP(ctx, hipGetLastError());
+    codes.resize(nruns);
+    counts.resize(nruns);
+    first.resize(nruns);
+    KMH_HIP(ctx, hipMemcpyAsync(codes.data(), keys_a, nruns * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(counts.data(), cnt_d, nruns * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(first.data(), first_d, nruns * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    return KMH_OK;
+}
+
+}  // namespace kmh

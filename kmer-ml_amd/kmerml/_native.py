@@ -1,0 +1,261 @@
+"""ctypes binding to libkmerhip.so (the C ABI declared in include/kmerhip.h).
+
+There is no CPU fallback: if the library or a HIP device is missing, every counting
+call raises.  ctypes releases the GIL for the duration of each foreign call.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkmerhip.so")
+
+KMH_OK = 0
+KMH_ERR_INVALID = -1
+KMH_ERR_HIP = -2
+KMH_ERR_NOMEM = -3
+KMH_ERR_UNSUPPORTED = -4
+KMH_ERR_IO = -5
+MAX_DENSE_K = 12
+MAX_SPARSE_K = 32
+
+_c = ctypes
+_vp = _c.c_void_p
+_u64 = _c.c_uint64
+_u64p = _c.POINTER(_c.c_uint64)
+
+# (name, restype, argtypes) for every symbol of include/kmerhip.h
+SIGNATURES = [
+    ("kmh_version", _c.c_char_p, []),
+    ("kmh_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_vp)]),
+    ("kmh_ctx_destroy", None, [_vp]),
+    ("kmh_last_error", _c.c_char_p, [_vp]),
+    ("kmh_timing_enable", _c.c_int, [_vp, _c.c_int]),
+    ("kmh_timing_report", _c.c_int, [_vp, _c.POINTER(_c.c_char_p), _u64p,
+                                     _c.POINTER(_c.c_double), _c.c_int]),
+    ("kmh_fasta_read", _c.c_int, [_c.c_char_p, _c.POINTER(_vp)]),
+    ("kmh_fasta_count", _u64, [_vp]),
+    ("kmh_fasta_record", _c.c_int, [_vp, _u64, _c.POINTER(_c.c_char_p), _u64p,
+                                    _c.POINTER(_vp), _u64p, _u64p]),
+    ("kmh_fasta_pack", _c.c_int, [_vp, _u64, _vp, _u64, _u64p, _vp]),
+    ("kmh_fasta_free", None, [_vp]),
+    ("kmh_count_host", _c.c_int, [_vp, _vp, _u64, _c.c_int, _c.c_int, _c.POINTER(_vp)]),
+    ("kmh_kmers_size", _u64, [_vp]),
+    ("kmh_kmers_export", _c.c_int, [_vp, _vp, _vp, _vp]),
+    ("kmh_kmers_free", None, [_vp]),
+    ("kmh_count_dense_host", _c.c_int, [_vp, _vp, _u64, _c.c_int, _vp]),
+    ("kmh_count_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
+    ("kmh_first_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
+    ("kmh_synth_dev", _c.c_int, [_vp, _vp, _u64, _u64, _c.c_int, _u64, _vp]),
+    ("kmh_format_lines", _c.c_int64, [_c.c_int, _vp, _vp, _u64, _vp, _u64]),
+]
+
+_lib = None
+_lock = threading.Lock()
+_contexts = {}
+
+
+class KmhError(RuntimeError):
+    """A libkmerhip call failed; ``code`` is the KMH_ERR_* value."""
+
+    def __init__(self, code, message):
+        super().__init__(f"libkmerhip error {code}: {message}")
+        self.code = code
+
+
+def lib():
+    """Load libkmerhip.so (raises ImportError if it was not built)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(f"libkmerhip.so not found at {LIB_PATH}; build it with `make lib` "
+                                      "(the k-mer path has no CPU fallback)")
+                L = ctypes.CDLL(LIB_PATH)
+                for name, res, args in SIGNATURES:
+                    fn = getattr(L, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = L
+    return _lib
+
+
+def _check(rc, ctx=None):
+    if rc < 0:
+        msg = lib().kmh_last_error(ctx)
+        msg = msg.decode(errors="replace") if msg else ""
+        if rc == KMH_ERR_UNSUPPORTED:
+            raise NotImplementedError(msg)
+        if rc == KMH_ERR_INVALID:
+            raise ValueError(msg)
+        if rc == KMH_ERR_IO:
+            raise OSError(msg)
+        if rc == KMH_ERR_NOMEM:
+            raise MemoryError(msg)
+        raise KmhError(rc, msg)
+    return rc
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Context:
+    """A libkmerhip context bound to one HIP device (kmh_ctx_create)."""
+
+    def __init__(self, device=0):
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        _check(lib().kmh_ctx_create(self.device, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().kmh_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host-buffer counting (the drop-in path) --
+    def count(self, seq, k, canonical=False):
+        """Distinct k-mers of ``seq`` in first-occurrence order.
+
+        Returns (codes u64, counts u32, first u64) numpy arrays; codes use A0 C1 G2 T3,
+        first base most significant.
+        """
+        buf = _as_u8(seq)
+        r = ctypes.c_void_p()
+        _check(lib().kmh_count_host(self._h, _ptr(buf), buf.size, int(k), int(bool(canonical)),
+                                    ctypes.byref(r)), self._h)
+        try:
+            n = lib().kmh_kmers_size(r)
+            codes = np.empty(n, np.uint64)
+            counts = np.empty(n, np.uint32)
+            first = np.empty(n, np.uint64)
+            _check(lib().kmh_kmers_export(r, _ptr(codes), _ptr(counts), _ptr(first)))
+        finally:
+            lib().kmh_kmers_free(r)
+        return codes, counts, first
+
+    def count_dense(self, seq, k):
+        buf = _as_u8(seq)
+        out = np.empty(1 << (2 * int(k)), np.uint32)
+        _check(lib().kmh_count_dense_host(self._h, _ptr(buf), buf.size, int(k), _ptr(out)), self._h)
+        return out
+
+    # -- device-resident batch (pointers are device addresses, e.g. tensor.data_ptr()) --
+    def count_dense_dev(self, d_seq, offsets, k, d_matrix, stream=None):
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        _check(lib().kmh_count_dense_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1,
+                                         int(k), ctypes.c_void_p(d_matrix),
+                                         ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def first_dense_dev(self, d_seq, offsets, k, d_first, stream=None):
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        _check(lib().kmh_first_dense_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1,
+                                         int(k), ctypes.c_void_p(d_first),
+                                         ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def synth_dev(self, d_seq, length, stride, n_genomes, seed0, stream=None):
+        _check(lib().kmh_synth_dev(self._h, ctypes.c_void_p(d_seq), int(length), int(stride),
+                                   int(n_genomes), int(seed0),
+                                   ctypes.c_void_p(stream) if stream else None), self._h)
+
+    # -- kernel timing --
+    def timing(self, enable):
+        _check(lib().kmh_timing_enable(self._h, int(bool(enable))), self._h)
+
+    def timing_report(self):
+        cap = 64
+        names = (ctypes.c_char_p * cap)()
+        launches = (ctypes.c_uint64 * cap)()
+        total = (ctypes.c_double * cap)()
+        n = _check(lib().kmh_timing_report(self._h, names, launches, total, cap), self._h)
+        return {names[i].decode(): (int(launches[i]), float(total[i])) for i in range(min(n, cap))}
+
+
+def context(device=0):
+    """Process-wide context per device (created on first use)."""
+    device = int(device)
+    with _lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = Context(device)
+            _contexts[device] = ctx
+    return ctx
+
+
+def _as_u8(seq):
+    if isinstance(seq, np.ndarray):
+        return np.ascontiguousarray(seq, dtype=np.uint8)
+    return np.frombuffer(bytes(seq), dtype=np.uint8)
+
+
+class FastaFile:
+    """Records of a FASTA file parsed by kmh_fasta_read (generate.py:39-41 semantics)."""
+
+    def __init__(self, path):
+        h = ctypes.c_void_p()
+        _check(lib().kmh_fasta_read(os.fsencode(str(path)), ctypes.byref(h)))
+        self._h = h
+        n = lib().kmh_fasta_count(h)
+        self.ids, self.char_lens, self.seq_lens = [], [], []
+        idp, idl = ctypes.c_char_p(), ctypes.c_uint64()
+        sp, sl, cl = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint64()
+        for i in range(n):
+            _check(lib().kmh_fasta_record(h, i, ctypes.byref(idp), ctypes.byref(idl),
+                                          ctypes.byref(sp), ctypes.byref(sl), ctypes.byref(cl)))
+            raw = ctypes.string_at(idp, idl.value) if idl.value else b""
+            self.ids.append(raw.decode("utf-8", errors="surrogateescape"))
+            self.seq_lens.append(sl.value)
+            self.char_lens.append(cl.value)
+
+    def __len__(self):
+        return len(self.ids)
+
+    def sequence(self, i):
+        sp, sl = ctypes.c_void_p(), ctypes.c_uint64()
+        _check(lib().kmh_fasta_record(self._h, i, None, None, ctypes.byref(sp), ctypes.byref(sl), None))
+        return ctypes.string_at(sp, sl.value) if sl.value else b""
+
+    def pack(self, min_len, align=1):
+        """Kept records (char length >= min_len) joined by '\\n' -> (uint8 array, kept flags)."""
+        need = ctypes.c_uint64()
+        kept = np.zeros(max(len(self), 1), np.uint8)
+        _check(lib().kmh_fasta_pack(self._h, int(min_len), None, 0, ctypes.byref(need), _ptr(kept)))
+        out = np.empty(need.value + align, np.uint8)
+        _check(lib().kmh_fasta_pack(self._h, int(min_len), _ptr(out), out.size, ctypes.byref(need),
+                                    None))
+        return out[:need.value], kept[:len(self)].astype(bool)
+
+    def close(self):
+        if self._h:
+            lib().kmh_fasta_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def format_lines(k, codes, counts):
+    """k{k}.txt bytes for (codes, counts) -- generate.py:86-91 text."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint64)
+    counts = np.ascontiguousarray(counts, dtype=np.uint64)
+    n = codes.size
+    need = _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, None, 0))
+    out = ctypes.create_string_buffer(max(need, 1))
+    _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, out, need))
+    return out.raw[:need]

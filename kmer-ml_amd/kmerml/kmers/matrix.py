@@ -1,0 +1,100 @@
+"""Genomes x k-mers count matrix, one block of genomes per GPU, assembled by all-gather.
+
+The reference builds its organisms x k-mers matrix on one CPU from per-organism files
+(/root/reference/kmerml/ml/features.py:28-117, ``KmerFeatureBuilder``; rows in the sorted
+file order of find_files, features.py:46).  Here every rank (one process per GPU,
+``torch.distributed`` with the "nccl" backend = RCCL over xGMI) counts a contiguous
+block of the genome list straight into its rows of a dense ``[G, 4^k]`` uint32 matrix in
+HBM, and one ``all_gather_into_tensor`` assembles the full matrix on every rank.  Row g
+is genome g of the input order; column c is the k-mer with 2-bit code c (A0 C1 G2 T3,
+first base most significant, i.e. lexicographic order).  Counting follows
+generate.py:39-58 exactly (records shorter than k skipped, non-ACGT windows dropped).
+
+Nothing here falls back to the CPU; ``count_fn`` exists so the sharding and assembly
+logic can be exercised with the gloo backend in CPU-only tests.
+"""
+import numpy as np
+
+from kmerml import _native
+
+
+def shard_bounds(n_items, world, rank):
+    """Contiguous block [lo, hi) of n_items for `rank` (sizes differ by at most one)."""
+    lo = (n_items * rank) // world
+    hi = (n_items * (rank + 1)) // world
+    return lo, hi
+
+
+def block_rows(n_items, world):
+    """Rows per rank in the padded all-gather buffer."""
+    return -(-n_items // world) if n_items else 0
+
+
+def pack_genomes(genome_files, k):
+    """Parse FASTA files and lay them out for kmh_count_dense_dev.
+
+    Returns (buffer uint8, offsets uint64[G+1]); genome starts are 16-byte aligned and
+    separated by non-base padding; records shorter than k are dropped
+    (generate.py:44-46 with k_values = [k]).
+    """
+    parts, offsets, pos = [], [0], 0
+    for path in genome_files:
+        f = _native.FastaFile(path)
+        seq, _ = f.pack(k)
+        f.close()
+        pad = (-(seq.size)) % 16
+        parts.append(seq)
+        if pad:
+            parts.append(np.full(pad, ord("\n"), np.uint8))
+        pos += seq.size + pad
+        offsets.append(pos)  # genome g = [offsets[g], offsets[g+1]); its padding is not a base
+    buf = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return buf, np.asarray(offsets, dtype=np.uint64)
+
+
+def _hip_count_block(genome_files, k, device):
+    import torch
+
+    buf, offsets = pack_genomes(genome_files, k)
+    dev = torch.device("cuda", device)
+    d_seq = torch.from_numpy(buf).to(dev) if buf.size else torch.zeros(16, dtype=torch.uint8, device=dev)
+    out = torch.empty((len(genome_files), 1 << (2 * k)), dtype=torch.int32, device=dev)
+    if len(genome_files):
+        ctx = _native.context(device)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, out.data_ptr(), stream)
+    return out
+
+
+def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
+    """Dense [G, 4^k] count matrix of `genome_files` (torch tensor, int32 storage of u32).
+
+    Without an initialised torch.distributed process group this counts every genome on
+    one device.  With one, rank r counts block shard_bounds(G, W, r) and the blocks are
+    all-gathered, so every rank returns the full matrix in input order.
+    count_fn(files, k) -> tensor [len(files), 4^k] replaces the HIP counter (tests).
+    """
+    import torch
+    import torch.distributed as dist
+
+    if not 1 <= k <= _native.MAX_DENSE_K:
+        raise NotImplementedError("the dense count matrix needs 1 <= k <= 12")
+    files = list(genome_files)
+    G = len(files)
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    counter = count_fn or (lambda fs, kk: _hip_count_block(fs, kk, device))
+    if not (dist.is_available() and dist.is_initialized()):
+        return counter(files, k)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_bounds(G, world, rank)
+    local = counter(files[lo:hi], k)
+    B = block_rows(G, world)
+    padded = torch.zeros((B, 1 << (2 * k)), dtype=local.dtype, device=local.device)
+    padded[: hi - lo] = local
+    gathered = torch.empty((world * B, 1 << (2 * k)), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(gathered, padded, group=group)
+    rows = [gathered[r * B: r * B + (shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0])]
+            for r in range(world)]
+    return torch.cat(rows, 0) if rows else gathered[:0]

@@ -1,0 +1,269 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden
+fixtures produced by the reference.  Bit-exact for every count, code and position."""
+import contextlib
+import gzip
+import hashlib
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from kmerml import _native  # noqa: E402
+from kmerml.kmers.generate import KmerExtractor  # noqa: E402
+from kmerml.kmers import matrix as kmatrix  # noqa: E402
+from kmerml.utils.path_utils import find_files  # noqa: E402
+from oracle import synth as osynth  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return _native.context(0)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+def _rand_seq(rng, n, alphabet=b"ACGTACGTACGTacgtNn-\n"):
+    return np.frombuffer(alphabet, np.uint8)[rng.integers(0, len(alphabet), n)]
+
+
+def _layout(genomes):
+    """Concatenate host genomes with 16-byte aligned starts -> (buffer, offsets)."""
+    parts, offs, pos = [], [0], 0
+    for g in genomes:
+        pad = (-g.size) % 16
+        parts += [g, np.full(pad, 0x4E, np.uint8)]  # 'N' padding is not a base
+        pos += g.size + pad
+        offs.append(pos)
+    return np.concatenate(parts), np.array(offs, np.uint64)
+
+
+def _dense_rows(ctx, dev, genomes, k):
+    buf, offs = _layout(genomes)
+    d_seq = torch.from_numpy(buf.copy()).to(dev)
+    out = torch.full((len(genomes), 1 << (2 * k)), -7, dtype=torch.int32, device=dev)
+    ctx.count_dense_dev(d_seq.data_ptr(), offs, k, out.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32), buf, offs
+
+
+# ---------------------------------------------------------------- device generator
+def test_synth_matches_oracle(ctx, dev):
+    L, stride, G = 100_003, 100_016, 3
+    d = torch.zeros(G * stride, dtype=torch.uint8, device=dev)
+    ctx.synth_dev(d.data_ptr(), L, stride, G, osynth.SEED_BASE, torch.cuda.current_stream().cuda_stream)
+    host = d.cpu().numpy()
+    for g in range(G):
+        want = osynth.synth_bases(L, osynth.genome_seed(g))
+        assert np.array_equal(host[g * stride: g * stride + L], want), g
+
+
+# ---------------------------------------------------------------- dense, every k
+@pytest.mark.parametrize("k", list(range(1, 13)))
+def test_dense_all_k_vs_oracle(ctx, dev, oracle_lib, k):
+    rng = np.random.default_rng(100 + k)
+    genomes = [_rand_seq(rng, 250_000), _rand_seq(rng, k - 1 if k > 1 else 0),
+               np.zeros(0, np.uint8), _rand_seq(rng, 70_001), _rand_seq(rng, 16_384 + k)]
+    rows, _, _ = _dense_rows(ctx, dev, genomes, k)
+    for g, seq in enumerate(genomes):
+        want = oracle_lib.count_dense(seq, k)
+        assert np.array_equal(rows[g], want), (k, g)
+
+
+@pytest.mark.parametrize("k", [4, 8, 10, 12])
+def test_dense_low_complexity(ctx, dev, oracle_lib, k):
+    genomes = [np.full(1_000_000, ord("A"), np.uint8),
+               np.frombuffer(b"AT" * 300_000 + b"a" * 5000, np.uint8).copy()]
+    rows, _, _ = _dense_rows(ctx, dev, genomes, k)
+    for g, seq in enumerate(genomes):
+        assert np.array_equal(rows[g], oracle_lib.count_dense(seq, k)), (k, g)
+
+
+def test_dense_rejects_misaligned_offsets(ctx, dev):
+    d_seq = torch.zeros(64, dtype=torch.uint8, device=dev)
+    out = torch.zeros((2, 256), dtype=torch.int32, device=dev)
+    with pytest.raises(ValueError):
+        ctx.count_dense_dev(d_seq.data_ptr(), np.array([0, 7, 64], np.uint64), 4, out.data_ptr())
+    with pytest.raises(NotImplementedError):
+        ctx.count_dense_dev(d_seq.data_ptr(), np.array([0, 64], np.uint64), 13, out.data_ptr())
+
+
+# ---------------------------------------------------------------- BASELINE configs
+def test_config2_8x10mbp_k8(ctx, dev, oracle_lib, synthetic_cases):
+    """Config 2: 8 synthetic 10 Mbp genomes, k=8, bit-exact vs the oracle; genomes 0 and
+    1 also match the reference's own k8.txt hashes (first-occurrence order)."""
+    G, L, k = 8, 10_000_000, 8
+    d = torch.empty(G * L, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.synth_dev(d.data_ptr(), L, L, G, osynth.SEED_BASE, s)
+    offs = np.arange(G + 1, dtype=np.uint64) * L
+    out = torch.empty((G, 1 << (2 * k)), dtype=torch.int32, device=dev)
+    first = torch.empty_like(out)
+    ctx.count_dense_dev(d.data_ptr(), offs, k, out.data_ptr(), s)
+    ctx.first_dense_dev(d.data_ptr(), offs, k, first.data_ptr(), s)
+    torch.cuda.synchronize()
+    rows = out.cpu().numpy().view(np.uint32)
+    firsts = first.cpu().numpy().view(np.uint32)
+    host = d.cpu().numpy()
+    for g in range(G):
+        want, wfirst = oracle_lib.count_dense(host[g * L:(g + 1) * L], k, with_first=True)
+        assert np.array_equal(rows[g], want), g
+        assert np.array_equal(firsts[g], wfirst), g
+    for case in synthetic_cases:
+        if not case["name"].startswith("c2_"):
+            continue
+        g = int(case["name"][-4:])
+        nz = np.nonzero(rows[g])[0]
+        order = nz[np.argsort(firsts[g][nz])]
+        text = _native.format_lines(k, order.astype(np.uint64), rows[g][order].astype(np.uint64))
+        assert hashlib.sha256(text).hexdigest() == case["sha256"]["k8.txt"]
+
+
+def test_config3_64x100mbp_k12(ctx, dev, oracle_lib):
+    """Config 3 at full size: row sums equal the valid-window count for all 64 genomes,
+    two runs are identical, and genomes 0, 31 and 63 are bit-exact vs the oracle."""
+    G, L, k = 64, 100_000_000, 12
+    d = torch.empty(G * L, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.synth_dev(d.data_ptr(), L, L, G, osynth.SEED_BASE, s)
+    offs = np.arange(G + 1, dtype=np.uint64) * L
+    out = torch.empty((G, 1 << (2 * k)), dtype=torch.int32, device=dev)
+    ctx.count_dense_dev(d.data_ptr(), offs, k, out.data_ptr(), s)
+    sums = out.sum(1, dtype=torch.int64)
+    assert torch.all(sums == L - k + 1).item()
+    first_run = out.clone()
+    ctx.count_dense_dev(d.data_ptr(), offs, k, out.data_ptr(), s)
+    assert torch.equal(first_run, out)
+    del first_run
+    for g in (0, 31, 63):
+        host = d[g * L:(g + 1) * L].cpu().numpy()
+        assert np.array_equal(out[g].cpu().numpy().view(np.uint32), oracle_lib.count_dense(host, k)), g
+
+
+# ---------------------------------------------------------------- sparse, k > 12
+@pytest.mark.parametrize("k,canonical", [(13, 0), (16, 0), (21, 0), (21, 1), (31, 0), (32, 0), (32, 1), (5, 1)])
+def test_sparse_vs_oracle(ctx, oracle_lib, k, canonical):
+    rng = np.random.default_rng(k * 10 + canonical)
+    seq = _rand_seq(rng, 300_000)
+    codes, counts, first = ctx.count(seq, k, canonical=bool(canonical))
+    wc, wn, wf = oracle_lib.count_sparse(seq, k, canonical=bool(canonical))
+    order = np.argsort(wf, kind="stable")
+    assert np.array_equal(codes, wc[order])
+    assert np.array_equal(counts, wn[order])
+    assert np.array_equal(first, wf[order])
+
+
+@pytest.mark.parametrize("k", [1, 7, 12])
+def test_count_host_dense_first_order(ctx, oracle_lib, k):
+    rng = np.random.default_rng(k)
+    seq = _rand_seq(rng, 200_000)
+    codes, counts, first = ctx.count(seq, k)
+    wc, wn, wf = oracle_lib.count_sparse(seq, k)
+    order = np.argsort(wf, kind="stable")
+    assert np.array_equal(codes, wc[order]) and np.array_equal(counts, wn[order])
+    assert np.array_equal(first, wf[order])
+
+
+# ---------------------------------------------------------------- the drop-in API
+def _run_extractor(tmp_path, fasta, ks, compress=False, org="org"):
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        ext = KmerExtractor(output_dir=str(tmp_path), compress=compress)
+        ret = ext.extract_kmers_from_fasta(fasta, ks, organism_id=org)
+    odir = tmp_path / org
+    files = {}
+    if odir.is_dir():
+        for p in sorted(odir.iterdir()):
+            data = p.read_bytes()
+            if p.suffix == ".gz":
+                data = gzip.decompress(data)
+            files[p.name.replace(".gz", "")] = data.decode()
+    return ret, buf.getvalue().splitlines(), files
+
+
+def test_dropin_edge_cases_byte_identical(tmp_path, golden_dir, edge_cases):
+    for i, case in enumerate(edge_cases):
+        if max(case["k_values"]) > 32:
+            with pytest.raises(NotImplementedError):
+                _run_extractor(tmp_path / f"c{i}", os.path.join(golden_dir, "inputs", case["input"]),
+                               case["k_values"])
+            continue
+        ret, out, files = _run_extractor(tmp_path / f"c{i}", os.path.join(golden_dir, "inputs", case["input"]),
+                                         case["k_values"])
+        assert ret == case["returned"]
+        assert out == case["stdout"], case["input"]
+        assert files == case["files"], (case["input"], case["k_values"])
+
+
+def test_dropin_compressed(tmp_path, golden_dir, edge_cases):
+    case = edge_cases[3]
+    _, _, files = _run_extractor(tmp_path, os.path.join(golden_dir, "inputs", case["input"]),
+                                 case["k_values"], compress=True)
+    assert files == case["files"]
+    assert all(p.name.endswith(".txt.gz") for p in (tmp_path / "org").iterdir())
+
+
+def test_dropin_synthetic_hashes(tmp_path, synthetic_cases):
+    for case in synthetic_cases:
+        if case["name"] == "yeast_standin":
+            recs = osynth.yeast_standin_records()
+            fa = tmp_path / "yeast_standin.fa"
+            osynth.write_fasta(fa, recs)
+            _, out, files = _run_extractor(tmp_path / "ys", fa, [4], org="yeast_standin")
+            assert files["k4.txt"] == case["text"]["k4.txt"]
+            assert out == case["stdout"]
+            continue
+        (g,) = case["genomes"]
+        fa = tmp_path / f"{case['name']}.fa"
+        osynth.write_fasta(fa, [(g["id"], osynth.synth_bases(g["length"], g["seed"], g["start"]).tobytes())])
+        (k,) = case["k_values"]
+        _, out, files = _run_extractor(tmp_path / case["name"], fa, [k])
+        assert out == case["stdout"]
+        assert hashlib.sha256(files[f"k{k}.txt"].encode()).hexdigest() == case["sha256"][f"k{k}.txt"], case["name"]
+
+
+def test_cli_call_pattern_and_genome_list(tmp_path, golden_dir, edge_cases):
+    """scripts/extract_kmers.py:46-61 and generate.py:93-129 call patterns."""
+    src = tmp_path / "raw"
+    src.mkdir()
+    for name in ("e1_mixed.fa", "e2_crlf.fa", "e4_short.fa"):
+        (src / name).write_bytes(open(os.path.join(golden_dir, "inputs", name), "rb").read())
+    (src / "notes.txt").write_text("ignored")
+    genomes = find_files(src, patterns="*.fa,*.fasta".split(","), recursive=False)
+    assert [g.name for g in genomes] == ["e1_mixed.fa", "e2_crlf.fa", "e4_short.fa"]
+    ext = KmerExtractor(output_dir=str(tmp_path / "out"), compress=False)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        for genome in genomes:
+            ext.extract_kmers_from_fasta(genome, [3, 8], organism_id=genome.stem)
+        ids = ext.extract_from_genome_list([str(g) for g in genomes] + [str(src / "missing.fa")], [3, 8])
+    assert ids == ["e1_mixed", "e2_crlf", "e4_short"]
+    assert "Error processing missing" in buf.getvalue()
+    want = next(c for c in edge_cases if c["input"] == "e2_crlf.fa" and c["k_values"] == [3, 8])
+    assert (tmp_path / "out" / "e2_crlf" / "k8.txt").read_text() == want["files"]["k8.txt"]
+    with pytest.raises(ValueError):
+        ext.extract_from_genome_list([str(genomes[0])], [3], organism_ids=["a", "b"])
+
+
+def test_count_matrix_single_process(tmp_path, oracle_lib):
+    rng = np.random.default_rng(3)
+    files, seqs = [], []
+    for i in range(5):
+        s = _rand_seq(rng, 40_000 + 1000 * i, b"ACGTACGTN").tobytes()
+        p = tmp_path / f"g{i}.fa"
+        osynth.write_fasta(p, [(f"r{i}", s[:20_000]), (f"q{i}", s[20_000:])])
+        files.append(p)
+        seqs.append(s[:20_000] + b"\n" + s[20_000:] + b"\n")
+    m = kmatrix.count_matrix(files, 10).cpu().numpy().view(np.uint32)
+    for i, s in enumerate(seqs):
+        assert np.array_equal(m[i], oracle_lib.count_dense(s, 10)), i

@@ -1,0 +1,113 @@
+"""CPU: the C-ABI library loads, exports every declared symbol, and its host-side pieces
+(FASTA ingest, text formatter, error reporting) match the oracle.  No GPU needed."""
+import os
+import re
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from kmerml import _native
+from oracle import fasta as ofasta
+from oracle import kmers as okmers
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "kmerhip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(kmh_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _native.lib()
+    names = declared_functions()
+    assert len(names) >= 20
+    for name in names:
+        assert hasattr(L, name), name
+    bound = {n for n, _, _ in _native.SIGNATURES}
+    assert bound == set(names), "ctypes signatures and header disagree"
+
+
+def test_version_string():
+    assert _native.lib().kmh_version().decode().startswith("kmerhip")
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(_native.KmhError):
+        _native.Context(0)
+
+
+def _native_records(path):
+    f = _native.FastaFile(path)
+    out = [(f.ids[i], f.sequence(i), f.char_lens[i]) for i in range(len(f))]
+    f.close()
+    return out
+
+
+def test_fasta_parser_matches_oracle_on_golden_inputs(golden_dir):
+    inputs = os.path.join(golden_dir, "inputs")
+    for name in sorted(os.listdir(inputs)):
+        path = os.path.join(inputs, name)
+        ref = ofasta.parse_fasta(path)
+        got = _native_records(path)
+        assert [r[0] for r in got] == [r[0] for r in ref], name
+        assert [r[1].decode() for r in got] == [r[2] for r in ref], name
+        assert [r[2] for r in got] == [len(r[2]) for r in ref], name
+
+
+def test_fasta_missing_file_raises_oserror(tmp_path):
+    with pytest.raises(OSError):
+        _native.FastaFile(tmp_path / "nope.fa")
+
+
+_alphabet = st.sampled_from(list("ACGTacgtNnRY \t\r\n>;-*xé") + [" ", " ", "　"])
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(_alphabet, max_size=300).map("".join))
+def test_fasta_parser_property(tmp_path_factory, text):
+    path = tmp_path_factory.mktemp("fa") / "x.fa"
+    path.write_bytes(text.encode("utf-8"))
+    ref = ofasta.parse_fasta(path)
+    got = _native_records(path)
+    assert [(r[0], r[2]) for r in ref] == [(g[0], g[1].decode("utf-8")) for g in got]
+    assert [len(r[2]) for r in ref] == [g[2] for g in got]
+
+
+def test_pack_applies_short_record_rule(golden_dir):
+    path = os.path.join(golden_dir, "inputs", "e1_mixed.fa")
+    f = _native.FastaFile(path)
+    packed, kept = f.pack(4)
+    ref = ofasta.parse_fasta(path)
+    assert list(kept) == [len(s) >= 4 for _, _, s in ref]
+    assert packed.tobytes() == b"".join(s.encode() + b"\n" for _, _, s in ref if len(s) >= 4)
+    f.close()
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 12, 21, 32])
+def test_format_lines_matches_reference_text(k):
+    rng = np.random.default_rng(k)
+    codes = rng.integers(0, 1 << min(62, 2 * k), 500, dtype=np.uint64)
+    if k == 32:
+        codes[0] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    counts = rng.integers(1, 1 << 40, 500, dtype=np.uint64)
+    got = _native.format_lines(k, codes, counts).decode()
+    want = okmers.kmer_text({okmers.code_kmer(int(c), k): int(n) for c, n in zip(codes, counts)}
+                            ) if len(set(codes.tolist())) == codes.size else None
+    if want is not None:
+        assert got == want
+    lines = got.splitlines()
+    assert len(lines) == 500
+    c0 = okmers.code_kmer(int(codes[0]), k)
+    assert lines[0] == "".join(okmers.DIGIT[b] for b in c0) + f"\t{int(counts[0])}"
+
+
+def test_format_lines_empty():
+    assert _native.format_lines(8, np.empty(0, np.uint64), np.empty(0, np.uint64)) == b""
