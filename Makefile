@@ -11,7 +11,7 @@ LIB      := $(OUTDIR)/libkmerhip.so
 OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o
 HDRS     := $(CSRC)/kmh_internal.h include/kmerhip.h
 
-all: lib oracle
+all: lib oracle selftest
 
 lib: $(LIB)
 
@@ -35,3 +35,11 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib oracle clean
+
+SELFTEST := $(OUTDIR)/kmh_selftest
+selftest: $(SELFTEST)
+
+$(SELFTEST): tests/native/kmh_selftest.cpp $(LIB) include/kmerhip.h
+	$(HIPCC) -O2 -std=c++17 -o $@ $< -L$(OUTDIR) -lkmerhip -Wl,-rpath,'$$ORIGIN'
+
+.PHONY: selftest

@@ -15,7 +15,8 @@
  *   - The caller owns every host buffer; the library owns the device buffers of a
  *     context.  Functions with a _dev suffix take DEVICE pointers (hipMalloc /
  *     torch tensors on the context's device) and a hipStream_t passed as void*
- *     (NULL = the context's own stream); they only enqueue work.
+ *     (NULL = the HIP null stream, as everywhere in HIP; torch's default stream);
+ *     they only enqueue work.
  *   - One context per (thread, device).  Calls on one context are serialised by the
  *     caller; different contexts may be used concurrently.
  *   - Base alphabet: A/C/G/T in either case are bases (generate.py:41 upper()s the

@@ -100,9 +100,9 @@ void time_end(Ctx* ctx, hipStream_t s) {
 
 using kmh::fail;
 
-static hipStream_t pick_stream(kmh_ctx* ctx, void* stream) {
-    return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-}
+// NULL means the HIP null stream (the convention of every HIP API, and the handle of
+// torch's default stream); the context's own stream serves the host-buffer calls only.
+static hipStream_t pick_stream(kmh_ctx*, void* stream) { return static_cast<hipStream_t>(stream); }
 
 extern "C" {
 

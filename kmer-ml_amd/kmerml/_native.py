@@ -52,7 +52,8 @@ SIGNATURES = [
 ]
 
 _lib = None
-_lock = threading.Lock()
+_lib_lock = threading.Lock()
+_ctx_lock = threading.Lock()   # separate: context() loads the library while holding it
 _contexts = {}
 
 
@@ -68,7 +69,7 @@ def lib():
     """Load libkmerhip.so (raises ImportError if it was not built)."""
     global _lib
     if _lib is None:
-        with _lock:
+        with _lib_lock:
             if _lib is None:
                 if not os.path.exists(LIB_PATH):
                     raise ImportError(f"libkmerhip.so not found at {LIB_PATH}; build it with `make lib` "
@@ -187,7 +188,7 @@ class Context:
 def context(device=0):
     """Process-wide context per device (created on first use)."""
     device = int(device)
-    with _lock:
+    with _ctx_lock:
         ctx = _contexts.get(device)
         if ctx is None:
             ctx = Context(device)

@@ -42,6 +42,8 @@ def test_ctx_create_without_gpu_fails_loudly():
         pytest.skip("a GPU is present")
     with pytest.raises(_native.KmhError):
         _native.Context(0)
+    with pytest.raises(_native.KmhError):   # the cached-context path must not deadlock
+        _native.context(0)
 
 
 def _native_records(path):
