@@ -7,7 +7,7 @@
 //   k <= 9   k_direct:     each workgroup counts a span of one genome into an LDS table
 //                          (4^k bins, or 32768-bin slices in 4^k/32768 passes for k = 8, 9)
 //                          and adds it into the genome's row.
-//   k >= 10  k_partition:  one 16384-window tile per workgroup; k-mers are bucketed by
+//   k >= 10  k_partition:  one 32768-window tile per workgroup; k-mers are bucketed by
 //                          their top 2k-15 bits with an LDS counting sort and each tile
 //                          writes its bucket-ordered 15-bit suffixes + bucket offsets.
 //            k_bucket_count: one workgroup per (genome, bucket) gathers that bucket's
@@ -92,6 +92,7 @@ __device__ __forceinline__ void enc16(uint4 v, uint32_t& code, uint32_t& inv) {
 template <int K, typename F>
 __device__ __forceinline__ void walk_tile(const uint8_t* __restrict__ seq, uint64_t tstart,
                                           uint64_t gend, F&& f) {
+    // A tile of any workgroup size: thread t covers starts [tstart + 32 t, + 32).
     static_assert(K >= 1 && K <= 16, "dense windows need k <= 16");
     const int lane = threadIdx.x & 63;
     const uint64_t base = tstart + (uint64_t)threadIdx.x * kTileBpt;
@@ -173,33 +174,35 @@ __global__ __launch_bounds__(kDirectThreads) void k_direct(const uint8_t* __rest
 }
 
 // ---------------------------------------------------------------- k >= 10: partition
-template <int K>
-__global__ __launch_bounds__(kTileThreads) void k_partition(const uint8_t* __restrict__ seq,
-                                                            GenomeMap m,
-                                                            uint16_t* __restrict__ suf,
-                                                            uint16_t* __restrict__ toff) {
+// Ablation bits (experiments only; outputs are wrong when set): 1 = no histogram atomics
+// (synthetic uniform bucket starts), 2 = no scatter, 4 = no write-out.
+template <int K, int TPB, int ABL>
+__global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ seq,
+                                                   GenomeMap m, uint16_t* __restrict__ suf,
+                                                   uint16_t* __restrict__ toff) {
     constexpr int NBK = num_buckets<K>();
     constexpr int TS = toff_stride<K>();
-    static_assert(NBK <= kTileThreads, "one scan element per thread");
-    __shared__ __attribute__((aligned(16))) uint16_t sorted[kTile];
+    constexpr int TILE = TPB * kTileBpt;
+    static_assert(NBK <= TPB, "one scan element per thread");
+    __shared__ __attribute__((aligned(16))) uint16_t sorted[TILE];
     __shared__ uint32_t cnt[NBK];
     __shared__ uint32_t cur[NBK];
-    __shared__ uint32_t wsum[kTileThreads / 64];
+    __shared__ uint32_t wsum[TPB / 64];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt = blockIdx.x;
     const uint64_t gt = m.tile_lo + lt;
     const int g = find_genome(m, gt);
-    const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)kTile;
+    const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)TILE;
     const uint64_t ge = m.goff[g + 1];
 
-    for (int b = tid; b < NBK; b += kTileThreads) cnt[b] = 0u;
+    for (int b = tid; b < NBK; b += TPB) cnt[b] = (ABL & 1) ? (uint32_t)(TILE / NBK) : 0u;
     __syncthreads();
 
     uint32_t km[kTileBpt];
     walk_tile<K>(seq, tstart, ge, [&](int j, uint32_t code, bool ok) {
         km[j] = ok ? code : 0xFFFFFFFFu;
-        if (ok) atomicAdd(&cnt[code >> kSubBits], 1u);
+        if (!(ABL & 1) && ok) atomicAdd(&cnt[code >> kSubBits], 1u);
     });
     __syncthreads();
 
@@ -215,7 +218,7 @@ __global__ __launch_bounds__(kTileThreads) void k_partition(const uint8_t* __res
     __syncthreads();
     uint32_t pre = 0u, total = 0u;
 #pragma unroll
-    for (int w = 0; w < kTileThreads / 64; ++w) {
+    for (int w = 0; w < TPB / 64; ++w) {
         pre += (w < wave) ? wsum[w] : 0u;
         total += wsum[w];
     }
@@ -228,30 +231,57 @@ __global__ __launch_bounds__(kTileThreads) void k_partition(const uint8_t* __res
     __syncthreads();
 
     // Scatter 15-bit suffixes into bucket order.
+    if (!(ABL & 2)) {
 #pragma unroll
-    for (int j = 0; j < kTileBpt; ++j) {
-        const uint32_t c = km[j];
-        if (c != 0xFFFFFFFFu) {
-            const uint32_t slot = atomicAdd(&cur[c >> kSubBits], 1u);
-            sorted[slot] = (uint16_t)(c & (kSubBins - 1));
+        for (int j = 0; j < kTileBpt; ++j) {
+            const uint32_t c = km[j];
+            if (c != 0xFFFFFFFFu) {
+                const uint32_t slot = atomicAdd(&cur[c >> kSubBits], 1u) & (TILE - 1);
+                sorted[slot] = (uint16_t)(c & (kSubBins - 1));
+            }
         }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kTileBpt; ++j) asm volatile("" ::"v"(km[j]));
     }
     __syncthreads();
 
-    uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)kTile);
-    const uint4* src = reinterpret_cast<const uint4*>(sorted);
-    const uint32_t nchunk = (total + 7u) >> 3;
-    for (uint32_t c = tid; c < nchunk; c += kTileThreads) dst[c] = src[c];
+    if (!(ABL & 4)) {
+        uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)TILE);
+        const uint4* src = reinterpret_cast<const uint4*>(sorted);
+        const uint32_t nchunk = (total + 7u) >> 3;
+        for (uint32_t c = tid; c < nchunk; c += TPB) dst[c] = src[c];
+    }
 }
 
-template <int K, int GS>
+// Count one 15-bit suffix stream chunk of 8 entries (a 16-byte load) whose entry
+// indices are [c, c + 8); only entries inside [s0, e0) belong to this bucket.
+__device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t c, uint32_t s0,
+                                            uint32_t e0) {
+    const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t idx = c + (uint32_t)i;
+        if (idx >= s0 && idx < e0) atomicAdd(&tbl[(wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu], 1u);
+    }
+}
+
+// One workgroup per (genome, bucket[, split]): gathers the bucket's segment from every
+// tile of the genome into a 32768-bin LDS histogram, then writes the row slice once.
+// The tiles' segment bounds are staged in LDS first (kSegStage tiles at a time), so the
+// suffix loads do not wait behind dependent offset loads; each group of GS lanes covers
+// one segment and U tiles' loads are issued before their LDS atomics.
+// Ablation bits (experiments only): 1 = no LDS atomics, 2 = no suffix loads.
+template <int K, int GS, int U, int TILE, int ABL>
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, GenomeMap m, int S,
     uint32_t* __restrict__ out) {
     constexpr int NBK = num_buckets<K>();
     constexpr int TS = toff_stride<K>();
     constexpr int NGRP = kCountThreads / GS;
+    constexpr uint32_t ROW = GS * 8u;  // entries covered by one load of every lane of a group
     __shared__ __attribute__((aligned(16))) uint32_t tbl[kSubBins];
+    __shared__ uint32_t seg[kSegStage];
 
     const uint32_t w = xcd_work_id();
     const int s = (int)(w % (uint32_t)S);
@@ -263,20 +293,51 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
 
     uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
     for (int i = threadIdx.x; i < kSubBins / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
 
-    const int grp = threadIdx.x / GS, r = threadIdx.x % GS;
-    for (uint64_t t = ta + grp; t < tb; t += NGRP) {
-        const uint16_t* row = toff + t * (uint64_t)TS;
-        const uint32_t s0 = row[b], e0 = row[b + 1];
-        const uint16_t* p = suf + t * (uint64_t)kTile;
-        for (uint32_t c = (s0 & ~7u) + (uint32_t)r * 8u; c < e0; c += GS * 8u) {
-            const uint4 q = *reinterpret_cast<const uint4*>(p + c);
-            const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+    const int grp = threadIdx.x / GS;
+    const uint32_t r8 = (uint32_t)(threadIdx.x % GS) * 8u;
+    for (uint64_t c0 = ta; c0 < tb; c0 += kSegStage) {
+        const int n = (int)((tb - c0) < (uint64_t)kSegStage ? (tb - c0) : (uint64_t)kSegStage);
+        __syncthreads();  // previous stage fully consumed (and the table zeroed)
+        for (int i = threadIdx.x; i < n; i += kCountThreads) {
+            const uint16_t* row = toff + (c0 + (uint64_t)i) * TS;
+            seg[i] = (uint32_t)row[b] | ((uint32_t)row[b + 1] << 16);
+        }
+        __syncthreads();
+        for (int base = grp; base < n; base += NGRP * U) {
+            uint4 q0[U], q1[U];
+            uint32_t lo[U], hi[U], cc[U];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t idx = c + (uint32_t)i;
-                if (idx >= s0 && idx < e0) atomicAdd(&tbl[(wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu], 1u);
+            for (int u = 0; u < U; ++u) {
+                const int i = base + u * NGRP;
+                const uint32_t sv = i < n ? seg[i] : 0u;
+                lo[u] = sv & 0xFFFFu;
+                hi[u] = sv >> 16;
+                cc[u] = (lo[u] & ~7u) + r8;
+                const uint16_t* p = suf + (c0 + (uint64_t)(i < n ? i : 0)) * (uint64_t)TILE;
+                if (ABL & 2) {
+                    const uint32_t x = (uint32_t)i * 2654435761u + r8;
+                    q0[u] = make_uint4(x, x * 3u, x * 5u, x * 7u);
+                    q1[u] = make_uint4(x * 11u, x * 13u, x * 17u, x * 19u);
+                } else {
+                    q0[u] = cc[u] < hi[u] ? *reinterpret_cast<const uint4*>(p + cc[u]) : make_uint4(0u, 0u, 0u, 0u);
+                    q1[u] = cc[u] + ROW < hi[u] ? *reinterpret_cast<const uint4*>(p + cc[u] + ROW)
+                                                : make_uint4(0u, 0u, 0u, 0u);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (ABL & 1) {
+                    asm volatile("" ::"v"(q0[u].x ^ q0[u].y ^ q0[u].z ^ q0[u].w ^ q1[u].x ^ q1[u].y ^ q1[u].z ^ q1[u].w));
+                    continue;
+                }
+                count_chunk(tbl, q0[u], cc[u], lo[u], hi[u]);
+                count_chunk(tbl, q1[u], cc[u] + ROW, lo[u], hi[u]);
+                // long segments (skewed input): the rest, one row at a time
+                const int i = base + u * NGRP;
+                const uint16_t* p = suf + (c0 + (uint64_t)(i < n ? i : 0)) * (uint64_t)TILE;
+                for (uint32_t c = cc[u] + 2 * ROW; c < hi[u]; c += ROW)
+                    count_chunk(tbl, *reinterpret_cast<const uint4*>(p + c), c, lo[u], hi[u]);
             }
         }
     }
@@ -350,7 +411,7 @@ struct Layout {
     uint64_t ntiles = 0;
 };
 
-int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, Layout& L) {
+int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, uint64_t tile, Layout& L) {
     if (G < 1) return fail(ctx, KMH_ERR_INVALID, "G must be >= 1");
     if (!offsets) return fail(ctx, KMH_ERR_INVALID, "offsets is NULL");
     L.goff.assign(offsets, offsets + G + 1);
@@ -361,7 +422,7 @@ int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, Layout& L) {
         if (a % 16 != 0) return fail(ctx, KMH_ERR_INVALID, "genome start offsets must be multiples of 16");
         if (b - a >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "a genome must be shorter than 2^32 - 1 bytes");
         const uint64_t nwin = (b - a >= (uint64_t)k) ? (b - a - (uint64_t)k + 1) : 0;
-        L.tbase[g + 1] = L.tbase[g] + (nwin + kTile - 1) / kTile;
+        L.tbase[g + 1] = L.tbase[g] + (nwin + tile - 1) / tile;
     }
     L.ntiles = L.tbase[G];
     return KMH_OK;
@@ -409,19 +470,21 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
     return KMH_OK;
 }
 
-template <int K>
+template <int K, int TPB, int PABL, int CABL>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
     constexpr int NBK = num_buckets<K>();
     constexpr int TS = toff_stride<K>();
-    constexpr int GS0 = kTile / NBK / 8;
+    constexpr int TILE = TPB * kTileBpt;
+    constexpr int GS0 = TILE / NBK / 8;   // lanes per segment: one 16-B load each
     constexpr int GS = GS0 < 1 ? 1 : (GS0 > 64 ? 64 : GS0);
+    constexpr int U = 4;                  // tiles in flight per lane group
     const size_t row = (size_t)1 << (2 * K);
     // Genomes per batch: keep the suffix buffer of one batch within the budget (it is
     // written and re-read, so a budget inside the 256 MiB Infinity Cache can keep it
     // on-die).  KMH_SUF_BUDGET_MB overrides.
     const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 256) << 20;
-    const size_t tile_bytes = (size_t)kTile * sizeof(uint16_t);
+    const size_t tile_bytes = (size_t)TILE * sizeof(uint16_t);
     uint64_t max_batch_tiles = 0;
     {
         int g = 0;
@@ -460,13 +523,13 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
         if (S > 1) KMH_HIP(ctx, hipMemsetAsync(d_out + (size_t)g * row, 0, (size_t)nG * row * sizeof(uint32_t), s));
         if (tiles) {
             time_begin(ctx, s, "k_partition");
-            hipLaunchKernelGGL(k_partition<K>, dim3((unsigned)tiles), dim3(kTileThreads), 0, s,
+            hipLaunchKernelGGL((k_partition<K, TPB, PABL>), dim3((unsigned)tiles), dim3(TPB), 0, s,
                                d_seq, m, suf, toff);
             time_end(ctx, s);
             KMH_HIP(ctx, hipGetLastError());
         }
         time_begin(ctx, s, "k_bucket_count");
-        hipLaunchKernelGGL((k_bucket_count<K, GS>), dim3((unsigned)(nG * NBK * S)),
+        hipLaunchKernelGGL((k_bucket_count<K, GS, U, TILE, CABL>), dim3((unsigned)(nG * NBK * S)),
                            dim3(kCountThreads), 0, s, suf, toff, m, S, d_out);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
@@ -476,15 +539,48 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
 }
 
 template <int K>
-int count_k(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
-            const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
-    if constexpr (K <= 9) return run_direct<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-    else return run_partitioned<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint32_t* d_out,
+            hipStream_t s) {
+    Layout L;
+    const uint64_t *d_goff, *d_tbase;
+    if constexpr (K <= 9) {
+        int rc = make_layout(ctx, offsets, G, K, kTile, L);
+        if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+        if (rc) return rc;
+        return run_direct<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+    } else {
+        // Tile workgroup size (512 or 1024 threads); KMH_TPB overrides.  For k = 12,
+        // KMH_ABLATE_P / KMH_ABLATE_C select ablation builds (experiments only: wrong
+        // counts) -- see the ablation bits of k_partition / k_bucket_count.
+        const int tpb = (int)env_mb("KMH_TPB", 512) == 1024 ? 1024 : 512;
+        int rc = make_layout(ctx, offsets, G, K, (uint64_t)tpb * kTileBpt, L);
+        if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+        if (rc) return rc;
+        if constexpr (K == 12) {
+            const int pa = (int)env_mb("KMH_ABLATE_P", 0), ca = (int)env_mb("KMH_ABLATE_C", 0);
+            if (pa || ca) {
+                if (tpb != 512) return fail(ctx, KMH_ERR_INVALID, "ablations use KMH_TPB=512");
+                if (pa == 1) return run_partitioned<K, 512, 1, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (pa == 2) return run_partitioned<K, 512, 2, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (pa == 4) return run_partitioned<K, 512, 4, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 1) return run_partitioned<K, 512, 0, 1>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 2) return run_partitioned<K, 512, 0, 2>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                return fail(ctx, KMH_ERR_INVALID, "unknown ablation");
+            }
+        }
+        if (tpb == 1024) return run_partitioned<K, 1024, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+        return run_partitioned<K, 512, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+    }
 }
 
 template <int K>
-int first_k(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
-            const uint64_t* d_tbase, int G, uint32_t* d_first, hipStream_t s) {
+int first_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint32_t* d_first,
+            hipStream_t s) {
+    Layout L;
+    const uint64_t *d_goff, *d_tbase;
+    int rc = make_layout(ctx, offsets, G, K, kTile, L);
+    if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+    if (rc) return rc;
     const size_t row = (size_t)1 << (2 * K);
     KMH_HIP(ctx, hipMemsetAsync(d_first, 0xFF, row * (size_t)G * sizeof(uint32_t), s));
     if (L.ntiles == 0) return KMH_OK;
@@ -520,13 +616,7 @@ int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, 
                 uint32_t* d_out, hipStream_t s) {
     if (k < 1 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "dense counting needs 1 <= k <= 12");
     if (!d_seq || !d_out) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
-    Layout L;
-    int rc = make_layout(ctx, offsets, G, k, L);
-    if (rc) return rc;
-    const uint64_t *d_goff, *d_tbase;
-    rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
-    if (rc) return rc;
-    KMH_DISPATCH_K(count_k, k, ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+    KMH_DISPATCH_K(count_k, k, ctx, d_seq, offsets, G, d_out, s);
     return fail(ctx, KMH_ERR_UNSUPPORTED, "unsupported k");
 }
 
@@ -534,13 +624,7 @@ int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, 
                 uint32_t* d_first, hipStream_t s) {
     if (k < 1 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "dense counting needs 1 <= k <= 12");
     if (!d_seq || !d_first) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
-    Layout L;
-    int rc = make_layout(ctx, offsets, G, k, L);
-    if (rc) return rc;
-    const uint64_t *d_goff, *d_tbase;
-    rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
-    if (rc) return rc;
-    KMH_DISPATCH_K(first_k, k, ctx, d_seq, L, d_goff, d_tbase, G, d_first, s);
+    KMH_DISPATCH_K(first_k, k, ctx, d_seq, offsets, G, d_first, s);
     return fail(ctx, KMH_ERR_UNSUPPORTED, "unsupported k");
 }
 
