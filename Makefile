@@ -43,3 +43,10 @@ $(SELFTEST): tests/native/kmh_selftest.cpp $(LIB) include/kmerhip.h
 	$(HIPCC) -O2 -std=c++17 -o $@ $< -L$(OUTDIR) -lkmerhip -Wl,-rpath,'$$ORIGIN'
 
 .PHONY: selftest
+
+LDSBENCH := $(OUTDIR)/lds_bench
+ldsbench: $(LDSBENCH)
+$(LDSBENCH): tests/native/lds_bench.hip
+	@mkdir -p $(OUTDIR)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+.PHONY: ldsbench

@@ -33,13 +33,21 @@ struct GenomeMap {
     const uint64_t* tbase;  // cumulative tile counts, G + 1 (device), tbase[0] = 0
     int g0, g1;             // genomes covered by this launch
     uint64_t tile_lo;       // tbase[g0]
+    uint64_t data_end;      // offsets[G]: bytes at or past it may not be readable
 };
 
 template <int K>
 constexpr int num_buckets() { return 1 << (2 * K - kSubBits); }
 
+
+// Entries per tile in the suffix buffer: every bucket segment is padded to whole 16-byte
+// chunks (8 entries) so the count kernel reads aligned chunks with no masking.  Padding
+// entries hold kPadBase + ((8 * bucket + slot) & 63): 64 dummy LDS bins past the real
+// 32768, spread so that padding lanes of one instruction rarely share an address.
 template <int K>
-constexpr int toff_stride() { return ((num_buckets<K>() + 1 + 7) / 8) * 8; }
+constexpr int tile_cap(int tile) { return tile + num_buckets<K>() * 7; }
+constexpr uint32_t kPadBase = (uint32_t)kSubBins;
+constexpr uint32_t kPadBins = 64;
 
 // Largest g in [g0, g1) with tbase[g] <= gt (genomes without tiles are skipped).
 __device__ __forceinline__ int find_genome(const GenomeMap& m, uint64_t gt) {
@@ -86,22 +94,40 @@ __device__ __forceinline__ void enc16(uint4 v, uint32_t& code, uint32_t& inv) {
     inv = (i0 << 12) | (i1 << 8) | (i2 << 4) | i3;
 }
 
-// Visit the 32 windows that start at tstart + 32 * threadIdx.x + j, j = 0..31, of a
-// kTileThreads-thread workgroup: f(j, code, is_valid).  The k - 1 <= 15 bases past a
-// thread's 32 come from the next lane's first 16 (lane 63 loads them).
-template <int K, typename F>
+// Invalid-mask bits for the bytes of a 16-byte chunk at pos that lie at or past `end`
+// (bit 15 = byte 0).
+__device__ __forceinline__ uint32_t tail_mask(uint64_t pos, uint64_t end) {
+    if (end >= pos + 16) return 0u;
+    if (end <= pos) return 0xFFFFu;
+    return 0xFFFFu >> (uint32_t)(end - pos);
+}
+
+// Visit the 32 windows that start at tstart + 32 * threadIdx.x + j, j = 0..31:
+// f(j, code, is_valid).  Each thread loads its 32 bytes plus the next 16 (the k - 1 <= 15
+// bases its last windows need).  FAST: the three 16-byte loads are issued back to back
+// with no guard (the caller checked that every byte read lies before data_end) and bytes
+// past the genome end are masked arithmetically; otherwise byte-wise guarded loads.
+template <int K, bool FAST, typename F>
 __device__ __forceinline__ void walk_tile(const uint8_t* __restrict__ seq, uint64_t tstart,
                                           uint64_t gend, F&& f) {
-    // A tile of any workgroup size: thread t covers starts [tstart + 32 t, + 32).
     static_assert(K >= 1 && K <= 16, "dense windows need k <= 16");
-    const int lane = threadIdx.x & 63;
     const uint64_t base = tstart + (uint64_t)threadIdx.x * kTileBpt;
-    uint32_t cA, iA, cB, iB;
-    enc16(load16(seq, base, gend), cA, iA);
-    enc16(load16(seq, base + 16, gend), cB, iB);
-    uint32_t cN = __shfl_down(cA, 1);
-    uint32_t iN = __shfl_down(iA, 1);
-    if (lane == 63) enc16(load16(seq, base + 32, gend), cN, iN);
+    uint32_t cA, iA, cB, iB, cN, iN;
+    if constexpr (FAST) {
+        const uint4 a = *reinterpret_cast<const uint4*>(seq + base);
+        const uint4 b = *reinterpret_cast<const uint4*>(seq + base + 16);
+        const uint4 n = *reinterpret_cast<const uint4*>(seq + base + 32);
+        enc16(a, cA, iA);
+        enc16(b, cB, iB);
+        enc16(n, cN, iN);
+        iA |= tail_mask(base, gend);
+        iB |= tail_mask(base + 16, gend);
+        iN |= tail_mask(base + 32, gend);
+    } else {
+        enc16(load16(seq, base, gend), cA, iA);
+        enc16(load16(seq, base + 16, gend), cB, iB);
+        enc16(load16(seq, base + 32, gend), cN, iN);
+    }
     constexpr uint32_t KM = (K == 16) ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
     constexpr uint32_t VM = (1u << K) - 1u;
     const uint64_t wAB = ((uint64_t)cA << 32) | cB;
@@ -120,11 +146,22 @@ __device__ __forceinline__ void walk_tile(const uint8_t* __restrict__ seq, uint6
     }
 }
 
+// Dispatch a tile walk of `tpb` threads to the fast or the guarded loads (uniform per
+// workgroup: only tiles within 48 bytes of the end of the whole buffer take the slow path).
+template <int K, typename F>
+__device__ __forceinline__ void walk(const uint8_t* __restrict__ seq, const GenomeMap& m,
+                                     uint64_t tstart, uint64_t gend, int tpb, F&& f) {
+    if (tstart + (uint64_t)tpb * kTileBpt + 16 <= m.data_end) walk_tile<K, true>(seq, tstart, gend, f);
+    else walk_tile<K, false>(seq, tstart, gend, f);
+}
+
 // XCD-aware work order: blocks b and b+8 share an XCD under the observed round-robin
 // placement, so hand each XCD a contiguous range of work items (speed only).
+// Bijective for any grid size: XCD group x = b % 8 owns a contiguous run of work items.
 __device__ __forceinline__ uint32_t xcd_work_id() {
     const uint32_t nb = gridDim.x, b = blockIdx.x;
-    return (nb % 8u == 0u) ? (b % 8u) * (nb / 8u) + b / 8u : b;
+    const uint32_t q = nb / 8u, rem = nb % 8u, x = b % 8u;
+    return x * q + (x < rem ? x : rem) + b / 8u;
 }
 
 // ---------------------------------------------------------------- k <= 9: direct
@@ -152,7 +189,7 @@ __global__ __launch_bounds__(kDirectThreads) void k_direct(const uint8_t* __rest
         for (uint32_t i = threadIdx.x; i < REP * SLICE; i += kDirectThreads) tbl[i] = 0u;
         __syncthreads();
         for (uint64_t t = ta; t < tb; ++t) {
-            walk_tile<K>(seq, gs + t * (uint64_t)kTile, ge, [&](int, uint32_t code, bool ok) {
+            walk<K>(seq, m, gs + t * (uint64_t)kTile, ge, kDirectThreads, [&](int, uint32_t code, bool ok) {
                 if (NPASS == 1) {
                     if (ok) atomicAdd(&tab[code], 1u);
                 } else if (ok && (code / SLICE) == (uint32_t)p) {
@@ -179,19 +216,19 @@ __global__ __launch_bounds__(kDirectThreads) void k_direct(const uint8_t* __rest
 template <int K, int TPB, int ABL>
 __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ seq,
                                                    GenomeMap m, uint16_t* __restrict__ suf,
-                                                   uint16_t* __restrict__ toff) {
+                                                   uint16_t* __restrict__ toff, uint32_t ldt) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int TS = toff_stride<K>();
     constexpr int TILE = TPB * kTileBpt;
     static_assert(NBK <= TPB, "one scan element per thread");
-    __shared__ __attribute__((aligned(16))) uint16_t sorted[TILE];
+    constexpr int CAP = tile_cap<K>(TILE);
+    __shared__ __attribute__((aligned(16))) uint16_t sorted[CAP];
     __shared__ uint32_t cnt[NBK];
     __shared__ uint32_t cur[NBK];
     __shared__ uint32_t wsum[TPB / 64];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t lt = blockIdx.x;
-    const uint64_t gt = m.tile_lo + lt;
+    const uint64_t lt = xcd_work_id();  // neighbouring tiles on one XCD: their toff
+    const uint64_t gt = m.tile_lo + lt; // stores combine in that XCD's L2
     const int g = find_genome(m, gt);
     const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)TILE;
     const uint64_t ge = m.goff[g + 1];
@@ -200,14 +237,15 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
     __syncthreads();
 
     uint32_t km[kTileBpt];
-    walk_tile<K>(seq, tstart, ge, [&](int j, uint32_t code, bool ok) {
+    walk<K>(seq, m, tstart, ge, TPB, [&](int j, uint32_t code, bool ok) {
         km[j] = ok ? code : 0xFFFFFFFFu;
         if (!(ABL & 1) && ok) atomicAdd(&cnt[code >> kSubBits], 1u);
     });
     __syncthreads();
 
     // Exclusive scan of the bucket histogram -> bucket starts.
-    const uint32_t v = tid < NBK ? cnt[tid] : 0u;
+    const uint32_t nb = tid < NBK ? cnt[tid] : 0u;  // entries of bucket tid
+    const uint32_t v = (nb + 7u) & ~7u;              // padded to whole chunks
     uint32_t incl = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -222,12 +260,14 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
         pre += (w < wave) ? wsum[w] : 0u;
         total += wsum[w];
     }
-    uint16_t* trow = toff + lt * (uint64_t)TS;
+    // toff, bucket-major [NBK + 1][ldt]: chunk index of every bucket's segment in this
+    // tile, then the tile's total chunk count (a count workgroup reads one row).
+    const uint32_t start = pre + incl - v;
     if (tid < NBK) {
-        cur[tid] = pre + incl - v;
-        trow[tid] = (uint16_t)(pre + incl - v);
+        cur[tid] = start;
+        toff[(uint64_t)tid * ldt + lt] = (uint16_t)(start >> 3);
     }
-    if (tid == 0) trow[NBK] = (uint16_t)total;
+    if (tid == 0) toff[(uint64_t)NBK * ldt + lt] = (uint16_t)(total >> 3);
     __syncthreads();
 
     // Scatter 15-bit suffixes into bucket order.
@@ -236,10 +276,14 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
         for (int j = 0; j < kTileBpt; ++j) {
             const uint32_t c = km[j];
             if (c != 0xFFFFFFFFu) {
-                const uint32_t slot = atomicAdd(&cur[c >> kSubBits], 1u) & (TILE - 1);
+                uint32_t slot = atomicAdd(&cur[c >> kSubBits], 1u);
+                if (ABL & 1) slot %= (uint32_t)CAP;  // synthetic starts may overrun
                 sorted[slot] = (uint16_t)(c & (kSubBins - 1));
             }
         }
+        if (tid < NBK)  // pad the bucket's segment to its chunk boundary
+            for (uint32_t q = start + nb; q < start + v; ++q)
+                sorted[q] = (uint16_t)(kPadBase + ((8u * (uint32_t)tid + q) & (kPadBins - 1)));
     } else {
 #pragma unroll
         for (int j = 0; j < kTileBpt; ++j) asm volatile("" ::"v"(km[j]));
@@ -247,41 +291,41 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
     __syncthreads();
 
     if (!(ABL & 4)) {
-        uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)TILE);
+        uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)CAP);
         const uint4* src = reinterpret_cast<const uint4*>(sorted);
-        const uint32_t nchunk = (total + 7u) >> 3;
+        const uint32_t nchunk = total >> 3;
         for (uint32_t c = tid; c < nchunk; c += TPB) dst[c] = src[c];
     }
 }
 
-// Count one 15-bit suffix stream chunk of 8 entries (a 16-byte load) whose entry
-// indices are [c, c + 8); only entries inside [s0, e0) belong to this bucket.
-__device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t c, uint32_t s0,
-                                            uint32_t e0) {
+// Add one 16-byte chunk (8 suffixes) into the LDS table; padding entries land in the
+// dummy bins past kSubBins.
+__device__ __forceinline__ void count8(uint32_t* tbl, uint4 q) {
     const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t idx = c + (uint32_t)i;
-        if (idx >= s0 && idx < e0) atomicAdd(&tbl[(wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu], 1u);
-    }
+    for (int i = 0; i < 8; ++i) atomicAdd(&tbl[(wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu], 1u);
 }
 
 // One workgroup per (genome, bucket[, split]): gathers the bucket's segment from every
 // tile of the genome into a 32768-bin LDS histogram, then writes the row slice once.
-// The tiles' segment bounds are staged in LDS first (kSegStage tiles at a time), so the
-// suffix loads do not wait behind dependent offset loads; each group of GS lanes covers
-// one segment and U tiles' loads are issued before their LDS atomics.
-// Ablation bits (experiments only): 1 = no LDS atomics, 2 = no suffix loads.
+// Each wave takes 64 tiles at a time (one per lane; their segment bounds are consecutive
+// u16s of the bucket-major offset table), prefix-sums their chunk counts and lists every
+// chunk in a per-wave LDS queue; the queue is then streamed with all 64 lanes active:
+// U coalesced 16-byte loads in flight per lane, 8 LDS atomics per load.  A batch whose
+// chunks overflow the queue (skewed input) is walked lane by lane instead.
+// Ablation bits (experiments only): 1 = no LDS atomics, 2 = no suffix loads, 4 = no main
+// loop (table zeroing, offset reads and the row store only).
 template <int K, int GS, int U, int TILE, int ABL>
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
-    const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, GenomeMap m, int S,
-    uint32_t* __restrict__ out) {
+    const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, uint32_t ldt,
+    GenomeMap m, int S, uint32_t* __restrict__ out) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int TS = toff_stride<K>();
-    constexpr int NGRP = kCountThreads / GS;
-    constexpr uint32_t ROW = GS * 8u;  // entries covered by one load of every lane of a group
-    __shared__ __attribute__((aligned(16))) uint32_t tbl[kSubBins];
-    __shared__ uint32_t seg[kSegStage];
+    constexpr int CAP = tile_cap<K>(TILE);
+    constexpr uint32_t CPT = CAP / 8;            // chunks per tile in the suffix buffer
+    constexpr int NW = kCountThreads / 64;
+    constexpr int QMAX = U * 64;                 // queue entries per wave: one load round
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[kSubBins + kPadBins];
+    __shared__ uint32_t queue[NW][QMAX];
 
     const uint32_t w = xcd_work_id();
     const int s = (int)(w % (uint32_t)S);
@@ -290,55 +334,69 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint64_t t0 = m.tbase[g] - m.tile_lo, nt = m.tbase[g + 1] - m.tbase[g];
     const uint64_t ta = t0 + nt * (uint64_t)s / (uint64_t)S;
     const uint64_t tb = t0 + nt * (uint64_t)(s + 1) / (uint64_t)S;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint4* chunks = reinterpret_cast<const uint4*>(suf);
 
     uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
-    for (int i = threadIdx.x; i < kSubBins / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = threadIdx.x; i < (kSubBins + (int)kPadBins) / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
 
-    const int grp = threadIdx.x / GS;
-    const uint32_t r8 = (uint32_t)(threadIdx.x % GS) * 8u;
-    for (uint64_t c0 = ta; c0 < tb; c0 += kSegStage) {
-        const int n = (int)((tb - c0) < (uint64_t)kSegStage ? (tb - c0) : (uint64_t)kSegStage);
-        __syncthreads();  // previous stage fully consumed (and the table zeroed)
-        for (int i = threadIdx.x; i < n; i += kCountThreads) {
-            const uint16_t* row = toff + (c0 + (uint64_t)i) * TS;
-            seg[i] = (uint32_t)row[b] | ((uint32_t)row[b + 1] << 16);
+    uint32_t* q = queue[wave];
+    // segment bounds of this lane's tile in batch tw (prefetched one batch ahead)
+    auto bounds = [&](uint64_t tw, uint32_t& lo, uint32_t& hi) {
+        const uint64_t t = tw + (uint64_t)lane;
+        lo = t < tb ? toff[(uint64_t)b * ldt + t] : 0u;
+        hi = t < tb ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
+    };
+    uint32_t lo_n, hi_n;
+    uint64_t tw = ta + (uint64_t)wave * 64;
+    if (tw < tb) bounds(tw, lo_n, hi_n);
+    for (; tw < tb; tw += (uint64_t)NW * 64) {
+        const uint32_t lo = lo_n, nc = hi_n - lo_n;
+        if (ABL & 4) {
+            asm volatile("" ::"v"(nc));
+            if (tw + (uint64_t)NW * 64 < tb) bounds(tw + (uint64_t)NW * 64, lo_n, hi_n);
+            continue;
         }
-        __syncthreads();
-        for (int base = grp; base < n; base += NGRP * U) {
-            uint4 q0[U], q1[U];
-            uint32_t lo[U], hi[U], cc[U];
+        uint32_t incl = nc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        const uint32_t cbase = (uint32_t)(tw + (uint64_t)lane) * CPT + lo;  // segment's first chunk
+        if (total <= (uint32_t)QMAX) {
+            const uint32_t ex = incl - nc;
+            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = cbase + j;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int i = base + u * NGRP;
-                const uint32_t sv = i < n ? seg[i] : 0u;
-                lo[u] = sv & 0xFFFFu;
-                hi[u] = sv >> 16;
-                cc[u] = (lo[u] & ~7u) + r8;
-                const uint16_t* p = suf + (c0 + (uint64_t)(i < n ? i : 0)) * (uint64_t)TILE;
+                const uint32_t e = (uint32_t)(u * 64 + lane);
+                const uint32_t ci = e < total ? q[e] : 0u;  // idle lanes re-read chunk 0
                 if (ABL & 2) {
-                    const uint32_t x = (uint32_t)i * 2654435761u + r8;
-                    q0[u] = make_uint4(x, x * 3u, x * 5u, x * 7u);
-                    q1[u] = make_uint4(x * 11u, x * 13u, x * 17u, x * 19u);
+                    const uint32_t x = ci * 2654435761u;
+                    v[u] = make_uint4(x & 0x7FFF7FFFu, (x * 3u) & 0x7FFF7FFFu, (x * 5u) & 0x7FFF7FFFu, (x * 7u) & 0x7FFF7FFFu);
                 } else {
-                    q0[u] = cc[u] < hi[u] ? *reinterpret_cast<const uint4*>(p + cc[u]) : make_uint4(0u, 0u, 0u, 0u);
-                    q1[u] = cc[u] + ROW < hi[u] ? *reinterpret_cast<const uint4*>(p + cc[u] + ROW)
-                                                : make_uint4(0u, 0u, 0u, 0u);
+                    v[u] = chunks[ci];
                 }
             }
+            // next batch's bounds load behind this batch's data loads
+            if (tw + (uint64_t)NW * 64 < tb) bounds(tw + (uint64_t)NW * 64, lo_n, hi_n);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if (ABL & 1) {
-                    asm volatile("" ::"v"(q0[u].x ^ q0[u].y ^ q0[u].z ^ q0[u].w ^ q1[u].x ^ q1[u].y ^ q1[u].z ^ q1[u].w));
-                    continue;
-                }
-                count_chunk(tbl, q0[u], cc[u], lo[u], hi[u]);
-                count_chunk(tbl, q1[u], cc[u] + ROW, lo[u], hi[u]);
-                // long segments (skewed input): the rest, one row at a time
-                const int i = base + u * NGRP;
-                const uint16_t* p = suf + (c0 + (uint64_t)(i < n ? i : 0)) * (uint64_t)TILE;
-                for (uint32_t c = cc[u] + 2 * ROW; c < hi[u]; c += ROW)
-                    count_chunk(tbl, *reinterpret_cast<const uint4*>(p + c), c, lo[u], hi[u]);
+                if (ABL & 1) asm volatile("" ::"v"(v[u].x ^ v[u].y ^ v[u].z ^ v[u].w));
+                else if ((uint32_t)(u * 64 + lane) < total) count8(tbl, v[u]);
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            if (tw + (uint64_t)NW * 64 < tb) bounds(tw + (uint64_t)NW * 64, lo_n, hi_n);
+            for (uint32_t j = 0; j < nc; ++j) count8(tbl, chunks[cbase + j]);
         }
     }
     __syncthreads();
@@ -365,10 +423,10 @@ __global__ __launch_bounds__(kTileThreads) void k_first(const uint8_t* __restric
     const uint64_t gs = m.goff[g];
     const uint64_t rel = (gt - m.tbase[g]) * (uint64_t)kTile + (uint64_t)threadIdx.x * kTileBpt;
     uint32_t* frow = first + (uint64_t)g * (1ull << (2 * K));
-    walk_tile<K>(seq, gs + (gt - m.tbase[g]) * (uint64_t)kTile, m.goff[g + 1],
-                 [&](int j, uint32_t code, bool ok) {
-                     if (ok) atomicMin(&frow[code], (uint32_t)(rel + (uint64_t)j));
-                 });
+    walk<K>(seq, m, gs + (gt - m.tbase[g]) * (uint64_t)kTile, m.goff[g + 1], kTileThreads,
+            [&](int j, uint32_t code, bool ok) {
+                if (ok) atomicMin(&frow[code], (uint32_t)(rel + (uint64_t)j));
+            });
 }
 
 // ---------------------------------------------------------------- synthetic genomes
@@ -461,7 +519,7 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
     if (maxt == 0) return KMH_OK;
     const uint64_t want = (2 * (uint64_t)kTargetWorkgroups + G - 1) / G;
     const int S = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, maxt));
-    GenomeMap m{d_goff, d_tbase, 0, G, 0};
+    GenomeMap m{d_goff, d_tbase, 0, G, 0, L.goff[G]};
     time_begin(ctx, s, "k_direct");
     hipLaunchKernelGGL(k_direct<K>, dim3((unsigned)(G * S)), dim3(kDirectThreads), 0, s, d_seq,
                        m, S, d_out);
@@ -470,21 +528,22 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
     return KMH_OK;
 }
 
-template <int K, int TPB, int PABL, int CABL>
+template <int K, int TPB, int PABL, int CABL, int GSX = 0, int UX = 0>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int TS = toff_stride<K>();
     constexpr int TILE = TPB * kTileBpt;
-    constexpr int GS0 = TILE / NBK / 8;   // lanes per segment: one 16-B load each
-    constexpr int GS = GS0 < 1 ? 1 : (GS0 > 64 ? 64 : GS0);
-    constexpr int U = 4;                  // tiles in flight per lane group
+    constexpr int CAP = tile_cap<K>(TILE);
+    constexpr int GS0 = TILE / NBK / 8;   // lanes per segment: one 16-B chunk each
+    constexpr int GS1 = GS0 < 1 ? 1 : (GS0 > 64 ? 64 : GS0);
+    constexpr int GS = GSX ? GSX : GS1;
+    constexpr int U = UX ? UX : 6;        // chunk loads in flight per lane (queue = 64 U)
     const size_t row = (size_t)1 << (2 * K);
     // Genomes per batch: keep the suffix buffer of one batch within the budget (it is
     // written and re-read, so a budget inside the 256 MiB Infinity Cache can keep it
     // on-die).  KMH_SUF_BUDGET_MB overrides.
     const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 256) << 20;
-    const size_t tile_bytes = (size_t)TILE * sizeof(uint16_t);
+    const size_t tile_bytes = (size_t)CAP * sizeof(uint16_t);
     uint64_t max_batch_tiles = 0;
     {
         int g = 0;
@@ -501,7 +560,8 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
     }
     int rc = ensure(ctx, ctx->suf, std::max<uint64_t>(max_batch_tiles, 1) * tile_bytes);
     if (rc) return rc;
-    rc = ensure(ctx, ctx->toff, std::max<uint64_t>(max_batch_tiles, 1) * TS * sizeof(uint16_t));
+    const uint32_t ldt = (uint32_t)((std::max<uint64_t>(max_batch_tiles, 1) + 63) / 64 * 64);
+    rc = ensure(ctx, ctx->toff, (size_t)ldt * (NBK + 1) * sizeof(uint16_t));
     if (rc) return rc;
     uint16_t* suf = static_cast<uint16_t*>(ctx->suf.ptr);
     uint16_t* toff = static_cast<uint16_t*>(ctx->toff.ptr);
@@ -515,7 +575,7 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
             ++h;
         } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget);
         const int nG = h - g;
-        GenomeMap m{d_goff, d_tbase, g, h, L.tbase[g]};
+        GenomeMap m{d_goff, d_tbase, g, h, L.tbase[g], L.goff[G]};
         uint64_t maxt = 0;
         for (int q = g; q < h; ++q) maxt = std::max<uint64_t>(maxt, L.tbase[q + 1] - L.tbase[q]);
         const uint64_t want = ((uint64_t)kTargetWorkgroups + (uint64_t)nG * NBK - 1) / ((uint64_t)nG * NBK);
@@ -524,13 +584,13 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
         if (tiles) {
             time_begin(ctx, s, "k_partition");
             hipLaunchKernelGGL((k_partition<K, TPB, PABL>), dim3((unsigned)tiles), dim3(TPB), 0, s,
-                               d_seq, m, suf, toff);
+                               d_seq, m, suf, toff, ldt);
             time_end(ctx, s);
             KMH_HIP(ctx, hipGetLastError());
         }
         time_begin(ctx, s, "k_bucket_count");
         hipLaunchKernelGGL((k_bucket_count<K, GS, U, TILE, CABL>), dim3((unsigned)(nG * NBK * S)),
-                           dim3(kCountThreads), 0, s, suf, toff, m, S, d_out);
+                           dim3(kCountThreads), 0, s, suf, toff, ldt, m, S, d_out);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
         g = h;
@@ -565,8 +625,15 @@ int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
                 if (pa == 4) return run_partitioned<K, 512, 4, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
                 if (ca == 1) return run_partitioned<K, 512, 0, 1>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
                 if (ca == 2) return run_partitioned<K, 512, 0, 2>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 4) return run_partitioned<K, 512, 0, 4>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 3) return run_partitioned<K, 512, 0, 3>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
                 return fail(ctx, KMH_ERR_INVALID, "unknown ablation");
             }
+        }
+        if constexpr (K == 12) {  // loads-in-flight sweep (experiments): KMH_GSU = U
+            const int gsu = (int)env_mb("KMH_GSU", 0);
+            if (tpb == 512 && gsu == 4) return run_partitioned<K, 512, 0, 0, 0, 4>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+            if (tpb == 512 && gsu == 7) return run_partitioned<K, 512, 0, 0, 0, 7>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
         }
         if (tpb == 1024) return run_partitioned<K, 1024, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
         return run_partitioned<K, 512, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
@@ -584,7 +651,7 @@ int first_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
     const size_t row = (size_t)1 << (2 * K);
     KMH_HIP(ctx, hipMemsetAsync(d_first, 0xFF, row * (size_t)G * sizeof(uint32_t), s));
     if (L.ntiles == 0) return KMH_OK;
-    GenomeMap m{d_goff, d_tbase, 0, G, 0};
+    GenomeMap m{d_goff, d_tbase, 0, G, 0, L.goff[G]};
     time_begin(ctx, s, "k_first");
     hipLaunchKernelGGL(k_first<K>, dim3((unsigned)L.ntiles), dim3(kTileThreads), 0, s, d_seq, m,
                        d_first);

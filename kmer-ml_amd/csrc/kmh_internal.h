@@ -19,7 +19,6 @@ constexpr int kTile = kTileThreads * kTileBpt;         // 32768 window starts pe
 constexpr int kSubBits = 15;                           // bins owned by one count workgroup
 constexpr int kSubBins = 1 << kSubBits;                // 32768 u32 = 128 KiB of LDS
 constexpr int kCountThreads = 1024;                    // threads of a bucket-count workgroup
-constexpr int kSegStage = 4096;                        // tiles whose offsets a count workgroup stages in LDS
 constexpr int kDirectMaxK = 7;                         // k <= 7: whole table in LDS
 
 // A growable device allocation owned by a context.
