@@ -50,3 +50,10 @@ $(LDSBENCH): tests/native/lds_bench.hip
 	@mkdir -p $(OUTDIR)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 .PHONY: ldsbench
+
+MALLBENCH := $(OUTDIR)/mall_bench
+mallbench: $(MALLBENCH)
+$(MALLBENCH): tests/native/mall_bench.hip
+	@mkdir -p $(OUTDIR)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+.PHONY: mallbench

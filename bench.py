@@ -47,9 +47,13 @@ def parse():
     p.add_argument("--genomes", type=int, default=64, help="total genomes over all ranks")
     p.add_argument("--genome-len", type=int, default=100_000_000)
     p.add_argument("--assemble", choices=["auto", "allgather", "none"], default="auto")
-    p.add_argument("--cpu-sample", type=int, default=4_000_000,
+    p.add_argument("--cpu-sample", type=int, default=16_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
     p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="process-group backend (gloo + --single-device: multi-rank logic check on one GPU)")
+    p.add_argument("--single-device", action="store_true",
+                   help="map every rank to cuda:0 (validation only; never used for reported numbers)")
     return p.parse_args()
 
 
@@ -100,10 +104,14 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = 0 if a.single_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
     k, G, L = a.k, a.genomes, a.genome_len
     lo, hi = (G * rank) // world, (G * (rank + 1)) // world
     g_local = hi - lo
@@ -116,7 +124,7 @@ def main():
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         cpu = cpu_baseline(a.cpu_sample, k)
 
-    ctx = _native.context(local_rank)
+    ctx = _native.context(dev_index)
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream
     stride = (L + 15) // 16 * 16   # genome starts 16-byte aligned; any gap is 'N' (not a base)
@@ -141,7 +149,12 @@ def main():
             e1.record(stream)
             t_count.append((e0, e1))
         if assemble:
-            dist.all_gather_into_tensor(full, local)
+            if a.backend == "nccl":
+                dist.all_gather_into_tensor(full, local)
+            else:  # gloo validation path: host staging
+                host = torch.empty((world * B, bins), dtype=torch.int32)
+                dist.all_gather_into_tensor(host, local.cpu())
+                full.copy_(host)
 
     for _ in range(a.warmup):
         step()
@@ -162,7 +175,8 @@ def main():
     ctx.timing(False)
     count_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in t_count]))
     if world > 1:
-        t = torch.tensor([elapsed, count_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, count_ms], dtype=torch.float64,
+                         device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, count_ms = float(t[0]), float(t[1])
 

@@ -139,7 +139,7 @@ void kmh_ctx_destroy(kmh_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    for (kmh::DevBuf* b : {&ctx->seq, &ctx->suf, &ctx->toff, &ctx->meta, &ctx->out, &ctx->out2})
+    for (kmh::DevBuf* b : {&ctx->seq, &ctx->suf, &ctx->toff, &ctx->meta, &ctx->out, &ctx->out2, &ctx->fix})
         if (b->ptr) (void)hipFree(b->ptr);
     for (auto& b : ctx->sparse)
         if (b.ptr) (void)hipFree(b.ptr);
@@ -150,6 +150,9 @@ void kmh_ctx_destroy(kmh_ctx* ctx) {
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (auto e : ctx->pipe_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -47,6 +47,18 @@ constexpr int num_buckets() { return 1 << (2 * K - kSubBits); }
 template <int K>
 constexpr int tile_cap(int tile) { return tile + num_buckets<K>() * 7; }
 constexpr uint32_t kPadBase = (uint32_t)kSubBins;
+
+// Tiles per wave batch of the count kernels: the expected chunks of a batch must fit the
+// per-wave queue of qmax entries (a batch that overflows it is walked lane by lane).
+template <int K>
+constexpr int batch_tiles(int tile, int qmax) {
+    const int per = tile / num_buckets<K>() / 8 + 1;       // expected chunks per segment
+    int bt = qmax / per;
+    bt = bt < 1 ? 1 : (bt > 64 ? 64 : bt);
+    int p2 = 1;
+    while (p2 * 2 <= bt) p2 *= 2;
+    return p2;
+}
 constexpr uint32_t kPadBins = 64;
 
 // Largest g in [g0, g1) with tbase[g] <= gt (genomes without tiles are skipped).
@@ -213,12 +225,13 @@ __global__ __launch_bounds__(kDirectThreads) void k_direct(const uint8_t* __rest
 // ---------------------------------------------------------------- k >= 10: partition
 // Ablation bits (experiments only; outputs are wrong when set): 1 = no histogram atomics
 // (synthetic uniform bucket starts), 2 = no scatter, 4 = no write-out.
-template <int K, int TPB, int ABL>
+// SUBT sub-tiles of TPB * 32 windows form one tile (longer bucket segments).
+template <int K, int TPB, int ABL, int SUBT = 1>
 __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ seq,
                                                    GenomeMap m, uint16_t* __restrict__ suf,
                                                    uint16_t* __restrict__ toff, uint32_t ldt) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int TILE = TPB * kTileBpt;
+    constexpr int TILE = TPB * kTileBpt * SUBT;
     static_assert(NBK <= TPB, "one scan element per thread");
     constexpr int CAP = tile_cap<K>(TILE);
     __shared__ __attribute__((aligned(16))) uint16_t sorted[CAP];
@@ -236,11 +249,14 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
     for (int b = tid; b < NBK; b += TPB) cnt[b] = (ABL & 1) ? (uint32_t)(TILE / NBK) : 0u;
     __syncthreads();
 
-    uint32_t km[kTileBpt];
-    walk<K>(seq, m, tstart, ge, TPB, [&](int j, uint32_t code, bool ok) {
-        km[j] = ok ? code : 0xFFFFFFFFu;
-        if (!(ABL & 1) && ok) atomicAdd(&cnt[code >> kSubBits], 1u);
-    });
+    uint32_t km[kTileBpt * SUBT];
+#pragma unroll
+    for (int sub = 0; sub < SUBT; ++sub) {
+        walk<K>(seq, m, tstart + (uint64_t)sub * TPB * kTileBpt, ge, TPB, [&](int j, uint32_t code, bool ok) {
+            km[sub * kTileBpt + j] = ok ? code : 0xFFFFFFFFu;
+            if (!(ABL & 1) && ok) atomicAdd(&cnt[code >> kSubBits], 1u);
+        });
+    }
     __syncthreads();
 
     // Exclusive scan of the bucket histogram -> bucket starts.
@@ -273,7 +289,7 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
     // Scatter 15-bit suffixes into bucket order.
     if (!(ABL & 2)) {
 #pragma unroll
-        for (int j = 0; j < kTileBpt; ++j) {
+        for (int j = 0; j < kTileBpt * SUBT; ++j) {
             const uint32_t c = km[j];
             if (c != 0xFFFFFFFFu) {
                 uint32_t slot = atomicAdd(&cur[c >> kSubBits], 1u);
@@ -286,7 +302,7 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
                 sorted[q] = (uint16_t)(kPadBase + ((8u * (uint32_t)tid + q) & (kPadBins - 1)));
     } else {
 #pragma unroll
-        for (int j = 0; j < kTileBpt; ++j) asm volatile("" ::"v"(km[j]));
+        for (int j = 0; j < kTileBpt * SUBT; ++j) asm volatile("" ::"v"(km[j]));
     }
     __syncthreads();
 
@@ -315,7 +331,7 @@ __device__ __forceinline__ void count8(uint32_t* tbl, uint4 q) {
 // chunks overflow the queue (skewed input) is walked lane by lane instead.
 // Ablation bits (experiments only): 1 = no LDS atomics, 2 = no suffix loads, 4 = no main
 // loop (table zeroing, offset reads and the row store only).
-template <int K, int GS, int U, int TILE, int ABL>
+template <int K, int GS, int U, int TILE, int ABL, int PIPE>
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, uint32_t ldt,
     GenomeMap m, int S, uint32_t* __restrict__ out) {
@@ -341,62 +357,147 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     for (int i = threadIdx.x; i < (kSubBins + (int)kPadBins) / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
 
-    uint32_t* q = queue[wave];
-    // segment bounds of this lane's tile in batch tw (prefetched one batch ahead)
-    auto bounds = [&](uint64_t tw, uint32_t& lo, uint32_t& hi) {
-        const uint64_t t = tw + (uint64_t)lane;
-        lo = t < tb ? toff[(uint64_t)b * ldt + t] : 0u;
-        hi = t < tb ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
-    };
-    uint32_t lo_n, hi_n;
-    uint64_t tw = ta + (uint64_t)wave * 64;
-    if (tw < tb) bounds(tw, lo_n, hi_n);
-    for (; tw < tb; tw += (uint64_t)NW * 64) {
-        const uint32_t lo = lo_n, nc = hi_n - lo_n;
-        if (ABL & 4) {
-            asm volatile("" ::"v"(nc));
-            if (tw + (uint64_t)NW * 64 < tb) bounds(tw + (uint64_t)NW * 64, lo_n, hi_n);
-            continue;
-        }
-        uint32_t incl = nc;
+    if constexpr (PIPE) {
+        // Two-stage software pipeline over 32-tile batches: while batch i's loads are in
+        // flight, batch i+1's queue is built and its loads issued; then batch i's atomics.
+        constexpr int BT = 32;                    // tiles per wave batch
+        constexpr int QH = QMAX / 2;              // queue entries per stage (U/2 rounds)
+        constexpr int UH = QH / 64;
+        const uint64_t stride = (uint64_t)NW * BT;
+        auto bounds = [&](uint64_t tw, uint32_t& lo, uint32_t& hi) {
+            const uint64_t t = tw + (uint64_t)lane;
+            const bool in = lane < BT && t < tb;
+            lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
+            hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
+        };
+        // list the chunks of batch tw in queue slot `slot`; returns the chunk count
+        auto build = [&](uint64_t tw, uint32_t lo, uint32_t hi, uint32_t* qs, uint32_t& cb,
+                         uint32_t& nc) -> uint32_t {
+            nc = hi - lo;
+            uint32_t incl = nc;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
-        }
-        const uint32_t total = __shfl(incl, 63);
-        const uint32_t cbase = (uint32_t)(tw + (uint64_t)lane) * CPT + lo;  // segment's first chunk
-        if (total <= (uint32_t)QMAX) {
-            const uint32_t ex = incl - nc;
-            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = cbase + j;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t x = __shfl_up(incl, d);
+                if (lane >= d) incl += x;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            cb = (uint32_t)(tw + (uint64_t)lane) * CPT + lo;
+            if (total <= (uint32_t)QH) {
+                const uint32_t ex = incl - nc;
+                for (uint32_t j = 0; j < nc; ++j) qs[ex + j] = cb + j;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint4 v[U];
+            return total;
+        };
+        auto issue = [&](const uint32_t* qs, uint32_t total, uint4 (&v)[UH]) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
+            for (int u = 0; u < UH; ++u) {
                 const uint32_t e = (uint32_t)(u * 64 + lane);
-                const uint32_t ci = e < total ? q[e] : 0u;  // idle lanes re-read chunk 0
-                if (ABL & 2) {
-                    const uint32_t x = ci * 2654435761u;
-                    v[u] = make_uint4(x & 0x7FFF7FFFu, (x * 3u) & 0x7FFF7FFFu, (x * 5u) & 0x7FFF7FFFu, (x * 7u) & 0x7FFF7FFFu);
-                } else {
-                    v[u] = chunks[ci];
-                }
+                const uint32_t ci = (total <= (uint32_t)QH && e < total) ? qs[e] : 0u;
+                v[u] = chunks[ci];
             }
-            // next batch's bounds load behind this batch's data loads
-            if (tw + (uint64_t)NW * 64 < tb) bounds(tw + (uint64_t)NW * 64, lo_n, hi_n);
+        };
+        auto consume = [&](const uint4 (&v)[UH], uint32_t total, uint32_t cb, uint32_t nc) {
+            if (total <= (uint32_t)QH) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (ABL & 1) asm volatile("" ::"v"(v[u].x ^ v[u].y ^ v[u].z ^ v[u].w));
-                else if ((uint32_t)(u * 64 + lane) < total) count8(tbl, v[u]);
+                for (int u = 0; u < UH; ++u)
+                    if ((uint32_t)(u * 64 + lane) < total) count8(tbl, v[u]);
+            } else {
+                for (uint32_t j = 0; j < nc; ++j) count8(tbl, chunks[cb + j]);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
-            if (tw + (uint64_t)NW * 64 < tb) bounds(tw + (uint64_t)NW * 64, lo_n, hi_n);
-            for (uint32_t j = 0; j < nc; ++j) count8(tbl, chunks[cbase + j]);
+        };
+        uint32_t* qbase = queue[wave];
+        uint64_t tw = ta + (uint64_t)wave * BT;
+        if (tw < tb) {
+            uint32_t lo, hi, lo_n = 0, hi_n = 0;
+            bounds(tw, lo, hi);
+            if (tw + stride < tb) bounds(tw + stride, lo_n, hi_n);
+            uint32_t cb, nc;
+            int slot = 0;
+            uint32_t tot = build(tw, lo, hi, qbase, cb, nc);
+            uint4 v[UH];
+            issue(qbase, tot, v);
+            for (; tw < tb; tw += stride) {
+                const uint64_t twn = tw + stride;
+                uint4 vn[UH];
+                uint32_t tot_n = 0, cb_n = 0, nc_n = 0;
+                uint32_t* qn = qbase + (slot ^ 1) * QH;
+                if (twn < tb) {
+                    tot_n = build(twn, lo_n, hi_n, qn, cb_n, nc_n);
+                    issue(qn, tot_n, vn);
+                    if (twn + stride < tb) bounds(twn + stride, lo_n, hi_n);
+                }
+                consume(v, tot, cb, nc);
+#pragma unroll
+                for (int u = 0; u < UH; ++u) v[u] = vn[u];
+                tot = tot_n;
+                cb = cb_n;
+                nc = nc_n;
+                slot ^= 1;
+            }
+        }
+    } else {
+        constexpr int BT = batch_tiles<K>(TILE, QMAX);
+        uint32_t* q = queue[wave];
+        // segment bounds of this lane's tile in batch tw (prefetched one batch ahead)
+        auto bounds = [&](uint64_t tw, uint32_t& lo, uint32_t& hi) {
+            const uint64_t t = tw + (uint64_t)lane;
+            const bool in = lane < BT && t < tb;
+            lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
+            hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
+        };
+        uint32_t lo_n = 0, hi_n = 0;
+        uint64_t tw = ta + (uint64_t)wave * BT;
+        if (tw < tb) bounds(tw, lo_n, hi_n);
+        for (; tw < tb; tw += (uint64_t)NW * BT) {
+            const uint32_t lo = lo_n, nc = hi_n - lo_n;
+            if (ABL & 4) {
+                asm volatile("" ::"v"(nc));
+                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+                continue;
+            }
+            uint32_t incl = nc;
+    #pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t x = __shfl_up(incl, d);
+                if (lane >= d) incl += x;
+            }
+            const uint32_t total = __shfl(incl, 63);
+            const uint32_t cbase = (uint32_t)(tw + (uint64_t)lane) * CPT + lo;  // segment's first chunk
+            if (total <= (uint32_t)QMAX) {
+                const uint32_t ex = incl - nc;
+                for (uint32_t j = 0; j < nc; ++j) q[ex + j] = cbase + j;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint4 v[U];
+    #pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t e = (uint32_t)(u * 64 + lane);
+                    const uint32_t ci = e < total ? q[e] : 0u;  // idle lanes re-read chunk 0
+                    if (ABL & 2) {
+                        const uint32_t x = ci * 2654435761u;
+                        v[u] = make_uint4(x & 0x7FFF7FFFu, (x * 3u) & 0x7FFF7FFFu, (x * 5u) & 0x7FFF7FFFu, (x * 7u) & 0x7FFF7FFFu);
+                    } else {
+                        v[u] = chunks[ci];
+                    }
+                }
+                // next batch's bounds load behind this batch's data loads
+                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+    #pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (ABL & 1) asm volatile("" ::"v"(v[u].x ^ v[u].y ^ v[u].z ^ v[u].w));
+                    else if ((uint32_t)(u * 64 + lane) < total) count8(tbl, v[u]);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else {
+                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+                for (uint32_t j = 0; j < nc; ++j) count8(tbl, chunks[cbase + j]);
+            }
         }
     }
     __syncthreads();
@@ -410,6 +511,149 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             const uint32_t x = tbl[i];
             if (x) atomicAdd(&orow[i], x);
         }
+    }
+}
+
+// ---------------------------------------------------------------- u16 count tables
+// Bins are packed two per 32-bit LDS word (bin v in half v & 1 of word v >> 1), halving
+// the table so that two count workgroups -- or a count and a partition workgroup -- fit on
+// one CU.  Exactness: every wrap of a 16-bit half is seen by exactly one ds_add_rtn (the
+// adds to a word are serialised), which appends a correction to a global log:
+//   low add, old low == 0xFFFF:  bin v += 65536, and its partner v ^ 1 got a carry: -= 1;
+//                                if old high == 0xFFFF too, the carry wrapped it: += 65536
+//   high add, old high == 0xFFFF: bin v += 65536
+// so for every bin: count = stored half + sum of its logged corrections (mod 2^32), applied
+// by k_fixup after the count kernel.  Random genomes never wrap; the log stays empty.
+struct FixLog {
+    unsigned long long* entries;  // (row index << 1) | (1 = "-1", 0 = "+65536")
+    uint32_t* cursor;
+    uint32_t cap;
+};
+
+__device__ __forceinline__ void log_fix(const FixLog& L, uint64_t idx, uint32_t minus_one) {
+    const uint32_t at = atomicAdd(L.cursor, 1u);
+    if (at < L.cap) L.entries[at] = (idx << 1) | minus_one;
+}
+
+__device__ __forceinline__ void count8_u16(uint32_t* tbl, uint4 q, const FixLog& L,
+                                           uint64_t row0) {
+    const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t v = (wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        const uint32_t hi = v & 1u;
+        const uint32_t old = atomicAdd(&tbl[v >> 1], hi ? 0x10000u : 1u);
+        const bool wrap = hi ? (old >> 16) == 0xFFFFu : (old & 0xFFFFu) == 0xFFFFu;
+        if (wrap && v < kPadBase) {  // rare: log the corrections
+            log_fix(L, row0 + v, 0u);
+            if (!hi) {
+                log_fix(L, row0 + (v ^ 1u), 1u);
+                if ((old >> 16) == 0xFFFFu) log_fix(L, row0 + (v ^ 1u), 0u);
+            }
+        }
+    }
+}
+
+// Same work decomposition as k_bucket_count (per-wave chunk queue), NT threads, u16 table.
+template <int K, int U, int TILE, int NT>
+__global__ __launch_bounds__(NT) void k_bucket_count16(
+    const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, uint32_t ldt,
+    GenomeMap m, int S, uint32_t* __restrict__ out, FixLog L) {
+    constexpr int NBK = num_buckets<K>();
+    constexpr int CAP = tile_cap<K>(TILE);
+    constexpr uint32_t CPT = CAP / 8;
+    constexpr int NW = NT / 64;
+    constexpr int QMAX = U * 64;
+    constexpr int WORDS = (kSubBins + (int)kPadBins) / 2;
+    __shared__ __attribute__((aligned(16))) uint32_t tbl[WORDS];
+    __shared__ uint32_t queue[NW][QMAX];
+
+    const uint32_t w = xcd_work_id();
+    const int s = (int)(w % (uint32_t)S);
+    const uint32_t b = (w / (uint32_t)S) % NBK;
+    const int g = m.g0 + (int)(w / ((uint32_t)S * NBK));
+    const uint64_t t0 = m.tbase[g] - m.tile_lo, nt = m.tbase[g + 1] - m.tbase[g];
+    const uint64_t ta = t0 + nt * (uint64_t)s / (uint64_t)S;
+    const uint64_t tb = t0 + nt * (uint64_t)(s + 1) / (uint64_t)S;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint4* chunks = reinterpret_cast<const uint4*>(suf);
+    const uint64_t row0 = (uint64_t)g * (1ull << (2 * K)) + (uint64_t)b * kSubBins;
+
+    uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
+    for (int i = threadIdx.x; i < WORDS / 4; i += NT) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+
+    constexpr int BT = batch_tiles<K>(TILE, QMAX);
+    uint32_t* q = queue[wave];
+    auto bounds = [&](uint64_t tw, uint32_t& lo, uint32_t& hi) {
+        const uint64_t t = tw + (uint64_t)lane;
+        const bool in = lane < BT && t < tb;
+        lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
+        hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
+    };
+    uint32_t lo_n = 0, hi_n = 0;
+    uint64_t tw = ta + (uint64_t)wave * BT;
+    if (tw < tb) bounds(tw, lo_n, hi_n);
+    for (; tw < tb; tw += (uint64_t)NW * BT) {
+        const uint32_t lo = lo_n, nc = hi_n - lo_n;
+        uint32_t incl = nc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        const uint32_t cbase = (uint32_t)(tw + (uint64_t)lane) * CPT + lo;
+        if (total <= (uint32_t)QMAX) {
+            const uint32_t ex = incl - nc;
+            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = cbase + j;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t e = (uint32_t)(u * 64 + lane);
+                v[u] = chunks[e < total ? q[e] : 0u];
+            }
+            if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if ((uint32_t)(u * 64 + lane) < total) count8_u16(tbl, v[u], L, row0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+            for (uint32_t j = 0; j < nc; ++j) count8_u16(tbl, chunks[cbase + j], L, row0);
+        }
+    }
+    __syncthreads();
+
+    // Expand u16 pairs to the u32 row (plain stores, or adds when split).
+    uint32_t* orow = out + row0;
+    for (int i = threadIdx.x; i < kSubBins / 8; i += NT) {
+        const uint4 x = tbl4[i];
+        const uint4 lo4 = make_uint4(x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16);
+        const uint4 hi4 = make_uint4(x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16);
+        if (S == 1) {
+            reinterpret_cast<uint4*>(orow)[2 * i] = lo4;
+            reinterpret_cast<uint4*>(orow)[2 * i + 1] = hi4;
+        } else if (ta < tb) {
+            const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (e[j]) atomicAdd(&orow[8 * i + j], e[j]);
+        }
+    }
+}
+
+// Apply the logged u16-wrap corrections (usually none).
+__global__ __launch_bounds__(256) void k_fixup(FixLog L, uint32_t* __restrict__ out) {
+    const uint32_t n = min(*L.cursor, L.cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned long long e = L.entries[i];
+        atomicAdd(&out[e >> 1], (e & 1ull) ? 0xFFFFFFFFu : 65536u);
     }
 }
 
@@ -501,6 +745,11 @@ int upload_layout(Ctx* ctx, const Layout& L, hipStream_t s, const uint64_t** d_g
     return KMH_OK;
 }
 
+long env_long(const char* name, long dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atol(v) : dflt;
+}
+
 size_t env_mb(const char* name, size_t dflt) {
     const char* v = std::getenv(name);
     if (!v || !*v) return dflt;
@@ -528,11 +777,11 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
     return KMH_OK;
 }
 
-template <int K, int TPB, int PABL, int CABL, int GSX = 0, int UX = 0>
+template <int K, int TPB, int PABL, int CABL, int GSX = 0, int UX = 0, int PIPE = 0, int SUBT = 1>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int TILE = TPB * kTileBpt;
+    constexpr int TILE = TPB * kTileBpt * SUBT;
     constexpr int CAP = tile_cap<K>(TILE);
     constexpr int GS0 = TILE / NBK / 8;   // lanes per segment: one 16-B chunk each
     constexpr int GS1 = GS0 < 1 ? 1 : (GS0 > 64 ? 64 : GS0);
@@ -558,15 +807,42 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
             g = h;
         }
     }
-    int rc = ensure(ctx, ctx->suf, std::max<uint64_t>(max_batch_tiles, 1) * tile_bytes);
+    // Two suffix/offset buffers: the partition of batch i+1 (side stream) overlaps the
+    // count of batch i (caller's stream).  KMH_OVERLAP=0 runs both on the caller's stream.
+    const bool overlap = env_long("KMH_OVERLAP", 0) != 0;
+    const size_t slot_tiles = std::max<uint64_t>(max_batch_tiles, 1);
+    int rc = ensure(ctx, ctx->suf, 2 * slot_tiles * tile_bytes);
     if (rc) return rc;
-    const uint32_t ldt = (uint32_t)((std::max<uint64_t>(max_batch_tiles, 1) + 63) / 64 * 64);
-    rc = ensure(ctx, ctx->toff, (size_t)ldt * (NBK + 1) * sizeof(uint16_t));
+    const uint32_t ldt = (uint32_t)((slot_tiles + 63) / 64 * 64);
+    const size_t toff_slot = (size_t)ldt * (NBK + 1);
+    rc = ensure(ctx, ctx->toff, 2 * toff_slot * sizeof(uint16_t));
     if (rc) return rc;
-    uint16_t* suf = static_cast<uint16_t*>(ctx->suf.ptr);
-    uint16_t* toff = static_cast<uint16_t*>(ctx->toff.ptr);
+    // u16-packed count tables (KMH_COUNT16=1; KMH_COUNT16_NT=512|1024): half the LDS, same
+    // speed here; kept for co-residency experiments.  Default: the u32 kernel.
+    const bool c16 = env_long("KMH_COUNT16", 0) != 0;
+    const int c16nt = env_long("KMH_COUNT16_NT", 512) == 1024 ? 1024 : 512;
+    FixLog fl{nullptr, nullptr, 0};
+    if (c16) {
+        const uint64_t windows = (uint64_t)L.ntiles * (uint64_t)TILE;
+        const uint64_t cap = 3 * (windows / 65536 + 1) + 64;  // >= every possible wrap event
+        rc = ensure(ctx, ctx->fix, 256 + cap * sizeof(unsigned long long));
+        if (rc) return rc;
+        fl.cursor = static_cast<uint32_t*>(ctx->fix.ptr);
+        fl.entries = reinterpret_cast<unsigned long long*>(static_cast<char*>(ctx->fix.ptr) + 256);
+        fl.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+        KMH_HIP(ctx, hipMemsetAsync(fl.cursor, 0, 256, s));
+    }
+    hipStream_t sp = s;
+    if (overlap) {
+        if (!ctx->side) KMH_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        for (auto& e : ctx->pipe_ev)
+            if (!e) KMH_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        sp = ctx->side;
+        KMH_HIP(ctx, hipEventRecord(ctx->pipe_ev[0], s));  // inputs ready
+        KMH_HIP(ctx, hipStreamWaitEvent(sp, ctx->pipe_ev[0], 0));
+    }
 
-    int g = 0;
+    int g = 0, batch = 0;
     while (g < G) {
         int h = g;
         uint64_t tiles = 0;
@@ -575,25 +851,48 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
             ++h;
         } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget);
         const int nG = h - g;
+        const int slot = overlap ? (batch & 1) : 0;
+        uint16_t* suf = static_cast<uint16_t*>(ctx->suf.ptr) + (size_t)slot * slot_tiles * CAP;
+        uint16_t* toff = static_cast<uint16_t*>(ctx->toff.ptr) + (size_t)slot * toff_slot;
         GenomeMap m{d_goff, d_tbase, g, h, L.tbase[g], L.goff[G]};
         uint64_t maxt = 0;
         for (int q = g; q < h; ++q) maxt = std::max<uint64_t>(maxt, L.tbase[q + 1] - L.tbase[q]);
         const uint64_t want = ((uint64_t)kTargetWorkgroups + (uint64_t)nG * NBK - 1) / ((uint64_t)nG * NBK);
         const int S = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxt, 1)));
         if (S > 1) KMH_HIP(ctx, hipMemsetAsync(d_out + (size_t)g * row, 0, (size_t)nG * row * sizeof(uint32_t), s));
+        if (overlap && batch >= 2) KMH_HIP(ctx, hipStreamWaitEvent(sp, ctx->pipe_ev[3 + slot], 0));
         if (tiles) {
-            time_begin(ctx, s, "k_partition");
-            hipLaunchKernelGGL((k_partition<K, TPB, PABL>), dim3((unsigned)tiles), dim3(TPB), 0, s,
+            time_begin(ctx, sp, "k_partition");
+            hipLaunchKernelGGL((k_partition<K, TPB, PABL, SUBT>), dim3((unsigned)tiles), dim3(TPB), 0, sp,
                                d_seq, m, suf, toff, ldt);
-            time_end(ctx, s);
+            time_end(ctx, sp);
             KMH_HIP(ctx, hipGetLastError());
         }
+        if (overlap) {
+            KMH_HIP(ctx, hipEventRecord(ctx->pipe_ev[1 + slot], sp));
+            KMH_HIP(ctx, hipStreamWaitEvent(s, ctx->pipe_ev[1 + slot], 0));
+        }
         time_begin(ctx, s, "k_bucket_count");
-        hipLaunchKernelGGL((k_bucket_count<K, GS, U, TILE, CABL>), dim3((unsigned)(nG * NBK * S)),
-                           dim3(kCountThreads), 0, s, suf, toff, ldt, m, S, d_out);
+        if (c16 && c16nt == 1024)
+            hipLaunchKernelGGL((k_bucket_count16<K, U, TILE, 1024>), dim3((unsigned)(nG * NBK * S)),
+                               dim3(1024), 0, s, suf, toff, ldt, m, S, d_out, fl);
+        else if (c16)
+            hipLaunchKernelGGL((k_bucket_count16<K, U, TILE, 512>), dim3((unsigned)(nG * NBK * S)),
+                               dim3(512), 0, s, suf, toff, ldt, m, S, d_out, fl);
+        else
+            hipLaunchKernelGGL((k_bucket_count<K, GS, U, TILE, CABL, PIPE>), dim3((unsigned)(nG * NBK * S)),
+                               dim3(kCountThreads), 0, s, suf, toff, ldt, m, S, d_out);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
+        if (overlap) KMH_HIP(ctx, hipEventRecord(ctx->pipe_ev[3 + slot], s));
         g = h;
+        ++batch;
+    }
+    if (c16) {
+        time_begin(ctx, s, "k_fixup");
+        hipLaunchKernelGGL(k_fixup, dim3(64), dim3(256), 0, s, fl, d_out);
+        time_end(ctx, s);
+        KMH_HIP(ctx, hipGetLastError());
     }
     return KMH_OK;
 }
@@ -613,7 +912,10 @@ int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
         // KMH_ABLATE_P / KMH_ABLATE_C select ablation builds (experiments only: wrong
         // counts) -- see the ablation bits of k_partition / k_bucket_count.
         const int tpb = (int)env_mb("KMH_TPB", 512) == 1024 ? 1024 : 512;
-        int rc = make_layout(ctx, offsets, G, K, (uint64_t)tpb * kTileBpt, L);
+        // k = 12: two 16384-window sub-tiles per partition tile (64-entry segments) unless
+        // KMH_SUBT=1.
+        const int subt = (K == 12 && tpb == 512 && env_long("KMH_SUBT", 2) == 2) ? 2 : 1;
+        int rc = make_layout(ctx, offsets, G, K, (uint64_t)tpb * kTileBpt * subt, L);
         if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
         if (rc) return rc;
         if constexpr (K == 12) {
@@ -623,17 +925,20 @@ int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
                 if (pa == 1) return run_partitioned<K, 512, 1, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
                 if (pa == 2) return run_partitioned<K, 512, 2, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
                 if (pa == 4) return run_partitioned<K, 512, 4, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-                if (ca == 1) return run_partitioned<K, 512, 0, 1>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-                if (ca == 2) return run_partitioned<K, 512, 0, 2>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-                if (ca == 4) return run_partitioned<K, 512, 0, 4>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-                if (ca == 3) return run_partitioned<K, 512, 0, 3>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 1) return run_partitioned<K, 512, 0, 1, 0, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 2) return run_partitioned<K, 512, 0, 2, 0, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 4) return run_partitioned<K, 512, 0, 4, 0, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+                if (ca == 3) return run_partitioned<K, 512, 0, 3, 0, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
                 return fail(ctx, KMH_ERR_INVALID, "unknown ablation");
             }
         }
-        if constexpr (K == 12) {  // loads-in-flight sweep (experiments): KMH_GSU = U
+        if constexpr (K == 12) {
+            if (subt == 2) return run_partitioned<K, 512, 0, 0, 0, 0, 0, 2>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+        }
+        if constexpr (K == 12) {  // sweep (experiments): KMH_GSU=6 unpipelined, 4 = U 4 pipelined
             const int gsu = (int)env_mb("KMH_GSU", 0);
-            if (tpb == 512 && gsu == 4) return run_partitioned<K, 512, 0, 0, 0, 4>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-            if (tpb == 512 && gsu == 7) return run_partitioned<K, 512, 0, 0, 0, 7>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+            if (tpb == 512 && gsu == 6) return run_partitioned<K, 512, 0, 0, 0, 6, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+            if (tpb == 512 && gsu == 4) return run_partitioned<K, 512, 0, 0, 0, 4, 1>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
         }
         if (tpb == 1024) return run_partitioned<K, 1024, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
         return run_partitioned<K, 512, 0, 0>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);

@@ -36,9 +36,11 @@ struct TimedLaunch {
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;        // partition stream of the two-stream pipeline
+    hipEvent_t pipe_ev[5] = {};        // input-ready, partition-done x2, count-done x2
     std::string err;
     // device workspace
-    DevBuf seq, suf, toff, meta, out, out2, sparse[8];
+    DevBuf seq, suf, toff, meta, out, out2, fix, sparse[8];
     // pinned staging for small host->device tables
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
