@@ -6,15 +6,17 @@
 Workload (BASELINE.json configs): N = 1 is config 3 -- 64 synthetic 100 Mbp genomes,
 k = 12, dense 4^12 histogram per genome on one MI355X.  N > 1 is config 4 -- the same 64
 genomes sharded in contiguous blocks of 64/N per GPU (one process per GPU, launched by
-torch.distributed.run) with an RCCL all-gather that assembles the [64, 4^12] matrix on
-every rank inside each step.  A step is one pass of the count path over every genome
+torch.distributed.run) with an RCCL all-gather that assembles the [64, 4^12] u32 matrix on
+every rank inside each step (sent as saturating u8 rows + an exact escape list, step i's
+all-gather overlapped with step i+1's count; --assemble u32 sends plain rows instead).  A step is one pass of the count path over every genome
 (plus the all-gather for N > 1); the genomes are generated on the device before timing,
 so inputs are resident in HBM when the timed region starts.
 
 Printed by rank 0: one JSON line with the driver's fields plus
   roofline      the dominant kernel: algorithmic bytes per launch / mean launch time
                 (HIP events on the launch stream) against 8 TB/s;
-  step_roofline the whole step: (sum L * 1 B + G * 4^k * 4 B) / step time / 8 TB/s;
+  step_roofline the whole step per GPU: (its genomes' bases * 1 B + the count rows it ends up
+                holding * 4 B) / step time / 8 TB/s;
   cpu_baseline  the reference's algorithm (oracle/kmers.py, the same pure-Python window
                 loop as generate.py:49-58) timed on one host core over a bounded sample.
 """
@@ -46,7 +48,10 @@ def parse():
     p.add_argument("--k", type=int, default=12)
     p.add_argument("--genomes", type=int, default=64, help="total genomes over all ranks")
     p.add_argument("--genome-len", type=int, default=100_000_000)
-    p.add_argument("--assemble", choices=["auto", "allgather", "none"], default="auto")
+    p.add_argument("--assemble", choices=["auto", "u8", "u32", "none"], default="auto",
+                   help="N > 1 matrix assembly: u8 = saturating u8 rows + exact escape list, "
+                        "all-gather overlapped with the next step's count (default); u32 = plain "
+                        "all-gather of the u32 rows after each count")
     p.add_argument("--cpu-sample", type=int, default=16_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
     p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
@@ -116,7 +121,8 @@ def main():
     lo, hi = (G * rank) // world, (G * (rank + 1)) // world
     g_local = hi - lo
     B = -(-G // world)
-    assemble = (world > 1) if a.assemble == "auto" else (a.assemble == "allgather")
+    mode = ("u8" if world > 1 else "none") if a.assemble == "auto" else a.assemble
+    assemble = mode != "none"
     bins = 1 << (2 * k)
 
     # CPU baseline first (rank 0, N = 1 only), so it never overlaps GPU timing.
@@ -134,38 +140,108 @@ def main():
     if g_local:
         ctx.synth_dev(d_seq.data_ptr(), L, stride, g_local, SEED_BASE + lo, s)
     offsets = np.arange(g_local + 1, dtype=np.uint64) * np.uint64(stride)
-    local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
+    gloo = a.backend == "gloo"
     full = torch.empty((world * B, bins), dtype=torch.int32, device=dev) if assemble else None
     t_count = []
 
-    def step(record=False):
+    def count_into(buf, record):
         e0 = torch.cuda.Event(enable_timing=True) if record else None
         e1 = torch.cuda.Event(enable_timing=True) if record else None
         if record:
             e0.record(stream)
         if g_local:
-            ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, local.data_ptr(), s)
+            ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, buf.data_ptr(), s)
         if record:
             e1.record(stream)
             t_count.append((e0, e1))
-        if assemble:
-            if a.backend == "nccl":
-                dist.all_gather_into_tensor(full, local)
-            else:  # gloo validation path: host staging
-                host = torch.empty((world * B, bins), dtype=torch.int32)
-                dist.all_gather_into_tensor(host, local.cpu())
-                full.copy_(host)
 
-    for _ in range(a.warmup):
-        step()
+    if mode != "u8":
+        local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
+        locals_ = [local]
+
+        def step(i, record=False):
+            count_into(local, record)
+            if mode == "u32":
+                if not gloo:
+                    dist.all_gather_into_tensor(full, local)
+                else:  # gloo validation path: host staging
+                    host = torch.empty((world * B, bins), dtype=torch.int32)
+                    dist.all_gather_into_tensor(host, local.cpu())
+                    full.copy_(host)
+
+        def drain():
+            pass
+    else:
+        # One all-gather per step of a packed slot per rank:
+        #   [B * bins u8 rows][esc_n u32, 12 B pad][cap escape triples (row, col, value) u32]
+        # Step i's all-gather (RCCL stream) overlaps step i+1's count (compute stream); the
+        # widening to u32 rows runs on a side stream once the gather lands.  Everything is
+        # double-buffered and ordered by events, so each step's matrix is complete and exact.
+        from kmerml.kmers.matrix import slot_layout
+        cap, P = slot_layout(B, bins)
+        u8_bytes = B * bins
+        locals_ = [torch.zeros((B, bins), dtype=torch.int32, device=dev) for _ in range(2)]
+        send = [torch.zeros(P, dtype=torch.uint8, device=dev) for _ in range(2)]
+        recv = [torch.empty(world * P, dtype=torch.uint8, device=dev) for _ in range(2)]
+        esc_max = torch.zeros(world, dtype=torch.int32, device=dev)
+        side = torch.cuda.Stream(dev)
+        dec_done = [None, None]
+        pending = []
+
+        def finish(j, work):
+            """Widen step j's gathered slots into `full` on the side stream."""
+            if work is None:
+                side.wait_stream(stream)
+            with torch.cuda.stream(side):
+                if work is not None:
+                    work.wait()
+                r = recv[j % 2]
+                base = r.data_ptr()
+                for q in range(world):
+                    slot = base + q * P
+                    ctx.rows_decode_u8(slot, B, bins, slot + u8_bytes + 16, cap, slot + u8_bytes,
+                                       1, B, full[q * B:].data_ptr(), side.cuda_stream)
+                n = r.view(world, P)[:, u8_bytes:u8_bytes + 4].view(torch.int32)[:, 0]
+                torch.maximum(esc_max, n, out=esc_max)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                dec_done[j % 2] = ev
+
+        def step(i, record=False):
+            b = i % 2
+            count_into(locals_[b], record)
+            if dec_done[b] is not None:      # step i-2's gather (send[b] -> recv[b]) and widening
+                stream.wait_event(dec_done[b])
+            sb = send[b]
+            ctx.rows_encode_u8(locals_[b].data_ptr(), B, bins, sb.data_ptr(), sb[u8_bytes + 16:].data_ptr(),
+                               cap, sb[u8_bytes:].data_ptr(), s)
+            if not gloo:
+                work = dist.all_gather_into_tensor(recv[b], sb, async_op=True)
+            else:  # gloo validation path: host staging, synchronous
+                host = torch.empty(world * P, dtype=torch.uint8)
+                dist.all_gather_into_tensor(host, sb.cpu())
+                recv[b].copy_(host)
+                work = None
+            if pending:
+                finish(*pending.pop())
+            pending.append((i, work))
+
+        def drain():
+            while pending:
+                finish(*pending.pop())
+
+    for i in range(a.warmup):
+        step(i)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ctx.timing(True)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(record=True)
+    for i in range(a.steps):
+        step(i, record=True)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -181,14 +257,24 @@ def main():
         elapsed, count_ms = float(t[0]), float(t[1])
 
     # sanity: every row sums to the number of valid windows (all-ACGT genomes)
-    rows = full[:G] if (assemble and G % world == 0) else local[:g_local]
+    last = locals_[(a.steps - 1) % len(locals_)]
+    rows = full[:G] if (assemble and G % world == 0) else last[:g_local]
     ok = bool(torch.all(rows.sum(1, dtype=torch.int64) == max(L - k + 1, 0)).item())
+    if assemble:   # this rank's block of the assembled matrix is bit-identical to its own count
+        ok = ok and bool(torch.equal(full[rank * B:rank * B + g_local], last[:g_local]))
+    if mode == "u8" and int(esc_max.max().item()) > cap:
+        raise SystemExit(f"escape list overflow ({int(esc_max.max().item())} > {cap}): use --assemble u32")
+    if world > 1:
+        okt = torch.tensor([int(ok)], dtype=torch.int32, device=dev if not gloo else "cpu")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
 
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         total_bases = G * L if (assemble or world == 1) else g_local * L * world
         value = total_bases / (elapsed / a.steps)
-        algo_step = G * L + G * bins * 4
+        # per GPU: its genomes read once + the count rows it must end up holding written once
+        algo_step = g_local * L + (G if assemble else g_local) * bins * 4
         budget = int(os.environ.get("KMH_SUF_BUDGET_MB", "256")) << 20   # kmh_dense.hip batching
         genomes_per_batch = max(1, min(g_local, budget // max(1, ((L - k + 1 + 16383) // 16384) * 32768)))
         dom = max(kernels.items(), key=lambda kv: kv[1][1]) if kernels else None
@@ -200,6 +286,10 @@ def main():
                 algo = genomes_per_batch * L                 # bases read once (1 B each)
             elif name == "k_bucket_count":
                 algo = genomes_per_batch * bins * 4          # count row slice written once
+            elif name == "k_encode_u8":
+                algo = B * bins * 5                          # u32 rows read, u8 rows written
+            elif name == "k_decode_u8":
+                algo = B * bins * 5                          # u8 rows read, u32 rows written
             else:
                 algo = g_local * (L + bins * 4) / max(1, launches / a.steps)
             achieved = algo / (per_launch_ms * 1e-3) / 1e9
@@ -218,7 +308,8 @@ def main():
                                     f"genomes, k={k} dense 4^{k} count matrix"
                                     + ("" if world == 1 else f", sharded {G}/{world} per GPU + RCCL all-gather")),
                        "genomes": G, "genome_len": L, "k": k,
-                       "parallelism": f"genome-sharded x{world}" + (" + allgather" if assemble else "")},
+                       "parallelism": f"genome-sharded x{world}" + (f" + {mode} allgather" if assemble else ""),
+                       "assembly": mode},
             "roofline": roof,
             "step_roofline": {"algorithmic_bytes": algo_step, "achieved_GBs": round(algo_step / (ms * 1e-3) / 1e9, 1),
                               "frac": round(algo_step / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},

@@ -133,6 +133,25 @@ int kmh_first_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offs
 int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G,
                   uint64_t seed0, void* stream);
 
+/* ---- feature-matrix assembly (multi-GPU) ------------------------------------- */
+/* The reference assembles its organisms x k-mers matrix on one CPU (features.py:85-117).
+ * Here each rank owns a block of count rows; blocks are all-gathered over xGMI as
+ * saturating u8 rows plus an exact escape list, 4x fewer bytes than u32 rows.
+ *
+ * Encode rows x cols u32 counts (cols % 16 == 0) into d_u8 (values >= 255 stored as 255) and
+ * append every value >= 255 as a (row, col, value) u32 triple to d_esc (capacity `cap`
+ * triples).  *d_esc_n (device) receives the number of escapes; if it exceeds cap the
+ * encoding is incomplete and the caller must send u32 rows instead. */
+int kmh_rows_encode_u8_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
+                           uint8_t* d_u8, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
+                           void* stream);
+/* Widen gathered u8 rows (rows x cols) to u32 and apply the escapes of `ranks` ranks:
+ * rank r's escape triples are d_esc[r * cap * 3 ...], its count d_esc_n[r], its rows start
+ * at row r * rows_per_rank. */
+int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
+                           const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
+                           int ranks, uint64_t rows_per_rank, uint32_t* d_rows, void* stream);
+
 /* ---- k{k}.txt text (host) ----------------------------------------------------- */
 /* Replaces the writer loop of _save_kmers_to_file (generate.py:89-91): one line
  * "<digits>\t<count>\n" per k-mer, digits A=0 T=1 C=2 G=3 (generate.py:71).

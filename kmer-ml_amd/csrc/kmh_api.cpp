@@ -227,6 +227,25 @@ int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, i
     return kmh::synth(ctx, d_seq, len, stride, G, seed0, pick_stream(ctx, stream));
 }
 
+int kmh_rows_encode_u8_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
+                           uint8_t* d_u8, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
+                           void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::rows_encode_u8(ctx, d_rows, rows, cols, d_u8, d_esc, cap, d_esc_n, pick_stream(ctx, stream));
+}
+
+int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
+                           const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
+                           int ranks, uint64_t rows_per_rank, uint32_t* d_rows, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::rows_decode_u8(ctx, d_u8, rows, cols, d_esc, cap, d_esc_n, ranks, rows_per_rank,
+                               d_rows, pick_stream(ctx, stream));
+}
+
 // Host sequence -> device (padded with one non-base byte so loads past the end are safe).
 static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t** d_seq) {
     int rc = kmh::ensure(ctx, ctx->seq, (size_t)n + 64);

@@ -81,6 +81,14 @@ int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, 
 int synth(Ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G, uint64_t seed0,
           hipStream_t s);
 
+// ---- matrix assembly encoding (kmh_matrix.hip) ----
+int rows_encode_u8(Ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
+                   uint8_t* d_u8, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
+                   hipStream_t s);
+int rows_decode_u8(Ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
+                   const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n, int ranks,
+                   uint64_t rows_per_rank, uint32_t* d_rows, hipStream_t s);
+
 // ---- sparse path (kmh_sparse.hip) ----
 // Counts the windows of d_seq[0, n) for 13 <= k <= 32 (works for any 1 <= k <= 32).
 // On return the host vectors hold the distinct codes in ascending order, their counts

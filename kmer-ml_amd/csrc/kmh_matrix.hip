@@ -1,0 +1,121 @@
+// kmh_matrix.hip -- compact encoding of genomes x k-mers count rows for the multi-GPU
+// all-gather.  The reference assembles its organisms x k-mers matrix on one
+// CPU (/root/reference/kmerml/ml/features.py:85-117); here every rank owns a block of rows
+// and the blocks travel over xGMI.  Rows are sent as saturating u8 (values >= 255 stored as
+// 255) plus an exact escape list (row, column, value) of every value >= 255, and widened
+// back to u32 after the all-gather: 4x fewer bytes on the links for the same matrix.
+#include "kmh_internal.h"
+
+namespace kmh {
+namespace {
+
+__device__ __forceinline__ uint32_t sat8(uint32_t x) { return x < 255u ? x : 255u; }
+
+// 16 elements per thread per step: four 16-byte loads, one 16-byte store.
+__global__ __launch_bounds__(256) void k_encode_u8(const uint32_t* __restrict__ rows,
+                                                   uint64_t cols, uint64_t n16,
+                                                   uint8_t* __restrict__ out,
+                                                   uint32_t* __restrict__ esc, uint32_t cap,
+                                                   uint32_t* __restrict__ esc_n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4* src = reinterpret_cast<const uint4*>(rows) + 4 * i;
+        uint32_t packed[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = src[q];
+            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+            packed[q] = sat8(e[0]) | (sat8(e[1]) << 8) | (sat8(e[2]) << 16) | (sat8(e[3]) << 24);
+            if ((v.x | v.y | v.z | v.w) >= 255u) {  // rare: list the escapes
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (e[j] >= 255u) {
+                        const uint64_t idx = 16 * i + 4 * q + j;
+                        const uint32_t at = atomicAdd(esc_n, 1u);
+                        if (at < cap) {
+                            esc[3 * (uint64_t)at] = (uint32_t)(idx / cols);
+                            esc[3 * (uint64_t)at + 1] = (uint32_t)(idx % cols);
+                            esc[3 * (uint64_t)at + 2] = e[j];
+                        }
+                    }
+                }
+            }
+        }
+        reinterpret_cast<uint4*>(out)[i] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_decode_u8(const uint8_t* __restrict__ in, uint64_t n16,
+                                                   uint32_t* __restrict__ rows) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 v = reinterpret_cast<const uint4*>(in)[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint4* dst = reinterpret_cast<uint4*>(rows) + 4 * i;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            dst[q] = make_uint4(w[q] & 0xFFu, (w[q] >> 8) & 0xFFu, (w[q] >> 16) & 0xFFu, w[q] >> 24);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_apply_escapes(const uint32_t* __restrict__ esc,
+                                                       uint32_t cap,
+                                                       const uint32_t* __restrict__ esc_n,
+                                                       int ranks, uint64_t rows_per_rank,
+                                                       uint64_t cols, uint32_t* __restrict__ rows) {
+    for (int r = 0; r < ranks; ++r) {
+        const uint32_t n = min(esc_n[r], cap);
+        const uint32_t* e = esc + (uint64_t)r * cap * 3;
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+            const uint32_t row = e[3 * i], col = e[3 * i + 1];
+            if (row < rows_per_rank && col < cols)   // never trust a slot that came off the wire
+                rows[((uint64_t)r * rows_per_rank + row) * cols + col] = e[3 * i + 2];
+        }
+    }
+}
+
+unsigned grid_for(uint64_t n16) {
+    const uint64_t b = (n16 + 255) / 256;
+    return (unsigned)(b < 8192 ? (b ? b : 1) : 8192);
+}
+
+}  // namespace
+
+int rows_encode_u8(Ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
+                   uint8_t* d_u8, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
+                   hipStream_t s) {
+    if (!d_rows || !d_u8 || !d_esc_n || (cap && !d_esc)) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    if (cols % 16 != 0) return fail(ctx, KMH_ERR_INVALID, "cols must be a multiple of 16");
+    KMH_HIP(ctx, hipMemsetAsync(d_esc_n, 0, sizeof(uint32_t), s));
+    const uint64_t n16 = rows * cols / 16;
+    if (n16 == 0) return KMH_OK;
+    time_begin(ctx, s, "k_encode_u8");
+    hipLaunchKernelGGL(k_encode_u8, dim3(grid_for(n16)), dim3(256), 0, s, d_rows, cols, n16, d_u8,
+                       d_esc, cap, d_esc_n);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+int rows_decode_u8(Ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
+                   const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n, int ranks,
+                   uint64_t rows_per_rank, uint32_t* d_rows, hipStream_t s) {
+    if (!d_u8 || !d_rows || (ranks > 0 && (!d_esc_n || (cap && !d_esc))))
+        return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    if (cols % 16 != 0) return fail(ctx, KMH_ERR_INVALID, "cols must be a multiple of 16");
+    const uint64_t n16 = rows * cols / 16;
+    if (n16) {
+        time_begin(ctx, s, "k_decode_u8");
+        hipLaunchKernelGGL(k_decode_u8, dim3(grid_for(n16)), dim3(256), 0, s, d_u8, n16, d_rows);
+        time_end(ctx, s);
+        KMH_HIP(ctx, hipGetLastError());
+    }
+    if (ranks > 0 && cap > 0) {
+        hipLaunchKernelGGL(k_apply_escapes, dim3(64), dim3(256), 0, s, d_esc, cap, d_esc_n, ranks,
+                           rows_per_rank, cols, d_rows);
+        KMH_HIP(ctx, hipGetLastError());
+    }
+    return KMH_OK;
+}
+
+}  // namespace kmh

@@ -49,6 +49,9 @@ SIGNATURES = [
     ("kmh_first_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
     ("kmh_synth_dev", _c.c_int, [_vp, _vp, _u64, _u64, _c.c_int, _u64, _vp]),
     ("kmh_format_lines", _c.c_int64, [_c.c_int, _vp, _vp, _u64, _vp, _u64]),
+    ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
+    ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
+                                          _u64, _vp, _vp]),
 ]
 
 _lib = None
@@ -171,6 +174,20 @@ class Context:
         _check(lib().kmh_synth_dev(self._h, ctypes.c_void_p(d_seq), int(length), int(stride),
                                    int(n_genomes), int(seed0),
                                    ctypes.c_void_p(stream) if stream else None), self._h)
+
+    # -- matrix assembly encoding (device pointers) --
+    def rows_encode_u8(self, d_rows, rows, cols, d_u8, d_esc, cap, d_esc_n, stream=None):
+        _check(lib().kmh_rows_encode_u8_dev(self._h, ctypes.c_void_p(d_rows), int(rows), int(cols),
+                                            ctypes.c_void_p(d_u8), ctypes.c_void_p(d_esc), int(cap),
+                                            ctypes.c_void_p(d_esc_n),
+                                            ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def rows_decode_u8(self, d_u8, rows, cols, d_esc, cap, d_esc_n, ranks, rows_per_rank, d_rows,
+                       stream=None):
+        _check(lib().kmh_rows_decode_u8_dev(self._h, ctypes.c_void_p(d_u8), int(rows), int(cols),
+                                            ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
+                                            int(ranks), int(rows_per_rank), ctypes.c_void_p(d_rows),
+                                            ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- kernel timing --
     def timing(self, enable):

@@ -267,3 +267,57 @@ def test_count_matrix_single_process(tmp_path, oracle_lib):
     m = kmatrix.count_matrix(files, 10).cpu().numpy().view(np.uint32)
     for i, s in enumerate(seqs):
         assert np.array_equal(m[i], oracle_lib.count_dense(s, 10)), i
+
+
+# ---------------------------------------------------------------- matrix assembly encoding
+def _encode(ctx, d_rows, cap):
+    rows, cols = d_rows.shape
+    s = torch.cuda.current_stream().cuda_stream
+    u8 = torch.empty(rows * cols, dtype=torch.uint8, device=d_rows.device)
+    esc = torch.full((max(cap, 1) * 3,), 0x7777, dtype=torch.int32, device=d_rows.device)
+    n = torch.full((1,), -1, dtype=torch.int32, device=d_rows.device)
+    ctx.rows_encode_u8(d_rows.data_ptr(), rows, cols, u8.data_ptr(), esc.data_ptr(), cap, n.data_ptr(), s)
+    return u8, esc, n
+
+
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_rows_u8_round_trip_with_escapes(ctx, dev, ranks):
+    """Saturating u8 rows + escape list widen back to the exact u32 rows (features.py:85-117
+    matrix, multi-rank layout of bench.py / kmerml.kmers.matrix)."""
+    rng = np.random.default_rng(5)
+    rows_per_rank, cols = 3, 4096
+    cap = 2048
+    blocks, u8s, escs, ns = [], [], [], []
+    for r in range(ranks):
+        m = rng.poisson(6, (rows_per_rank, cols)).astype(np.uint32)
+        hot = rng.integers(0, m.size, 300 + 50 * r)
+        m.reshape(-1)[hot] = rng.choice(np.array([254, 255, 256, 1000, 65535, 65536, 2**32 - 1], np.uint64),
+                                        hot.size).astype(np.uint32)
+        blocks.append(m)
+        u8, esc, n = _encode(ctx, torch.from_numpy(m.view(np.int32)).to(dev), cap)
+        torch.cuda.synchronize()
+        assert int(n.item()) == int((m >= 255).sum())
+        assert np.array_equal(u8.cpu().numpy(), np.minimum(m, 255).astype(np.uint8).reshape(-1))
+        u8s.append(u8), escs.append(esc), ns.append(n)
+    out = torch.full((ranks * rows_per_rank, cols), -3, dtype=torch.int32, device=dev)
+    # keep the concatenations alive until the kernels have run (no allocator reuse)
+    all_u8, all_esc, all_n = torch.cat(u8s), torch.cat(escs), torch.cat(ns)
+    assert all_esc.numel() == ranks * cap * 3 and all_n.numel() == ranks
+    ctx.rows_decode_u8(all_u8.data_ptr(), ranks * rows_per_rank, cols, all_esc.data_ptr(),
+                       cap, all_n.data_ptr(), ranks, rows_per_rank, out.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), np.concatenate(blocks))
+
+
+def test_rows_u8_overflow_is_reported(ctx, dev):
+    m = torch.full((2, 64), 300, dtype=torch.int32, device=dev)
+    _, _, n = _encode(ctx, m, 16)
+    torch.cuda.synchronize()
+    assert int(n.item()) == 128     # > cap: the caller must fall back to u32 rows
+
+
+def test_rows_u8_rejects_ragged_cols(ctx, dev):
+    m = torch.zeros((2, 24), dtype=torch.int32, device=dev)
+    with pytest.raises(ValueError):
+        _encode(ctx, m, 16)

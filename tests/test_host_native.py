@@ -19,7 +19,7 @@ HEADER = os.path.join(REPO, "include", "kmerhip.h")
 def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(kmh_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(kmh_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_every_declared_symbol():
