@@ -8,8 +8,8 @@ CSRC     := kmer-ml_amd/csrc
 OUTDIR   := kmer-ml_amd/kmerml/_lib
 OBJDIR   := $(CSRC)/build
 LIB      := $(OUTDIR)/libkmerhip.so
-OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o
-HDRS     := $(CSRC)/kmh_internal.h include/kmerhip.h
+OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o $(OBJDIR)/kmh_hash.o
+HDRS     := $(CSRC)/kmh_internal.h $(CSRC)/kmh_device.h include/kmerhip.h
 
 all: lib oracle selftest
 

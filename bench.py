@@ -45,9 +45,14 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--k", type=int, default=12)
-    p.add_argument("--genomes", type=int, default=64, help="total genomes over all ranks")
-    p.add_argument("--genome-len", type=int, default=100_000_000)
+    p.add_argument("--workload", choices=["dense", "sparse"], default="dense",
+                   help="dense = configs 3/4 (default); sparse = config 5 (k = 21 canonical, "
+                        "250 Mbp genomes, 16 per GPU, no collective)")
+    p.add_argument("--k", type=int, default=None, help="default 12 (dense) / 21 (sparse)")
+    p.add_argument("--genomes", type=int, default=None,
+                   help="total genomes over all ranks (default 64 dense / 16 per GPU sparse)")
+    p.add_argument("--genome-len", type=int, default=None, help="default 100 Mbp dense / 250 Mbp sparse")
+    p.add_argument("--forward", action="store_true", help="sparse: forward-strand codes instead of canonical")
     p.add_argument("--assemble", choices=["auto", "u8", "u32", "none"], default="auto",
                    help="N > 1 matrix assembly: u8 = saturating u8 rows + exact escape list, "
                         "all-gather overlapped with the next step's count (default); u32 = plain "
@@ -59,11 +64,18 @@ def parse():
                    help="process-group backend (gloo + --single-device: multi-rank logic check on one GPU)")
     p.add_argument("--single-device", action="store_true",
                    help="map every rank to cuda:0 (validation only; never used for reported numbers)")
-    return p.parse_args()
+    a = p.parse_args()
+    dense = a.workload == "dense"
+    a.k = a.k if a.k is not None else (12 if dense else 21)
+    a.genome_len = a.genome_len if a.genome_len is not None else (100_000_000 if dense else 250_000_000)
+    if a.genomes is None:
+        a.genomes = 64 if dense else 16 * int(os.environ.get("WORLD_SIZE", "1"))
+    return a
 
 
 def cpu_baseline(sample, k):
-    """Time the reference's per-window loop (oracle restatement) on one core."""
+    """Time the reference's per-window loop (oracle restatement, forward strand: the
+    reference has no canonical mode) on one core."""
     sys.path.insert(0, HERE)
     from oracle import kmers as okmers
     from oracle import synth as osynth
@@ -118,6 +130,8 @@ def main():
         else:
             dist.init_process_group("gloo")
     k, G, L = a.k, a.genomes, a.genome_len
+    if a.workload == "sparse":
+        return run_sparse(a, world, rank, dev, dev_index)
     lo, hi = (G * rank) // world, (G * (rank + 1)) // world
     g_local = hi - lo
     B = -(-G // world)
@@ -328,6 +342,119 @@ def main():
         dist.destroy_process_group()
     if not ok:
         raise SystemExit("row-sum check failed")
+
+
+def run_sparse(a, world, rank, dev, dev_index):
+    """Config 5: k = 21 canonical k-mers of 250 Mbp genomes counted with the device hash-table
+    path (kmh_count_sparse_dev); each rank counts its contiguous block of genomes and keeps
+    its sparse rows (the full 4^21-column matrix would not fit: no all-gather)."""
+    k, G, L = a.k, a.genomes, a.genome_len
+    lo, hi = (G * rank) // world, (G * (rank + 1)) // world
+    g_local = hi - lo
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_sample > 0:
+        cpu = cpu_baseline(min(a.cpu_sample, 4_000_000), k)
+    ctx = _native.context(dev_index)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    stride = (L + 15) // 16 * 16
+    d_seq = torch.empty(max(g_local, 1) * stride, dtype=torch.uint8, device=dev)
+    if stride != L:
+        d_seq.fill_(ord("N"))
+    if g_local:
+        ctx.synth_dev(d_seq.data_ptr(), L, stride, g_local, SEED_BASE + lo, s)
+    offsets = np.arange(g_local + 1, dtype=np.uint64) * np.uint64(stride)
+    out_off = _native.sparse_out_offsets(offsets, k)
+    cap = max(int(out_off[-1]), 1)
+    d_codes = torch.empty(cap, dtype=torch.int64, device=dev)
+    d_counts = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_nk = torch.zeros(max(g_local, 1), dtype=torch.int64, device=dev)
+    canonical = 0 if a.forward else 1
+
+    def step():
+        if g_local:
+            ctx.count_sparse_dev(d_seq.data_ptr(), offsets, k, canonical, d_codes.data_ptr(),
+                                 d_counts.data_ptr(), d_nk.data_ptr(), s)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernels = ctx.timing_report()
+    ctx.timing(False)
+
+    # checks: every genome's counts sum to its windows; distinct within capacity
+    nk = d_nk.cpu().numpy()[:g_local]
+    ok = True
+    for g in range(g_local):
+        a0, n = int(out_off[g]), int(nk[g])
+        tot = int(d_counts[a0:a0 + n].to(torch.int64).sum().item())
+        ok = ok and tot == L - k + 1 and 0 < n <= L - k + 1
+    distinct = int(nk.sum())
+    if world > 1:
+        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64,
+                         device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, ok = float(t[0]), float(t[1]) == 0.0
+    if rank == 0:
+        ms = elapsed / a.steps * 1e3
+        value = G * L / (elapsed / a.steps)
+        algo_step = g_local * L + distinct * 12        # SURVEY 8(d): L x 1 B + distinct x 12 B
+        roof = None
+        if kernels:
+            name, (launches, tot) = max(kernels.items(), key=lambda kv: kv[1][1])
+            per_launch_ms = tot / launches
+            per_step = launches / a.steps
+            if name == "k_sp_partition":
+                algo = g_local * L / per_step               # bases read once per launch
+            elif name == "k_sp_count":
+                algo = distinct * 12 / per_step             # distinct (code u64, count u32) written once
+            else:
+                algo = algo_step / per_step
+            achieved = algo / (per_launch_ms * 1e-3) / 1e9
+            traffic = load_traffic(a.pmc_summary, f"{name}:k{k}:L{L}")
+            roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                    "algorithmic_bytes_per_launch": algo, "mean_launch_ms": round(per_launch_ms, 4),
+                    "launches_per_step": per_step}
+        out = {
+            "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": f"config5: {G} synthetic {L // 1_000_000} Mbp genomes, k={k} "
+                                   f"{'forward' if a.forward else 'canonical'} sparse counts "
+                                   f"({g_local} per GPU, hash-table path)",
+                       "genomes": G, "genome_len": L, "k": k, "parallelism": f"genome-sharded x{world}"},
+            "roofline": roof,
+            "step_roofline": {"algorithmic_bytes": algo_step,
+                              "achieved_GBs": round(algo_step / (ms * 1e-3) / 1e9, 1),
+                              "frac": round(algo_step / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "distinct_kmers_rank0": distinct,
+            "kernels": {n: {"launches": l, "total_ms": round(t, 4), "mean_ms": round(t / l, 4)}
+                        for n, (l, t) in kernels.items()},
+            "rows_checked": ok,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit("sparse count check failed")
 
 
 if __name__ == "__main__":

@@ -133,6 +133,24 @@ int kmh_first_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offs
 int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G,
                   uint64_t seed0, void* stream);
 
+/* ---- sparse counting, device-resident batch (BASELINE config 5) --------------- */
+/* The reference counts every k in a Python dict, a hash table (generate.py:36,58); for
+ * 13 <= k <= 21 this counts G device-resident genomes (layout as kmh_count_dense_dev)
+ * with partitioned LDS hash tables.  canonical != 0 counts min(forward, reverse
+ * complement) codes.  Genome g's distinct k-mers (2-bit codes, A0 C1 G2 T3, first base
+ * most significant) and their exact counts are written to d_codes / d_counts starting at
+ * entry out_off[g] (kmh_sparse_out_offsets: the number of windows of the genomes before
+ * g, so a genome never needs more room than its windows); d_nkmers[g] (device) receives
+ * the number of distinct k-mers.  Order within a genome is unspecified (grouped by the
+ * top 11 bits of the code).  Synchronises `stream` (the work list depends on the bucket
+ * sizes). */
+int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
+                         int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
+                         uint64_t* d_nkmers, void* stream);
+/* Output offsets of kmh_count_sparse_dev: out_off[g] for g = 0..G (out_off nullable);
+ * returns out_off[G], the total capacity in entries. */
+uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off);
+
 /* ---- feature-matrix assembly (multi-GPU) ------------------------------------- */
 /* The reference assembles its organisms x k-mers matrix on one CPU (features.py:85-117).
  * Here each rank owns a block of count rows; blocks are all-gathered over xGMI as

@@ -227,6 +227,21 @@ int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, i
     return kmh::synth(ctx, d_seq, len, stride, G, seed0, pick_stream(ctx, stream));
 }
 
+int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
+                         int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
+                         uint64_t* d_nkmers, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::sparse_count_dev(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers,
+                                 pick_stream(ctx, stream));
+}
+
+uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off) {
+    if (!offsets || G < 0) return 0;
+    return kmh::sparse_windows(offsets, G, k, out_off);
+}
+
 int kmh_rows_encode_u8_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
                            uint8_t* d_u8, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
                            void* stream) {

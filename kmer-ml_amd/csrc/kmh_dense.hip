@@ -20,21 +20,58 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "kmh_internal.h"
+#include "kmh_device.h"
 
 namespace kmh {
+
+int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, uint64_t tile, Layout& L) {
+    if (G < 1) return fail(ctx, KMH_ERR_INVALID, "G must be >= 1");
+    if (!offsets) return fail(ctx, KMH_ERR_INVALID, "offsets is NULL");
+    L.goff.assign(offsets, offsets + G + 1);
+    L.tbase.assign(G + 1, 0);
+    for (int g = 0; g < G; ++g) {
+        const uint64_t a = offsets[g], b = offsets[g + 1];
+        if (b < a) return fail(ctx, KMH_ERR_INVALID, "offsets must be non-decreasing");
+        if (a % 16 != 0) return fail(ctx, KMH_ERR_INVALID, "genome start offsets must be multiples of 16");
+        if (b - a >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "a genome must be shorter than 2^32 - 1 bytes");
+        const uint64_t nwin = (b - a >= (uint64_t)k) ? (b - a - (uint64_t)k + 1) : 0;
+        L.tbase[g + 1] = L.tbase[g] + (nwin + tile - 1) / tile;
+    }
+    L.ntiles = L.tbase[G];
+    return KMH_OK;
+}
+
+int upload_layout(Ctx* ctx, const Layout& L, hipStream_t s, const uint64_t** d_goff,
+                  const uint64_t** d_tbase) {
+    const size_t n = L.goff.size();
+    int rc = ensure(ctx, ctx->meta, 2 * n * sizeof(uint64_t));
+    if (rc) return rc;
+    std::vector<uint64_t> both(2 * n);
+    std::copy(L.goff.begin(), L.goff.end(), both.begin());
+    std::copy(L.tbase.begin(), L.tbase.end(), both.begin() + n);
+    rc = upload(ctx, ctx->meta.ptr, both.data(), both.size() * sizeof(uint64_t), s);
+    if (rc) return rc;
+    *d_goff = static_cast<const uint64_t*>(ctx->meta.ptr);
+    *d_tbase = *d_goff + n;
+    return KMH_OK;
+}
+
+long env_long(const char* name, long dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atol(v) : dflt;
+}
+
+size_t env_mb(const char* name, size_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    const long x = std::atol(v);
+    return x > 0 ? (size_t)x : dflt;
+}
+
 namespace {
 
 constexpr int kDirectThreads = kTileThreads;
 constexpr int kTargetWorkgroups = 512;
-
-struct GenomeMap {
-    const uint64_t* goff;   // genome byte offsets, G + 1 (device)
-    const uint64_t* tbase;  // cumulative tile counts, G + 1 (device), tbase[0] = 0
-    int g0, g1;             // genomes covered by this launch
-    uint64_t tile_lo;       // tbase[g0]
-    uint64_t data_end;      // offsets[G]: bytes at or past it may not be readable
-};
 
 template <int K>
 constexpr int num_buckets() { return 1 << (2 * K - kSubBits); }
@@ -60,59 +97,6 @@ constexpr int batch_tiles(int tile, int qmax) {
     return p2;
 }
 constexpr uint32_t kPadBins = 64;
-
-// Largest g in [g0, g1) with tbase[g] <= gt (genomes without tiles are skipped).
-__device__ __forceinline__ int find_genome(const GenomeMap& m, uint64_t gt) {
-    int lo = m.g0, hi = m.g1 - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (m.tbase[mid] <= gt) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-// 16 bytes at pos; bytes at or past `end` read as 0 (not a base).
-__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ seq, uint64_t pos,
-                                        uint64_t end) {
-    if (pos + 16 <= end) return *reinterpret_cast<const uint4*>(seq + pos);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (pos + i < end) w[i >> 2] |= (uint32_t)seq[pos + i] << (8 * (i & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// Four ASCII bytes (byte 0 first) -> 8 bits of 2-bit codes (byte 0 in bits 7:6) and a
-// 4-bit invalid mask (byte 0 in bit 3).  code = ((c >> 1) ^ (c >> 2)) & 3 maps A/a->0,
-// C/c->1, G/g->2, T/t->3; a byte is a base iff (c & 0xDF) == "ACGT"[code].
-__device__ __forceinline__ void enc4(uint32_t w, uint32_t& c8, uint32_t& i4) {
-    const uint32_t cb = ((w >> 1) ^ (w >> 2)) & 0x03030303u;
-    const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, cb);  // "ACGT"[cb]
-    const uint32_t e = (w & 0xDFDFDFDFu) ^ expect;                       // 0 byte = base
-    const uint32_t nz = (((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e) & 0x80808080u;
-    i4 = ((nz >> 7) * 0x08040201u) >> 24;
-    c8 = (cb * 0x40100401u) >> 24;
-}
-
-// 16 bytes -> 32-bit code word (first base in bits 31:30) + 16-bit invalid mask (first
-// base in bit 15).
-__device__ __forceinline__ void enc16(uint4 v, uint32_t& code, uint32_t& inv) {
-    uint32_t c0, c1, c2, c3, i0, i1, i2, i3;
-    enc4(v.x, c0, i0);
-    enc4(v.y, c1, i1);
-    enc4(v.z, c2, i2);
-    enc4(v.w, c3, i3);
-    code = (c0 << 24) | (c1 << 16) | (c2 << 8) | c3;
-    inv = (i0 << 12) | (i1 << 8) | (i2 << 4) | i3;
-}
-
-// Invalid-mask bits for the bytes of a 16-byte chunk at pos that lie at or past `end`
-// (bit 15 = byte 0).
-__device__ __forceinline__ uint32_t tail_mask(uint64_t pos, uint64_t end) {
-    if (end >= pos + 16) return 0u;
-    if (end <= pos) return 0xFFFFu;
-    return 0xFFFFu >> (uint32_t)(end - pos);
-}
 
 // Visit the 32 windows that start at tstart + 32 * threadIdx.x + j, j = 0..31:
 // f(j, code, is_valid).  Each thread loads its 32 bytes plus the next 16 (the k - 1 <= 15
@@ -165,15 +149,6 @@ __device__ __forceinline__ void walk(const uint8_t* __restrict__ seq, const Geno
                                      uint64_t tstart, uint64_t gend, int tpb, F&& f) {
     if (tstart + (uint64_t)tpb * kTileBpt + 16 <= m.data_end) walk_tile<K, true>(seq, tstart, gend, f);
     else walk_tile<K, false>(seq, tstart, gend, f);
-}
-
-// XCD-aware work order: blocks b and b+8 share an XCD under the observed round-robin
-// placement, so hand each XCD a contiguous range of work items (speed only).
-// Bijective for any grid size: XCD group x = b % 8 owns a contiguous run of work items.
-__device__ __forceinline__ uint32_t xcd_work_id() {
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
-    const uint32_t q = nb / 8u, rem = nb % 8u, x = b % 8u;
-    return x * q + (x < rem ? x : rem) + b / 8u;
 }
 
 // ---------------------------------------------------------------- k <= 9: direct
@@ -708,55 +683,6 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* __restrict__ out, uint64
 }
 
 // ---------------------------------------------------------------- host side
-struct Layout {
-    std::vector<uint64_t> goff, tbase;
-    uint64_t ntiles = 0;
-};
-
-int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, uint64_t tile, Layout& L) {
-    if (G < 1) return fail(ctx, KMH_ERR_INVALID, "G must be >= 1");
-    if (!offsets) return fail(ctx, KMH_ERR_INVALID, "offsets is NULL");
-    L.goff.assign(offsets, offsets + G + 1);
-    L.tbase.assign(G + 1, 0);
-    for (int g = 0; g < G; ++g) {
-        const uint64_t a = offsets[g], b = offsets[g + 1];
-        if (b < a) return fail(ctx, KMH_ERR_INVALID, "offsets must be non-decreasing");
-        if (a % 16 != 0) return fail(ctx, KMH_ERR_INVALID, "genome start offsets must be multiples of 16");
-        if (b - a >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "a genome must be shorter than 2^32 - 1 bytes");
-        const uint64_t nwin = (b - a >= (uint64_t)k) ? (b - a - (uint64_t)k + 1) : 0;
-        L.tbase[g + 1] = L.tbase[g] + (nwin + tile - 1) / tile;
-    }
-    L.ntiles = L.tbase[G];
-    return KMH_OK;
-}
-
-int upload_layout(Ctx* ctx, const Layout& L, hipStream_t s, const uint64_t** d_goff,
-                  const uint64_t** d_tbase) {
-    const size_t n = L.goff.size();
-    int rc = ensure(ctx, ctx->meta, 2 * n * sizeof(uint64_t));
-    if (rc) return rc;
-    std::vector<uint64_t> both(2 * n);
-    std::copy(L.goff.begin(), L.goff.end(), both.begin());
-    std::copy(L.tbase.begin(), L.tbase.end(), both.begin() + n);
-    rc = upload(ctx, ctx->meta.ptr, both.data(), both.size() * sizeof(uint64_t), s);
-    if (rc) return rc;
-    *d_goff = static_cast<const uint64_t*>(ctx->meta.ptr);
-    *d_tbase = *d_goff + n;
-    return KMH_OK;
-}
-
-long env_long(const char* name, long dflt) {
-    const char* v = std::getenv(name);
-    return (v && *v) ? std::atol(v) : dflt;
-}
-
-size_t env_mb(const char* name, size_t dflt) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return dflt;
-    const long x = std::atol(v);
-    return x > 0 ? (size_t)x : dflt;
-}
-
 template <int K>
 int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {

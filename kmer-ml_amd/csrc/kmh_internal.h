@@ -72,6 +72,20 @@ int upload(Ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s);
 void time_begin(Ctx* ctx, hipStream_t s, const char* name);
 void time_end(Ctx* ctx, hipStream_t s);
 
+// Genome/tile layout of a batch launch: goff = genome byte offsets (G + 1), tbase =
+// cumulative tile counts (G + 1) for tiles of `tile` window starts.
+struct Layout {
+    std::vector<uint64_t> goff, tbase;
+    uint64_t ntiles = 0;
+};
+int make_layout(Ctx* ctx, const uint64_t* offsets, int G, int k, uint64_t tile, Layout& L);
+// Copies goff and tbase to ctx->meta; returns their device addresses.
+int upload_layout(Ctx* ctx, const Layout& L, hipStream_t s, const uint64_t** d_goff,
+                  const uint64_t** d_tbase);
+// Integer environment knobs (experiments): env_mb treats values <= 0 as unset.
+long env_long(const char* name, long dflt);
+size_t env_mb(const char* name, size_t dflt);
+
 // ---- dense path (kmh_dense.hip) ----
 // offsets: host, G+1 entries.  d_out: G x 4^k u32.
 int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
@@ -96,5 +110,12 @@ int rows_decode_u8(Ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
 int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
                  std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
                  std::vector<uint64_t>& first, hipStream_t s);
+
+// ---- device-resident sparse path (kmh_hash.hip) ----
+// Windows per genome -> cumulative output offsets (out_off: G + 1 entries, nullable).
+uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off);
+int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                     int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
+                     hipStream_t s);
 
 }  // namespace kmh

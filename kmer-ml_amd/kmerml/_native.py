@@ -49,6 +49,8 @@ SIGNATURES = [
     ("kmh_first_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
     ("kmh_synth_dev", _c.c_int, [_vp, _vp, _u64, _u64, _c.c_int, _u64, _vp]),
     ("kmh_format_lines", _c.c_int64, [_c.c_int, _vp, _vp, _u64, _vp, _u64]),
+    ("kmh_count_sparse_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp]),
+    ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
     ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
                                           _u64, _vp, _vp]),
@@ -175,6 +177,16 @@ class Context:
                                    int(n_genomes), int(seed0),
                                    ctypes.c_void_p(stream) if stream else None), self._h)
 
+    # -- sparse counting, device-resident (BASELINE config 5) --
+    def count_sparse_dev(self, d_seq, offsets, k, canonical, d_codes, d_counts, d_nkmers, stream=None):
+        """Distinct k-mers of G device-resident genomes (13 <= k <= 21); genome g's entries
+        start at sparse_out_offsets(offsets, k)[g].  Synchronises the stream."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        _check(lib().kmh_count_sparse_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1, int(k),
+                                          int(bool(canonical)), ctypes.c_void_p(d_codes),
+                                          ctypes.c_void_p(d_counts), ctypes.c_void_p(d_nkmers),
+                                          ctypes.c_void_p(stream) if stream else None), self._h)
+
     # -- matrix assembly encoding (device pointers) --
     def rows_encode_u8(self, d_rows, rows, cols, d_u8, d_esc, cap, d_esc_n, stream=None):
         _check(lib().kmh_rows_encode_u8_dev(self._h, ctypes.c_void_p(d_rows), int(rows), int(cols),
@@ -277,3 +289,11 @@ def format_lines(k, codes, counts):
     out = ctypes.create_string_buffer(max(need, 1))
     _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, out, need))
     return out.raw[:need]
+
+
+def sparse_out_offsets(offsets, k):
+    """Entry offsets of every genome in the output of Context.count_sparse_dev (G + 1)."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = np.zeros(off.size, dtype=np.uint64)
+    lib().kmh_sparse_out_offsets(_ptr(off), off.size - 1, int(k), _ptr(out))
+    return out

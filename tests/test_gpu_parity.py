@@ -321,3 +321,93 @@ def test_rows_u8_rejects_ragged_cols(ctx, dev):
     m = torch.zeros((2, 24), dtype=torch.int32, device=dev)
     with pytest.raises(ValueError):
         _encode(ctx, m, 16)
+
+
+# ---------------------------------------------------------------- sparse, device-resident (config 5)
+def _sparse_dev(ctx, dev, genomes, k, canonical):
+    """kmh_count_sparse_dev on host genomes -> per-genome (codes, counts) sorted by code."""
+    buf, offs = _layout(genomes)
+    d_seq = torch.from_numpy(buf.copy()).to(dev)
+    out_off = _native.sparse_out_offsets(offs, k)
+    cap = max(int(out_off[-1]), 1)
+    d_codes = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+    d_counts = torch.zeros(cap, dtype=torch.int32, device=dev)
+    d_nk = torch.full((len(genomes),), -1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.count_sparse_dev(d_seq.data_ptr(), offs, k, canonical, d_codes.data_ptr(), d_counts.data_ptr(),
+                         d_nk.data_ptr(), s)
+    torch.cuda.synchronize()
+    nk = d_nk.cpu().numpy()
+    codes = d_codes.cpu().numpy().view(np.uint64)
+    counts = d_counts.cpu().numpy().view(np.uint32)
+    res = []
+    for g in range(len(genomes)):
+        a, n = int(out_off[g]), int(nk[g])
+        assert 0 <= n <= int(out_off[g + 1]) - a
+        c, m = codes[a:a + n], counts[a:a + n]
+        o = np.argsort(c, kind="stable")
+        res.append((c[o], m[o]))
+    return res
+
+
+def _ragged_genomes(rng, sizes):
+    gs = [_rand_seq(rng, n) for n in sizes]
+    gs.append(np.frombuffer(b"ACGTTGCAacgtN" * 3, np.uint8).copy())   # shorter than a tile, mixed
+    gs.append(np.zeros(0, np.uint8))                                    # empty genome
+    gs.append(np.frombuffer(b"ACGTACGTACGTACGTACGT", np.uint8).copy())  # 20 bases < k = 21
+    return gs
+
+
+@pytest.mark.parametrize("k,canonical", [(13, 0), (13, 1), (17, 1), (20, 0), (21, 0), (21, 1)])
+def test_sparse_dev_vs_oracle(ctx, dev, oracle_lib, k, canonical):
+    rng = np.random.default_rng(100 + k * 2 + canonical)
+    genomes = _ragged_genomes(rng, [400_000, 32768 + 21, 1_000_003, 17])
+    got = _sparse_dev(ctx, dev, genomes, k, canonical)
+    for g, seq in enumerate(genomes):
+        wc, wn, _ = oracle_lib.count_sparse(seq, k, canonical=bool(canonical))
+        assert np.array_equal(got[g][0], wc), g
+        assert np.array_equal(got[g][1], wn), g
+
+
+def test_sparse_dev_passes_and_fallback(ctx, dev, oracle_lib, monkeypatch):
+    """Every bucket split into many passes, and tables capped so most passes overflow into
+    the sort fallback: the counts must not change."""
+    rng = np.random.default_rng(7)
+    genomes = _ragged_genomes(rng, [600_000, 70_001])
+    want = [oracle_lib.count_sparse(s, 21, canonical=True)[:2] for s in genomes]
+    for target, limit in (("37", "12288"), ("100000", "40"), ("61", "9")):
+        monkeypatch.setenv("KMH_SP_TARGET", target)
+        monkeypatch.setenv("KMH_SP_LIMIT", limit)
+        got = _sparse_dev(ctx, dev, genomes, 21, 1)
+        for g in range(len(genomes)):
+            assert np.array_equal(got[g][0], want[g][0]), (target, limit, g)
+            assert np.array_equal(got[g][1], want[g][1]), (target, limit, g)
+
+
+def test_sparse_dev_low_complexity(ctx, dev, oracle_lib):
+    genomes = [np.full(300_000, ord("A"), np.uint8),
+               np.frombuffer(b"AC" * 150_000, np.uint8).copy(),
+               np.frombuffer(b"ACGTTTGACCA" * 30_000, np.uint8).copy()]
+    for canonical in (0, 1):
+        got = _sparse_dev(ctx, dev, genomes, 21, canonical)
+        for g, seq in enumerate(genomes):
+            wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=bool(canonical))
+            assert np.array_equal(got[g][0], wc)
+            assert np.array_equal(got[g][1], wn)
+
+
+def test_sparse_dev_config5_genome(ctx, dev, oracle_lib):
+    """One 25 Mbp synthetic genome (a tenth of a config-5 genome) at k = 21 canonical."""
+    seq = osynth.synth_bases(25_000_000, osynth.genome_seed(0))
+    got = _sparse_dev(ctx, dev, [seq], 21, 1)[0]
+    wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
+    assert got[0].size == wc.size
+    assert np.array_equal(got[0], wc) and np.array_equal(got[1], wn)
+
+
+def test_sparse_dev_rejects_k(ctx, dev):
+    d = torch.zeros(64, dtype=torch.uint8, device=dev)
+    o = torch.zeros(8, dtype=torch.int64, device=dev)
+    with pytest.raises(NotImplementedError):
+        ctx.count_sparse_dev(d.data_ptr(), np.array([0, 64], np.uint64), 12, 0, o.data_ptr(), o.data_ptr(),
+                             o.data_ptr())
