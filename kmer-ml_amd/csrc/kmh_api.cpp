@@ -127,7 +127,8 @@ int kmh_ctx_create(int device, kmh_ctx** out) {
     std::unique_ptr<kmh_ctx> c(new (std::nothrow) kmh_ctx);
     if (!c) return KMH_ERR_NOMEM;
     c->device = device;
-    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess) {
         kmh::set_thread_error(std::string("kmh_ctx_create: ") + hipGetErrorString(e));
         return KMH_ERR_HIP;
     }

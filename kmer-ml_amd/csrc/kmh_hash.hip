@@ -2,28 +2,33 @@
 // canonical) for BASELINE config 5: 250 Mbp genomes at k = 21, where 4^k bins cannot be
 // tabulated and almost every k-mer is distinct.  The reference counts into a Python dict
 // (a hash table, /root/reference/kmerml/kmers/generate.py:36,58); here the counting is done
-// by LDS hash tables after a partition pass, so every hash insert is an LDS operation:
+// by LDS hash tables after two partition passes, so every hash insert is an LDS operation
+// and every kernel streams whole 16-byte chunks:
 //
 //  1. k_sp_partition  one workgroup per 32768-window tile: forward (and reverse-complement)
-//                     codes from 2-bit packed registers, bucket = top 11 bits of the code
-//                     (2048 buckets), LDS histogram + scan + scatter of the low 2k - 11 bits
+//                     codes from 2-bit packed registers, bucket = top 10 bits of the code
+//                     (1024 buckets), LDS histogram + scan + scatter of the low 2k - 10 bits
 //                     (u32 residues), one coalesced store of the tile's entries and an exact
-//                     bucket-major offset table toff[bucket][tile] (u16 entry indices; no
-//                     padding: entries are consumed one per lane).
-//  2. k_sp_sizes      entries per (genome, bucket); the host splits every bucket into
-//                     P = ceil(entries / target) passes over equal residue ranges.
-//  3. k_sp_count      one workgroup per (genome, bucket, pass): streams the bucket's segments
-//                     through a per-wave LDS queue, inserts the pass's residues into a
-//                     16384-slot LDS hash table (linear probing, u32 key + u32 count), and
-//                     appends the distinct k-mers to the genome's output through one atomic
-//                     cursor.  The passes of a bucket are neighbouring work items on one XCD,
-//                     so the bucket is read from HBM once and re-read from that XCD's L2.
-//  4. fallback        a pass whose distinct keys exceed the table limit emits nothing and is
-//                     counted instead by gather + hipCUB radix sort + run-length encode (keys
-//                     of different passes are disjoint, so the two never double count).
+//                     bucket-major offset table toff[bucket][tile] (u16 entry indices).
+//  2. k_sp_sizes      entries per (genome, bucket).  The host splits every bucket into
+//                     P = ceil(entries / 8192) passes over equal residue ranges (one LDS hash
+//                     table each) and into split items of ~12K entries (ranges of tiles).
+//  3. k_sp_split      one workgroup per split item: gathers the bucket's segments of its
+//                     tiles (16-byte chunk loads, entries outside the segment masked by
+//                     position), partitions them by pass (LDS histogram, scan, scatter) and
+//                     stores them contiguously with per-pass offsets toff2[item][pass].
+//  4. k_sp_count      one workgroup per (genome, bucket, pass): reads that pass's segment of
+//                     every split item of the bucket, inserts it into a 16384-slot LDS hash
+//                     table (linear probing, 64-bit key|count slots) and appends the distinct
+//                     k-mers to the genome's output through one atomic cursor.
+//  5. fallback        a split item whose entries exceed its staging, or a pass whose distinct
+//                     keys exceed the table limit, emits nothing; those passes are counted by
+//                     gather + hipCUB radix sort + run-length encode from the step-1 entries
+//                     (keys of different passes are disjoint, so nothing is counted twice).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <vector>
 
 #include "kmh_device.h"
@@ -31,15 +36,18 @@
 namespace kmh {
 namespace {
 
-constexpr int kSpThreads = 1024;           // threads of partition and count workgroups
-constexpr int kSpBucketBits = 11;
+constexpr int kSpThreads = 1024;           // threads of every workgroup here
+constexpr int kNW = kSpThreads / 64;       // waves per workgroup
+constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kSpTile = kSpThreads * 32;   // 32768 window starts per tile (= kTile)
-constexpr int kSlotBits = 14;
-constexpr int kSlots = 1 << kSlotBits;     // LDS hash slots: 16384 x (key, count) = 128 KiB
-constexpr int kQueue = 256;                // per-wave queue entries (4 load rounds)
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-constexpr int kMaxPasses = 64;
+constexpr int kTileChunks = kSpTile / 4;   // 16-byte chunks of a tile's entries
+constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
+constexpr int kQU = 4;                     // chunk loads in flight per lane
+constexpr int kCaps = 20480;               // entries staged by one split item (80 KiB)
+constexpr int kMaxPasses = 256;
+constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
 
 // 2-bit-group reversal of the low 2K bits of ~x: the reverse complement of a K-mer code.
 template <int K>
@@ -112,11 +120,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
                                                              uint16_t* __restrict__ toff,
                                                              uint32_t ldt) {
     constexpr int R = 2 * K - kSpBucketBits;
-    constexpr uint64_t RM = (1ull << R) - 1ull;
+    constexpr uint64_t RM = (R == 32) ? 0xFFFFFFFFull : ((1ull << R) - 1ull);
+    static_assert(kSpBuckets == kSpThreads, "one bucket per thread in the scan");
     __shared__ __attribute__((aligned(16))) uint32_t sorted[kSpTile];
     __shared__ uint32_t cnt[kSpBuckets];
-    __shared__ uint32_t cur[kSpBuckets];
-    __shared__ uint32_t wsum[kSpThreads / 64];
+    __shared__ uint32_t wsum[kNW];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t lt = xcd_work_id();
@@ -125,7 +133,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)kSpTile;
     const uint64_t ge = m.goff[g + 1];
 
-    for (int b = tid; b < kSpBuckets; b += kSpThreads) cnt[b] = 0u;
+    cnt[tid] = 0u;
     __syncthreads();
 
     const uint64_t base = tstart + 32ull * (uint64_t)tid;
@@ -134,9 +142,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     each_window<K, CANON>(bs, [&](uint64_t c) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
     __syncthreads();
 
-    // Exclusive scan of the 2048 bucket counts (two consecutive buckets per thread).
-    const uint32_t n0 = cnt[2 * tid], n1 = cnt[2 * tid + 1];
-    uint32_t incl = n0 + n1;
+    // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
+    const uint32_t n0 = cnt[tid];
+    uint32_t incl = n0;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t t = __shfl_up(incl, d);
@@ -146,20 +154,18 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     __syncthreads();
     uint32_t pre = 0u, total = 0u;
 #pragma unroll
-    for (int w = 0; w < kSpThreads / 64; ++w) {
+    for (int w = 0; w < kNW; ++w) {
         pre += (w < wave) ? wsum[w] : 0u;
         total += wsum[w];
     }
-    const uint32_t s0 = pre + incl - n0 - n1;
-    cur[2 * tid] = s0;
-    cur[2 * tid + 1] = s0 + n0;
-    toff[(uint64_t)(2 * tid) * ldt + lt] = (uint16_t)s0;
-    toff[(uint64_t)(2 * tid + 1) * ldt + lt] = (uint16_t)(s0 + n0);
+    const uint32_t s0 = pre + incl - n0;
+    cnt[tid] = s0;
+    toff[(uint64_t)tid * ldt + lt] = (uint16_t)s0;
     if (tid == 0) toff[(uint64_t)kSpBuckets * ldt + lt] = (uint16_t)total;
     __syncthreads();
 
     each_window<K, CANON>(bs, [&](uint64_t c) {
-        const uint32_t slot = atomicAdd(&cur[(uint32_t)(c >> R)], 1u);
+        const uint32_t slot = atomicAdd(&cnt[(uint32_t)(c >> R)], 1u);
         sorted[slot] = (uint32_t)(c & RM);
     });
     __syncthreads();
@@ -189,84 +195,38 @@ __global__ __launch_bounds__(256) void k_sp_sizes(const uint16_t* __restrict__ t
     if (threadIdx.x == 0) nb[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// Work item of the count kernel.
-struct SpItem {
-    uint32_t g;        // genome index (absolute)
-    uint32_t b;        // bucket
-    uint16_t p, np;    // pass and passes of the bucket
-    uint32_t n;        // entries of the bucket
-};
-
 __device__ __forceinline__ uint32_t pass_of(uint32_t r, uint32_t np, int R) {
     return (uint32_t)(((uint64_t)r * np) >> R);
 }
 
-__global__ __launch_bounds__(kSpThreads) void k_sp_count(
-    const uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, uint32_t ldt,
-    const uint64_t* __restrict__ tbase, uint64_t tile_lo, const SpItem* __restrict__ items,
-    int R, uint32_t limit, const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
-    uint32_t* __restrict__ counts, unsigned long long* __restrict__ nk,
-    uint32_t* __restrict__ failed) {
-    constexpr int NW = kSpThreads / 64;
-    __shared__ uint32_t keys[kSlots];
-    __shared__ uint32_t cnts[kSlots];
-    __shared__ uint32_t queue[NW][kQueue];
-    __shared__ uint32_t used, fail;
-    __shared__ uint32_t wsum[NW];
-    __shared__ unsigned long long obase;
+__device__ __forceinline__ uint32_t lane_of(const uint4& v, int i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
 
-    const SpItem it = items[xcd_work_id()];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int i = tid; i < kSlots; i += kSpThreads) {
-        keys[i] = kEmpty;
-        cnts[i] = 0u;
-    }
-    if (tid == 0) {
-        used = 0u;
-        fail = 0u;
-    }
-    __syncthreads();
+// Split work item: tiles [t0, t1) (batch-relative) of bucket b of one genome.
+struct SplitItem {
+    uint32_t b, t0, t1, np;
+    uint32_t gb;       // (genome, bucket) index within the batch: failure flag slot
+    uint32_t per;      // expected entries per tile of this bucket
+};
 
-    const uint32_t b = it.b, p = it.p, np = it.np;
-    auto insert = [&](uint32_t r) {
-        if (*(volatile uint32_t*)&fail) return;
-        uint32_t s = (r * 0x9E3779B1u) >> (32 - kSlotBits);
-        for (int probe = 0; probe < kSlots; ++probe) {
-            const uint32_t k0 = keys[s];
-            if (k0 == r) {
-                atomicAdd(&cnts[s], 1u);
-                return;
-            }
-            if (k0 == kEmpty) {
-                const uint32_t old = atomicCAS(&keys[s], kEmpty, r);
-                if (old == kEmpty) {
-                    atomicAdd(&cnts[s], 1u);
-                    if (atomicAdd(&used, 1u) + 1u > limit) fail = 1u;
-                    return;
-                }
-                if (old == r) {
-                    atomicAdd(&cnts[s], 1u);
-                    return;
-                }
-            }
-            s = (s + 1u) & (kSlots - 1u);
-        }
-        fail = 1u;  // unreachable while used <= limit < kSlots - kSpThreads
-    };
-
-    const uint64_t ta = tbase[it.g] - tile_lo, tb = tbase[it.g + 1] - tile_lo;
-    // tiles per wave batch: expected entries of a batch fill about half the queue
-    const uint64_t nt = tb - ta;
-    const uint32_t per = nt ? (uint32_t)((it.n + nt - 1) / nt) : 1u;
-    uint32_t bt = (uint32_t)kQueue / 2u / (per + 1u);
-    bt = bt < 1u ? 1u : (bt > 64u ? 64u : bt);
-    uint32_t* q = queue[wave];
-    for (uint64_t tw = ta + (uint64_t)wave * bt; tw < tb; tw += (uint64_t)NW * bt) {
+// f(r) for every entry of bucket b in tiles [ta, tb), read as 16-byte chunks through a
+// per-wave queue: a wave takes bt tiles at a time (one per lane), lists the chunks that
+// cover their segments (tile-in-batch << 13 | chunk-in-tile) and streams them with kQU
+// loads in flight per lane; entries outside a segment are masked by position.
+template <typename F>
+__device__ __forceinline__ void walk_bucket(const uint32_t* __restrict__ ent,
+                                            const uint16_t* __restrict__ toff, uint32_t ldt,
+                                            uint32_t b, uint64_t ta, uint64_t tb, uint32_t bt,
+                                            uint32_t* q, uint32_t* slo, uint32_t* shi, F&& f) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint4* chunks = reinterpret_cast<const uint4*>(ent);
+    for (uint64_t tw = ta + (uint64_t)wave * bt; tw < tb; tw += (uint64_t)kNW * bt) {
         const uint64_t t = tw + (uint64_t)lane;
         const bool in = (uint32_t)lane < bt && t < tb;
         const uint32_t lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
         const uint32_t hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
-        const uint32_t nc = hi - lo;
+        const uint32_t c0 = lo >> 2, nc = hi > lo ? ((hi + 3u) >> 2) - c0 : 0u;
         uint32_t incl = nc;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -274,72 +234,294 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_count(
             if (lane >= d) incl += x;
         }
         const uint32_t total = __shfl(incl, 63);
-        const uint32_t ebase = (uint32_t)t * (uint32_t)kSpTile + lo;
+        if (total == 0u) continue;
         if (total <= (uint32_t)kQueue) {
+            slo[lane] = lo;
+            shi[lane] = hi;
             const uint32_t ex = incl - nc;
-            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = ebase + j;
+            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = ((uint32_t)lane << 13) | (c0 + j);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t v[kQueue / 64];
+            for (uint32_t r0 = 0; r0 < total; r0 += 64u * kQU) {
+                uint4 v[kQU];
+                uint32_t qe[kQU];
 #pragma unroll
-            for (int u = 0; u < kQueue / 64; ++u) {
-                const uint32_t e = (uint32_t)(u * 64 + lane);
-                v[u] = e < total ? ent[q[e]] : kEmpty;
+                for (int u = 0; u < kQU; ++u) {
+                    const uint32_t e = r0 + (uint32_t)(u * 64 + lane);
+                    qe[u] = q[e < total ? e : 0u];  // idle lanes re-read entry 0 (valid)
+                    v[u] = chunks[(tw + (qe[u] >> 13)) * (uint64_t)kTileChunks + (qe[u] & 8191u)];
+                    if (e >= total) qe[u] = kEmpty;
+                }
+#pragma unroll
+                for (int u = 0; u < kQU; ++u) {
+                    if (qe[u] == kEmpty) continue;
+                    const uint32_t tl = qe[u] >> 13, p0 = (qe[u] & 8191u) * 4u;
+                    const uint32_t l = slo[tl], h = shi[tl];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (p0 + i >= l && p0 + i < h) f(lane_of(v[u], i));
+                }
             }
-#pragma unroll
-            for (int u = 0; u < kQueue / 64; ++u)
-                if (v[u] != kEmpty && pass_of(v[u], np, R) == p) insert(v[u]);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {  // skewed batch: each lane walks its own segment
-            for (uint32_t j = 0; j < nc; ++j) {
-                const uint32_t r = ent[(uint64_t)ebase + j];
-                if (pass_of(r, np, R) == p) insert(r);
+            for (uint32_t j = lo; j < hi; ++j) f(ent[t * (uint64_t)kSpTile + j]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSpThreads) void k_sp_split(
+    const uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, uint32_t ldt,
+    const SplitItem* __restrict__ items, int R, uint32_t* __restrict__ out,
+    uint16_t* __restrict__ toff2, uint32_t* __restrict__ gb_fail) {
+    __shared__ __attribute__((aligned(16))) uint32_t sorted[kCaps];
+    __shared__ uint32_t hist[kMaxPasses];
+    __shared__ uint32_t q[kNW][kQueue];
+    __shared__ uint32_t slo[kNW][64], shi[kNW][64];
+    __shared__ uint32_t wsum[4], total_sh;
+
+    const uint32_t item = xcd_work_id();
+    const SplitItem it = items[item];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < kMaxPasses) hist[tid] = 0u;
+    __syncthreads();
+    uint32_t bt = (uint32_t)kQueue / 2u / (it.per / 4u + 2u);
+    bt = bt < 1u ? 1u : (bt > 64u ? 64u : bt);
+    const uint32_t np = it.np;
+    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave],
+                [&](uint32_t r) { atomicAdd(&hist[pass_of(r, np, R)], 1u); });
+    __syncthreads();
+    // exclusive scan of the pass histogram (threads 0..255)
+    uint32_t n0 = 0u, incl = 0u;
+    if (tid < kMaxPasses) {
+        n0 = hist[tid];
+        incl = n0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        if (lane == 63) wsum[wave] = incl;
+    }
+    __syncthreads();
+    if (tid < kMaxPasses) {
+        uint32_t pre = 0u;
+        for (int w = 0; w < wave; ++w) pre += wsum[w];
+        const uint32_t st = pre + incl - n0;
+        hist[tid] = st;
+        if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)st;
+        if (tid == 0) {
+            const uint32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            total_sh = tot;
+            toff2[(uint64_t)item * kT2 + np] = (uint16_t)(tot <= (uint32_t)kCaps ? tot : 0u);
+            if (tot > (uint32_t)kCaps) gb_fail[it.gb] = 1u;
+        }
+    }
+    __syncthreads();
+    const uint32_t total = total_sh;
+    if (total > (uint32_t)kCaps) return;  // staging overflow: the bucket goes to the fallback
+    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], [&](uint32_t r) {
+        const uint32_t slot = atomicAdd(&hist[pass_of(r, np, R)], 1u);
+        sorted[slot] = r;
+    });
+    __syncthreads();
+    uint32_t* dst = out + (uint64_t)item * kCaps;
+    const uint32_t n4 = total / 4;
+    for (uint32_t i = tid; i < n4; i += kSpThreads)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(sorted)[i];
+    if (tid < (int)(total & 3u)) dst[4 * n4 + tid] = sorted[4 * n4 + tid];
+}
+
+// Count work item: pass p of bucket b of genome g; its entries are segment p of split items
+// [s0, s1).
+struct CountItem {
+    uint32_t g, b, p, np;
+    uint32_t s0, s1;
+    uint32_t gb, n;
+};
+
+template <int SB, int NT>
+__global__ __launch_bounds__(NT) void k_sp_count(
+    const uint32_t* __restrict__ split, const uint16_t* __restrict__ toff2,
+    const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
+    const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
+    uint32_t* __restrict__ counts, unsigned long long* __restrict__ nk,
+    const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed, int abl,
+    unsigned long long* __restrict__ prof) {
+    // Slot = key << 32 | count; a slot is empty iff its count is 0, so every 32-bit residue
+    // (k = 21 uses all 32 bits) is a valid key.  `list` holds the slot of every key in the
+    // order it was first inserted: emission reads only those slots and stores contiguously.
+    constexpr int kSlots = 1 << SB, kSlotBits = SB, kNW = NT / 64;
+    constexpr int kList = kSlots * 3 / 4;          // distinct keys one table may hold
+    __shared__ unsigned long long tbl[kSlots];
+    __shared__ uint16_t list[kList];
+    __shared__ uint32_t nlist, fail;
+    __shared__ unsigned long long obase;
+    constexpr int kMaxProbe = 1024;
+    constexpr uint32_t SM = kSlots - 1u;
+    static_assert(kSlots <= 65536, "slot indices are u16");
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t cap = limit < (uint32_t)kList ? limit : (uint32_t)kList;
+    // Persistent: NT-thread workgroups walk the items.
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const CountItem it = items[item];
+    if (gb_fail[it.gb]) continue;  // the split overflowed: the fallback counts this bucket
+    const unsigned long long c0 = prof ? clock64() : 0ull;
+    unsigned long long iters = 0, calls = 0;
+    uint4* t4 = reinterpret_cast<uint4*>(tbl);
+    for (int i = tid; i < kSlots / 2; i += NT) t4[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (tid == 0) {
+        nlist = 0u;
+        fail = 0u;
+    }
+    __syncthreads();
+
+    // Each lane walks its own keys one probe per iteration: CAS(empty -> key|1) claims a
+    // slot, a slot holding the key gets +1, anything else sends the key to the next slot.
+    // The slots a lane claims stay in registers and are appended to `list` once per call
+    // (one LDS add per wave), so an iteration waits on a single LDS round trip.
+    auto insert_keys = [&](uint32_t (&r)[8], int n) {
+        ++calls;
+        uint32_t w[8];
+        int nw = 0;
+        uint32_t s = (r[0] * 0x9E3779B1u) >> (32 - kSlotBits);
+        int probes = 0;
+        while (__ballot(n > 0)) {
+            ++iters;
+            if (n > 0) {
+                const unsigned long long mine = ((unsigned long long)r[0] << 32) | 1ull;
+                const unsigned long long old = atomicCAS(&tbl[s], 0ull, mine);
+                const bool won = old == 0ull;
+                const bool match = !won && (uint32_t)(old >> 32) == r[0];
+                if (match) atomicAdd(&tbl[s], 1ull);
+                if (won) {
+#pragma unroll
+                    for (int i = 7; i > 0; --i) w[i] = w[i - 1];
+                    w[0] = s;
+                    ++nw;
+                }
+                if (won || match) {
+#pragma unroll
+                    for (int i = 0; i < 7; ++i) r[i] = r[i + 1];
+                    --n;
+                    probes = 0;
+                    s = (r[0] * 0x9E3779B1u) >> (32 - kSlotBits);
+                } else if (++probes == kMaxProbe) {
+                    fail = 1u;
+                    n = 0;
+                } else {
+                    s = (s + 1u) & SM;
+                }
+            }
+        }
+        // append this lane's claimed slots: wave prefix sum, one LDS add per wave
+        uint32_t incl = (uint32_t)nw;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        const uint32_t tot = __shfl(incl, 63);
+        uint32_t base = 0u;
+        if (lane == 0 && tot) base = atomicAdd(&nlist, tot);
+        base = __shfl(base, 0) + incl - (uint32_t)nw;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i < nw && base + i < (uint32_t)kList) list[base + i] = (uint16_t)w[i];
+    };
+
+    // Wave w owns split items s0 + w and s0 + w + kNW (and further ones when a bucket has
+    // more split items): it reads both segment bounds first, then issues the loads of up
+    // to 16 entries per lane before inserting any of them.
+    uint32_t sink = 0u;
+    for (uint32_t jA = it.s0 + (uint32_t)wave; jA < it.s1 && !(abl & 4); jA += 2u * kNW) {
+        const uint32_t jB = jA + kNW;
+        const bool hasB = jB < it.s1;
+        const uint32_t loA = toff2[(uint64_t)jA * kT2 + it.p], hiA = toff2[(uint64_t)jA * kT2 + it.p + 1];
+        const uint32_t loB = hasB ? toff2[(uint64_t)jB * kT2 + it.p] : 0u;
+        const uint32_t hiB = hasB ? toff2[(uint64_t)jB * kT2 + it.p + 1] : 0u;
+        const uint32_t nA = hiA - loA, n = nA + (hiB - loB);
+        const uint32_t* segA = split + (uint64_t)jA * kCaps + loA;
+        const uint32_t* segB = split + (uint64_t)(hasB ? jB : jA) * kCaps + loB;
+        for (uint32_t t0 = 0; t0 < n; t0 += 1024u) {
+            uint32_t r[16];
+            int cnt = 0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const uint32_t e = t0 + 64u * u + (uint32_t)lane;
+                const uint32_t* src = e < nA ? segA + e : (e < n ? segB + (e - nA) : segA);
+                r[u] = n ? *src : 0u;
+                cnt += e < n ? 1 : 0;   // valid entries of a lane are a prefix of r
+            }
+            if (abl & 1) {
+#pragma unroll
+                for (int u = 0; u < 16; ++u) sink ^= u < cnt ? r[u] : 0u;
+            } else {
+                uint32_t a8[8], b8[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    a8[u] = r[u];
+                    b8[u] = r[u + 8];
+                }
+                insert_keys(a8, cnt < 8 ? cnt : 8);
+                if (__ballot(cnt > 8)) insert_keys(b8, cnt > 8 ? cnt - 8 : 0);
             }
         }
     }
+    if (abl & 1) asm volatile("" ::"v"(sink));
+    if (prof && lane == 0) {
+        atomicAdd(&prof[3], iters);
+        atomicAdd(&prof[4], calls);
+    }
     __syncthreads();
-    if (fail) {
+    const uint32_t used = nlist;
+    const unsigned long long c1 = prof ? clock64() : 0ull;
+    if (fail || used > cap) {
         if (tid == 0) {
             const uint32_t at = atomicAdd(&failed[0], 1u);
-            failed[1 + at] = xcd_work_id();
+            failed[1 + at] = item;
         }
-        return;
+        __syncthreads();
+        continue;
     }
-
-    // Emit the occupied slots: slot i * 1024 + tid for round i; ballot compaction keeps
-    // each wave's stores of a round contiguous.
-    constexpr int ROUNDS = kSlots / kSpThreads;
-    uint32_t mine = 0u;
-#pragma unroll
-    for (int i = 0; i < ROUNDS; ++i) mine += __popcll(__ballot(keys[i * kSpThreads + tid] != kEmpty));
-    if (lane == 0) wsum[wave] = mine;
+    if (tid == 0) obase = (abl & 8) ? (unsigned long long)(item & 255u) * 4096ull   // timing only
+                                    : atomicAdd(&nk[it.g], (unsigned long long)used);
     __syncthreads();
-    if (tid == 0) {
-        uint32_t tot = 0u;
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t x = wsum[w];
-            wsum[w] = tot;
-            tot += x;
+    const uint64_t at = out_off[it.g] + obase;
+    const uint64_t hib = (uint64_t)it.b << R;
+    if (!(abl & 2)) {
+        for (uint32_t i0 = 0; i0 < used; i0 += 4u * NT) {
+            unsigned long long x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t i = i0 + u * NT + tid;
+                x[u] = tbl[list[i < used ? i : 0u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t i = i0 + u * NT + tid;
+                if (i < used) {
+                    codes[at + i] = hib | (x[u] >> 32);
+                    counts[at + i] = (uint32_t)x[u];
+                }
+            }
         }
-        obase = atomicAdd(&nk[it.g], (unsigned long long)tot);
     }
-    __syncthreads();
-    uint64_t at = out_off[it.g] + obase + wsum[wave];
-    const uint64_t hib = (uint64_t)b << R;
-    const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int i = 0; i < ROUNDS; ++i) {
-        const uint32_t key = keys[i * kSpThreads + tid];
-        const uint64_t mask = __ballot(key != kEmpty);
-        if (key != kEmpty) {
-            const uint64_t o = at + __popcll(mask & below);
-            codes[o] = hib | key;
-            counts[o] = cnts[i * kSpThreads + tid];
-        }
-        at += __popcll(mask);
+    // The table is reused by the next item: wait for this item's LDS reads only (their
+    // values fed the stores above), not for the stores to reach memory.
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (prof && tid == 0) {
+        const unsigned long long c2 = clock64();
+        atomicAdd(&prof[0], c1 - c0);
+        atomicAdd(&prof[1], c2 - c1);
+        atomicAdd(&prof[5], 1ull);
+    }
     }
 }
 
@@ -410,30 +592,30 @@ void launch_partition_k(int k, int canonical, unsigned tiles, hipStream_t s, con
     }
 }
 
-// Fallback for one failed work item: gather, radix sort, run-length encode, append.
-int fallback_item(Ctx* ctx, const SpItem& it, const uint32_t* ent, const uint16_t* toff,
-                  uint32_t ldt, uint64_t ta, uint64_t tb, int R, uint64_t out_off,
-                  unsigned long long* nk, uint64_t* codes, uint32_t* counts, hipStream_t s) {
-    const int n = (int)it.n;
+// Fallback for pass p of bucket b of genome g: gather, radix sort, run-length encode, append.
+int fallback_pass(Ctx* ctx, uint32_t g, uint32_t b, uint32_t p, uint32_t np, uint32_t n,
+                  const uint32_t* ent, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
+                  int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
+                  hipStream_t s) {
     size_t t_sort = 0, t_rle = 0;
     uint32_t* nul = nullptr;
-    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, nul, nul, n, 0, R, s));
-    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, nul, nul, nul, nul, n, s));
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, nul, nul, (int)n, 0, R, s));
+    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, nul, nul, nul, nul, (int)n, s));
     const size_t temp = std::max(t_sort, t_rle);
     const size_t arr = ((size_t)n * 4 + 255) & ~(size_t)255;
     int rc = ensure(ctx, ctx->sparse[5], 4 * arr + temp + 1024);
     if (rc) return rc;
-    char* p = static_cast<char*>(ctx->sparse[5].ptr);
-    uint32_t* a = static_cast<uint32_t*>(carve(p, (size_t)n * 4));
-    uint32_t* bsorted = static_cast<uint32_t*>(carve(p, (size_t)n * 4));
-    uint32_t* ukeys = static_cast<uint32_t*>(carve(p, (size_t)n * 4));
-    uint32_t* runs = static_cast<uint32_t*>(carve(p, (size_t)n * 4));
-    uint32_t* small = static_cast<uint32_t*>(carve(p, 256));
-    void* tmp = carve(p, temp);
+    char* p8 = static_cast<char*>(ctx->sparse[5].ptr);
+    uint32_t* a = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
+    uint32_t* bsorted = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
+    uint32_t* ukeys = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
+    uint32_t* runs = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
+    uint32_t* small = static_cast<uint32_t*>(carve(p8, 256));
+    void* tmp = carve(p8, temp);
     KMH_HIP(ctx, hipMemsetAsync(small, 0, 256, s));
     if (tb > ta) {
         hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)(tb - ta)), dim3(256), 0, s, ent, toff, ldt, ta, tb,
-                           it.b, (uint32_t)it.p, (uint32_t)it.np, R, a, small);
+                           b, p, np, R, a, small);
         KMH_HIP(ctx, hipGetLastError());
     }
     uint32_t m = 0;
@@ -445,7 +627,7 @@ int fallback_item(Ctx* ctx, const SpItem& it, const uint32_t* ent, const uint16_
     t = temp;
     KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(tmp, t, bsorted, ukeys, runs, small + 1, (int)m, s));
     hipLaunchKernelGGL(k_sp_append, dim3(1), dim3(256), 0, s, ukeys, runs, small + 1,
-                       (uint64_t)it.b << R, out_off, nk + it.g, codes, counts);
+                       (uint64_t)b << R, out_off, nk + g, codes, counts);
     KMH_HIP(ctx, hipGetLastError());
     KMH_HIP(ctx, hipStreamSynchronize(s));
     return KMH_OK;
@@ -476,7 +658,6 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     std::vector<uint64_t> out_off(G + 1);
     sparse_windows(offsets, G, k, out_off.data());
 
-    // Device metadata: goff, tbase (ctx->meta) and out_off (ctx->sparse[1], with the items).
     const uint64_t *d_goff, *d_tbase;
     rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
     if (rc) return rc;
@@ -485,10 +666,16 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
 
     const size_t tile_bytes = (size_t)kSpTile * sizeof(uint32_t);
     const size_t budget = env_mb("KMH_SP_BUDGET_MB", 8192) << 20;
-    const uint32_t target = (uint32_t)std::max<long>(1, env_long("KMH_SP_TARGET", 8192));
-    const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", 12288)),
-                                                    kSlots - kSpThreads - 1);
-    // batches of whole genomes whose entries fit the budget
+    // LDS hash table of the count kernel: 2^table_bits slots (KMH_SP_TABLE_BITS 12..14);
+    // smaller tables let several count workgroups share a CU and overlap their latencies.
+    const int table_bits = (int)std::min<long>(14, std::max<long>(12, env_long("KMH_SP_TABLE_BITS", 14)));
+    const unsigned wg_per_cu = 1u << (14 - table_bits);   // LDS-limited residency
+    const uint32_t target = (uint32_t)std::max<long>(1, env_long("KMH_SP_TARGET", 1l << (table_bits - 1)));
+    const uint32_t split_target = (uint32_t)std::max<long>(1, std::min<long>(env_long("KMH_SP_SPLIT", 12288), kCaps));
+    // KMH_SP_LIMIT caps the distinct keys of one table (tests force the fallback with it)
+    const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", 1l << table_bits)),
+                                                    1l << table_bits);
+    // batches of whole genomes whose step-1 entries fit the budget (at most 2^18 tiles)
     std::vector<std::pair<int, int>> batches;
     uint64_t max_tiles = 0;
     for (int g = 0; g < G;) {
@@ -497,12 +684,13 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         do {
             tiles += L.tbase[h + 1] - L.tbase[h];
             ++h;
-        } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget);
+        } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget &&
+                 tiles + (L.tbase[h + 1] - L.tbase[h]) <= (1u << 18));
         batches.emplace_back(g, h);
         max_tiles = std::max(max_tiles, tiles);
         g = h;
     }
-    if (max_tiles > 0xFFFFFFFFull / kSpTile) return fail(ctx, KMH_ERR_UNSUPPORTED, "batch too large");
+    if (max_tiles > (1u << 18)) return fail(ctx, KMH_ERR_UNSUPPORTED, "genome too large for the sparse path");
     const uint32_t ldt = (uint32_t)((max_tiles + 63) / 64 * 64);
     rc = ensure(ctx, ctx->sparse[2], std::max<uint64_t>(max_tiles, 1) * tile_bytes);
     if (!rc) rc = ensure(ctx, ctx->sparse[3], (size_t)ldt * (kSpBuckets + 1) * sizeof(uint16_t));
@@ -520,61 +708,121 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 
-        // bucket sizes -> work items
-        const size_t nb_n = (size_t)nG * kSpBuckets;
-        rc = ensure(ctx, ctx->sparse[4], nb_n * 4 + 4096);
+        // bucket sizes -> split and count work items
+        const size_t ngb = (size_t)nG * kSpBuckets;
+        rc = ensure(ctx, ctx->sparse[4], ngb * 8 + 4096);
         if (rc) return rc;
         uint32_t* d_nb = static_cast<uint32_t*>(ctx->sparse[4].ptr);
-        hipLaunchKernelGGL(k_sp_sizes, dim3((unsigned)nb_n), dim3(256), 0, s, toff, ldt, d_tbase, g0,
+        uint32_t* d_gbfail = d_nb + ngb;
+        KMH_HIP(ctx, hipMemsetAsync(d_gbfail, 0, ngb * 4, s));
+        hipLaunchKernelGGL(k_sp_sizes, dim3((unsigned)ngb), dim3(256), 0, s, toff, ldt, d_tbase, g0,
                            L.tbase[g0], d_nb);
         KMH_HIP(ctx, hipGetLastError());
-        std::vector<uint32_t> nb(nb_n);
-        KMH_HIP(ctx, hipMemcpyAsync(nb.data(), d_nb, nb_n * 4, hipMemcpyDeviceToHost, s));
+        std::vector<uint32_t> nb(ngb);
+        KMH_HIP(ctx, hipMemcpyAsync(nb.data(), d_nb, ngb * 4, hipMemcpyDeviceToHost, s));
         KMH_HIP(ctx, hipStreamSynchronize(s));
-        std::vector<SpItem> items;
-        items.reserve(nb_n * 2);
-        for (int gl = 0; gl < nG; ++gl)
+        std::vector<SplitItem> sitems;
+        std::vector<CountItem> citems;
+        sitems.reserve(ngb * 2);
+        citems.reserve(ngb * 4);
+        for (int gl = 0; gl < nG; ++gl) {
+            const int g = g0 + gl;
+            const uint64_t ta = L.tbase[g] - L.tbase[g0], tb = L.tbase[g + 1] - L.tbase[g0];
+            const uint64_t nt = tb - ta;
             for (int b = 0; b < kSpBuckets; ++b) {
                 const uint32_t n = nb[(size_t)gl * kSpBuckets + b];
                 if (!n) continue;
+                const uint32_t gb = (uint32_t)(gl * kSpBuckets + b);
                 const uint32_t np = std::min<uint32_t>(kMaxPasses, (n + target - 1) / target);
+                const uint32_t per = (uint32_t)((n + nt - 1) / nt);
+                const uint64_t ts = std::max<uint64_t>(1, split_target / (per + 1));
+                const uint32_t s0 = (uint32_t)sitems.size();
+                for (uint64_t t = ta; t < tb; t += ts)
+                    sitems.push_back(SplitItem{(uint32_t)b, (uint32_t)t, (uint32_t)std::min(t + ts, tb), np, gb, per});
+                const uint32_t s1 = (uint32_t)sitems.size();
                 for (uint32_t p = 0; p < np; ++p)
-                    items.push_back(SpItem{(uint32_t)(g0 + gl), (uint32_t)b, (uint16_t)p, (uint16_t)np, n});
+                    citems.push_back(CountItem{(uint32_t)g, (uint32_t)b, p, np, s0, s1, gb, n});
             }
-        if (items.empty()) continue;
-        // items + out_off + failed list in ctx->sparse[1]
-        const size_t ib = (items.size() * sizeof(SpItem) + 255) & ~(size_t)255;
+        }
+        if (citems.empty()) continue;
+        // split output + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
+        const size_t nsi = sitems.size();
+        const size_t sbytes = nsi * (size_t)kCaps * 4;
+        const size_t t2bytes = (nsi * kT2 * 2 + 255) & ~(size_t)255;
+        rc = ensure(ctx, ctx->sparse[6], sbytes + t2bytes);
+        if (rc) return rc;
+        uint32_t* d_split = static_cast<uint32_t*>(ctx->sparse[6].ptr);
+        uint16_t* d_toff2 = reinterpret_cast<uint16_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes);
+        const size_t sib = (nsi * sizeof(SplitItem) + 255) & ~(size_t)255;
+        const size_t cib = (citems.size() * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
-        const size_t fb = (items.size() + 1) * 4;
-        rc = ensure(ctx, ctx->sparse[1], ib + ob + fb);
+        const size_t fb = (citems.size() + 1) * 4;
+        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb);
         if (rc) return rc;
         char* base = static_cast<char*>(ctx->sparse[1].ptr);
-        SpItem* d_items = reinterpret_cast<SpItem*>(base);
-        uint64_t* d_out_off = reinterpret_cast<uint64_t*>(base + ib);
-        uint32_t* d_failed = reinterpret_cast<uint32_t*>(base + ib + ob);
-        KMH_HIP(ctx, hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(SpItem), hipMemcpyHostToDevice, s));
+        SplitItem* d_sitems = reinterpret_cast<SplitItem*>(base);
+        CountItem* d_citems = reinterpret_cast<CountItem*>(base + sib);
+        uint64_t* d_out_off = reinterpret_cast<uint64_t*>(base + sib + cib);
+        uint32_t* d_failed = reinterpret_cast<uint32_t*>(base + sib + cib + ob);
+        KMH_HIP(ctx, hipMemcpyAsync(d_sitems, sitems.data(), nsi * sizeof(SplitItem), hipMemcpyHostToDevice, s));
+        KMH_HIP(ctx, hipMemcpyAsync(d_citems, citems.data(), citems.size() * sizeof(CountItem), hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
-        time_begin(ctx, s, "k_sp_count");
-        hipLaunchKernelGGL(k_sp_count, dim3((unsigned)items.size()), dim3(kSpThreads), 0, s, ent, toff, ldt,
-                           d_tbase, L.tbase[g0], d_items, R, limit, d_out_off, d_codes, d_counts,
-                           reinterpret_cast<unsigned long long*>(d_nkmers), d_failed);
+        time_begin(ctx, s, "k_sp_split");
+        hipLaunchKernelGGL(k_sp_split, dim3((unsigned)nsi), dim3(kSpThreads), 0, s, ent, toff, ldt, d_sitems, R,
+                           d_split, d_toff2, d_gbfail);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
+        time_begin(ctx, s, "k_sp_count");
+        const unsigned cgrid = (unsigned)std::min<size_t>(citems.size(), (size_t)std::max(1, ctx->num_cu) * wg_per_cu);
+        // KMH_SP_PROF=1: per-phase cycle counters of k_sp_count on stderr (experiments)
+        unsigned long long* d_prof = nullptr;
+        const bool prof = env_long("KMH_SP_PROF", 0) != 0;
+        if (prof) {
+            rc = ensure(ctx, ctx->sparse[7], 256);
+            if (rc) return rc;
+            d_prof = static_cast<unsigned long long*>(ctx->sparse[7].ptr);
+            KMH_HIP(ctx, hipMemsetAsync(d_prof, 0, 256, s));
+        }
+#define KMH_SP_COUNT(SB, NT)                                                                         \
+    hipLaunchKernelGGL((k_sp_count<SB, NT>), dim3(cgrid), dim3(NT), 0, s, d_split, d_toff2, d_citems,   \
+                       (uint32_t)citems.size(), R, limit, d_out_off, d_codes, d_counts,                     \
+                       reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed,                  \
+                       (int)env_long("KMH_SP_ABL", 0), d_prof)
+        if (table_bits == 14) KMH_SP_COUNT(14, 1024);
+        else if (table_bits == 13) KMH_SP_COUNT(13, 1024);
+        else KMH_SP_COUNT(12, 512);
+#undef KMH_SP_COUNT
+        time_end(ctx, s);
+        KMH_HIP(ctx, hipGetLastError());
+        if (prof) {
+            unsigned long long h[8];
+            KMH_HIP(ctx, hipMemcpyAsync(h, d_prof, 64, hipMemcpyDeviceToHost, s));
+            KMH_HIP(ctx, hipStreamSynchronize(s));
+            std::fprintf(stderr, "k_sp_count prof: items %llu insert-phase cyc/item %.0f emit cyc/item %.0f "
+                         "iterations/call %.2f calls/item %.1f\n", h[5], (double)h[0] / h[5],
+                         (double)h[1] / h[5], (double)h[3] / (h[4] ? h[4] : 1), (double)h[4] / h[5]);
+        }
+        // passes left to the fallback: count items whose table overflowed, and every pass of
+        // a bucket whose split overflowed
         uint32_t nfail = 0;
+        std::vector<uint32_t> gbf(ngb);
         KMH_HIP(ctx, hipMemcpyAsync(&nfail, d_failed, 4, hipMemcpyDeviceToHost, s));
+        KMH_HIP(ctx, hipMemcpyAsync(gbf.data(), d_gbfail, ngb * 4, hipMemcpyDeviceToHost, s));
         KMH_HIP(ctx, hipStreamSynchronize(s));
+        std::vector<uint32_t> ids(nfail);
         if (nfail) {
-            std::vector<uint32_t> ids(nfail);
             KMH_HIP(ctx, hipMemcpyAsync(ids.data(), d_failed + 1, (size_t)nfail * 4, hipMemcpyDeviceToHost, s));
             KMH_HIP(ctx, hipStreamSynchronize(s));
-            for (uint32_t id : ids) {
-                const SpItem& it = items[id];
-                rc = fallback_item(ctx, it, ent, toff, ldt, L.tbase[it.g] - L.tbase[g0],
-                                   L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
-                                   reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, s);
-                if (rc) return rc;
-            }
+        }
+        for (const CountItem& it : citems)
+            if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
+        for (uint32_t id : ids) {
+            const CountItem& it = citems[id];
+            rc = fallback_pass(ctx, it.g, it.b, it.p, it.np, it.n, ent, toff, ldt, L.tbase[it.g] - L.tbase[g0],
+                               L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
+                               reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, s);
+            if (rc) return rc;
         }
     }
     return KMH_OK;

@@ -28,6 +28,18 @@ __global__ __launch_bounds__(T) void k_lds(uint32_t* out, uint32_t seed) {
             else if (MODE == 1) acc += atomicAdd(&tbl[a], 1u);
             else if (MODE == 3) reinterpret_cast<uint16_t*>(tbl)[a * 2 + (j & 1)] = (uint16_t)it;
             else if (MODE == 5) acc += tbl[a];
+            else if (MODE == 6) acc += atomicCAS(&tbl[a], 0u, r[j]);                     // cas b32, mostly fails
+            else if (MODE == 7) acc += atomicCAS(&tbl[a], tbl[a], r[j]);                 // cas b32, mostly succeeds
+            else if (MODE == 8) {
+                unsigned long long* t64 = reinterpret_cast<unsigned long long*>(tbl);
+                acc += (uint32_t)atomicCAS(&t64[a >> 1], 0ull, (unsigned long long)r[j]);  // cas b64
+            } else if (MODE == 9) {
+                unsigned long long* t64 = reinterpret_cast<unsigned long long*>(tbl);
+                atomicAdd(&t64[a >> 1], 1ull);                                           // add u64, no return
+            } else if (MODE == 10) {
+                unsigned long long* t64 = reinterpret_cast<unsigned long long*>(tbl);
+                acc += (uint32_t)t64[a >> 1];                                            // read b64
+            }
         }
     }
     __syncthreads();
@@ -71,5 +83,10 @@ int main() {
     run<4>("ds_add bank-per-lane", nb);
     run<3>("ds_write_b16 random", nb);
     run<5>("ds_read_b32 random", nb);
+    run<6>("ds_cmpst_rtn_b32 (fail)", nb);
+    run<7>("ds_cmpst_rtn_b32 (success)", nb);
+    run<8>("ds_cmpst_rtn_b64", nb);
+    run<9>("ds_add_u64", nb);
+    run<10>("ds_read_b64 random", nb);
     return 0;
 }

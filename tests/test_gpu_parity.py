@@ -385,7 +385,11 @@ def test_sparse_dev_passes_and_fallback(ctx, dev, oracle_lib, monkeypatch):
 
 
 def test_sparse_dev_low_complexity(ctx, dev, oracle_lib):
+    # poly-T: at k = 21 the forward code's low 32 bits are all ones (a residue that must not
+    # be mistaken for an empty slot)
     genomes = [np.full(300_000, ord("A"), np.uint8),
+               np.full(70_000, ord("T"), np.uint8),
+               np.frombuffer(b"A" * 5 + b"T" * 16 + b"G" * 3, np.uint8).copy(),
                np.frombuffer(b"AC" * 150_000, np.uint8).copy(),
                np.frombuffer(b"ACGTTTGACCA" * 30_000, np.uint8).copy()]
     for canonical in (0, 1):
