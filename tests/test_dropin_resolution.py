@@ -1,7 +1,8 @@
 """CPU: with kmer-ml_amd/activate on PYTHONPATH and the reference root as the working directory
 (how the reference's README runs its scripts), the reference's own CLI modules import unchanged,
-`kmerml.kmers.generate` resolves to this package, and the reference's other modules (statistics,
-features) still resolve to the reference.  Skipped where /root/reference is absent (GPU box)."""
+`kmerml.kmers.generate`, `.statistics` and `kmerml.ml.features` resolve to this package, and the
+reference's other modules (utils, scripts) still resolve to the reference.  Skipped where
+/root/reference is absent (GPU box)."""
 import os
 import subprocess
 import sys
@@ -35,8 +36,8 @@ def test_reference_cli_imports_this_package():
     import json
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["generate"].startswith(PKG)
-    assert d["statistics"].startswith(REFERENCE)
-    assert d["features"].startswith(REFERENCE)
+    assert d["statistics"].startswith(PKG)
+    assert d["features"].startswith(PKG)
     assert d["cli_file"].startswith(REFERENCE)
     assert d["cli_extractor"] == "kmerml.kmers.generate"
 
@@ -63,3 +64,27 @@ def test_reference_cli_counts_through_the_hip_library(tmp_path):
     else:
         assert r.returncode != 0
         assert "libkmerhip error" in r.stderr and "no HIP device" in r.stderr
+
+
+def test_reference_feature_cli_through_the_vectorised_extractor(tmp_path):
+    """scripts/generate_kmers_features.py, unchanged, on the k-mer files of the features/
+    fixture: the CSVs it writes equal the reference's own (entropy within 4 ulp)."""
+    import json
+    from test_features import GOLDEN, _assert_csv_equal, _read
+    cases = json.load(open(os.path.join(GOLDEN, "edge_cases.json")))["cases"]
+    kroot = tmp_path / "kmers"
+    for org, name, ks in (("orgA", "e1_mixed.fa", [2, 7, 4]), ("orgB", "e6_lowcomplex.fa", [1, 4, 12])):
+        case = next(c for c in cases if c["input"] == name and c["k_values"] == ks)
+        os.makedirs(kroot / org)
+        for fname, text in case["files"].items():
+            (kroot / org / fname).write_text(text)
+    out = tmp_path / "features"
+    env = dict(os.environ, PYTHONPATH=ACTIVATE, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-m", "scripts.generate_kmers_features", "-i", str(kroot),
+                        "-o", str(out), "-m", ""], env=env, capture_output=True, text=True,
+                       cwd=REFERENCE, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Generated 2 feature files" in r.stdout
+    for org in ("orgA", "orgB"):
+        _assert_csv_equal(_read(str(out / f"{org}_kmer_features.csv")),
+                          _read(os.path.join(GOLDEN, "features", f"{org}_kmer_features.csv")))
