@@ -5,11 +5,15 @@ the current directory) that serves
 
     kmerml.kmers.generate  -> kmer-ml_amd/kmerml/kmers/generate.py  (GPU KmerExtractor)
     kmerml.kmers.matrix    -> kmer-ml_amd/kmerml/kmers/matrix.py    (multi-GPU count matrix)
+    kmerml.kmers.statistics-> kmer-ml_amd/kmerml/kmers/statistics.py (vectorised feature CSVs)
+    kmerml.ml.features     -> kmer-ml_amd/kmerml/ml/features.py     (vectorised feature matrix)
     kmerml._native         -> kmer-ml_amd/kmerml/_native.py         (ctypes binding)
 
 while the `kmerml` package itself and all its other modules keep coming from the reference
 checkout.  So `python -m scripts.extract_kmers ...` run from the reference root counts on the
-GPU with no change to the reference (activate/sitecustomize.py imports this at startup).
+GPU, and `python -m scripts.generate_kmers_features ...` builds the same feature CSVs with the
+vectorised extractor, with no change to the reference (activate/sitecustomize.py imports this
+at startup).
 """
 import importlib.abc
 import importlib.util
@@ -21,6 +25,8 @@ MODULES = {
     "kmerml._native": "_native.py",
     "kmerml.kmers.generate": os.path.join("kmers", "generate.py"),
     "kmerml.kmers.matrix": os.path.join("kmers", "matrix.py"),
+    "kmerml.kmers.statistics": os.path.join("kmers", "statistics.py"),
+    "kmerml.ml.features": os.path.join("ml", "features.py"),
 }
 
 
