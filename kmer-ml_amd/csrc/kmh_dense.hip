@@ -289,6 +289,111 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
     }
 }
 
+// Fixed-capacity variant (k = 12 default): every bucket owns a row of FC suffix slots in
+// LDS, so one returning LDS add per k-mer yields both the bucket count and the k-mer's
+// rank, and the suffix is stored at row[bucket][rank] -- two LDS operations per k-mer
+// instead of three (histogram add, rank add, store).  The rows are then copied out as the
+// same padded, bucket-ordered segments k_partition writes (one thread per bucket, 16-byte
+// chunks).  If any bucket of the tile exceeds FC entries (uniform data: ~1e-8 per bucket;
+// repeats make it likelier) the tile is redone in place with the exact three-pass scheme.
+// Measured (experiment, KMH_FC=1): 126 us per 100 Mbp genome vs 97 us for k_partition --
+// the 117 KiB of rows leave one workgroup per CU, and the phase overlap of two co-resident
+// k_partition workgroups is worth more than the saved LDS operation.  Not the default.
+template <int K, int TPB, int FC>
+__global__ __launch_bounds__(TPB) void k_partition_fc(const uint8_t* __restrict__ seq,
+                                                      GenomeMap m, uint16_t* __restrict__ suf,
+                                                      uint16_t* __restrict__ toff, uint32_t ldt) {
+    constexpr int NBK = num_buckets<K>();
+    constexpr int TILE = TPB * kTileBpt;
+    constexpr int CAP = tile_cap<K>(TILE);
+    static_assert(FC % 8 == 0 && NBK * FC >= CAP, "rows hold whole chunks; the exact path reuses them");
+    static_assert(NBK <= TPB, "one bucket per thread");
+    __shared__ __attribute__((aligned(16))) uint16_t rows[NBK * FC];
+    __shared__ uint32_t cnt[NBK];
+    __shared__ uint32_t wsum[TPB / 64];
+    __shared__ uint32_t over;
+    __shared__ uint16_t cmap[CAP / 8];   // output chunk -> bucket
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = xcd_work_id();
+    const uint64_t gt = m.tile_lo + lt;
+    const int g = find_genome(m, gt);
+    const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)TILE;
+    const uint64_t ge = m.goff[g + 1];
+
+    if (tid < NBK) cnt[tid] = 0u;
+    if (tid == 0) over = 0u;
+    __syncthreads();
+
+    uint32_t km[kTileBpt];
+    walk<K>(seq, m, tstart, ge, TPB, [&](int j, uint32_t code, bool ok) {
+        km[j] = ok ? code : 0xFFFFFFFFu;
+        if (ok) {
+            const uint32_t b = code >> kSubBits;
+            const uint32_t r = atomicAdd(&cnt[b], 1u);
+            if (r < (uint32_t)FC) rows[b * FC + r] = (uint16_t)(code & (kSubBins - 1));
+            else over = 1u;
+        }
+    });
+    __syncthreads();
+    const bool exact = over != 0u;   // cnt holds the exact histogram either way
+
+    // Exclusive scan of the padded bucket sizes -> segment starts (entries).
+    const uint32_t nb = tid < NBK ? cnt[tid] : 0u;
+    const uint32_t v = (nb + 7u) & ~7u;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t pre = 0u, total = 0u;
+#pragma unroll
+    for (int w = 0; w < TPB / 64; ++w) {
+        pre += (w < wave) ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    const uint32_t start = pre + incl - v;
+    if (tid < NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)(start >> 3);
+    if (tid == 0) toff[(uint64_t)NBK * ldt + lt] = (uint16_t)(total >> 3);
+
+    uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)CAP);
+    if (!exact) {
+        // Each bucket pads its own row up to a whole chunk and marks its chunks in cmap; then
+        // every thread copies chunks c = tid, tid + TPB, ... so a wave's stores are contiguous.
+        if (tid < NBK) {
+            for (uint32_t q = nb; q < v; ++q)
+                rows[tid * FC + q] = (uint16_t)(kPadBase + ((8u * (uint32_t)tid + start + q) & (kPadBins - 1)));
+            for (uint32_t c = start >> 3; c < (start + v) >> 3; ++c) cmap[c] = (uint16_t)tid;
+            cnt[tid] = start >> 3;    // cnt now holds each bucket's first output chunk
+        }
+        __syncthreads();
+        for (uint32_t c = tid; c < (total >> 3); c += TPB) {
+            const uint32_t b = cmap[c];
+            dst[c] = reinterpret_cast<const uint4*>(rows + b * FC)[c - cnt[b]];
+        }
+        return;
+    }
+    // Exact path: scatter into the packed layout (rows reused as the tile buffer), pad,
+    // then one coalesced store of the tile.
+    uint16_t* sorted = rows;
+    if (tid < NBK) cnt[tid] = start;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kTileBpt; ++j) {
+        const uint32_t c = km[j];
+        if (c != 0xFFFFFFFFu) sorted[atomicAdd(&cnt[c >> kSubBits], 1u)] = (uint16_t)(c & (kSubBins - 1));
+    }
+    if (tid < NBK)
+        for (uint32_t q = start + nb; q < start + v; ++q)
+            sorted[q] = (uint16_t)(kPadBase + ((8u * (uint32_t)tid + q) & (kPadBins - 1)));
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(sorted);
+    for (uint32_t c = tid; c < (total >> 3); c += TPB) dst[c] = src[c];
+}
+
 // Add one 16-byte chunk (8 suffixes) into the LDS table; padding entries land in the
 // dummy bins past kSubBins.
 __device__ __forceinline__ void count8(uint32_t* tbl, uint4 q) {
@@ -703,7 +808,8 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
     return KMH_OK;
 }
 
-template <int K, int TPB, int PABL, int CABL, int GSX = 0, int UX = 0, int PIPE = 0, int SUBT = 1>
+template <int K, int TPB, int PABL, int CABL, int GSX = 0, int UX = 0, int PIPE = 0, int SUBT = 1,
+          int FCAP = 0>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
     constexpr int NBK = num_buckets<K>();
@@ -789,8 +895,12 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
         if (overlap && batch >= 2) KMH_HIP(ctx, hipStreamWaitEvent(sp, ctx->pipe_ev[3 + slot], 0));
         if (tiles) {
             time_begin(ctx, sp, "k_partition");
-            hipLaunchKernelGGL((k_partition<K, TPB, PABL, SUBT>), dim3((unsigned)tiles), dim3(TPB), 0, sp,
-                               d_seq, m, suf, toff, ldt);
+            if constexpr (FCAP > 0)
+                hipLaunchKernelGGL((k_partition_fc<K, TPB, FCAP>), dim3((unsigned)tiles), dim3(TPB), 0, sp,
+                                   d_seq, m, suf, toff, ldt);
+            else
+                hipLaunchKernelGGL((k_partition<K, TPB, PABL, SUBT>), dim3((unsigned)tiles), dim3(TPB), 0, sp,
+                                   d_seq, m, suf, toff, ldt);
             time_end(ctx, sp);
             KMH_HIP(ctx, hipGetLastError());
         }
@@ -859,6 +969,13 @@ int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
             }
         }
         if constexpr (K == 12) {
+            // KMH_FC=1: fixed-capacity partition (1024-thread tiles of the same 32768 windows)
+            if (env_long("KMH_FC", 0) == 1) {
+                int rc2 = make_layout(ctx, offsets, G, K, (uint64_t)1024 * kTileBpt, L);
+                if (!rc2) rc2 = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+                if (rc2) return rc2;
+                return run_partitioned<K, 1024, 0, 0, 0, 0, 0, 1, 112>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+            }
             if (subt == 2) return run_partitioned<K, 512, 0, 0, 0, 0, 0, 2>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
         }
         if constexpr (K == 12) {  // sweep (experiments): KMH_GSU=6 unpipelined, 4 = U 4 pipelined
