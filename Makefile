@@ -8,7 +8,7 @@ CSRC     := kmer-ml_amd/csrc
 OUTDIR   := kmer-ml_amd/kmerml/_lib
 OBJDIR   := $(CSRC)/build
 LIB      := $(OUTDIR)/libkmerhip.so
-OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o $(OBJDIR)/kmh_hash.o
+OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o $(OBJDIR)/kmh_hash.o $(OBJDIR)/kmh_io.o
 HDRS     := $(CSRC)/kmh_internal.h $(CSRC)/kmh_device.h include/kmerhip.h
 
 all: lib oracle selftest
@@ -17,7 +17,7 @@ lib: $(LIB)
 
 $(LIB): $(OBJS)
 	@mkdir -p $(OUTDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lz -lpthread
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

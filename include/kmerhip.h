@@ -170,6 +170,13 @@ int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uin
                            const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
                            int ranks, uint64_t rows_per_rank, uint32_t* d_rows, void* stream);
 
+/* ---- file output (host) -------------------------------------------------------- */
+/* Write n bytes to `path`: plain when gzip_level < 0, else gzip at that level (0..9; the
+ * reference uses 9 via gzip.open, generate.py:82-85) as independently deflated 8 MiB members
+ * on up to `threads` threads (0 = all cores, at most 16); any gzip reader returns the same
+ * bytes.  KMH_ERR_IO if the file cannot be written. */
+int kmh_write_file(const char* path, const void* data, uint64_t n, int gzip_level, int threads);
+
 /* ---- k{k}.txt text (host) ----------------------------------------------------- */
 /* Replaces the writer loop of _save_kmers_to_file (generate.py:89-91): one line
  * "<digits>\t<count>\n" per k-mer, digits A=0 T=1 C=2 G=3 (generate.py:71).

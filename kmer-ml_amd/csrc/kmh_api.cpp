@@ -318,49 +318,14 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
             const uint64_t off[2] = {0, n};
             if ((rc = kmh::dense_count(ctx, d_seq, off, 1, k, d_counts, ctx->stream))) return rc;
             if ((rc = kmh::dense_first(ctx, d_seq, off, 1, k, d_first, ctx->stream))) return rc;
-            std::vector<uint32_t> counts(bins), first(bins);
-            KMH_HIP(ctx, hipMemcpyAsync(counts.data(), d_counts, bins * 4, hipMemcpyDeviceToHost, ctx->stream));
-            KMH_HIP(ctx, hipMemcpyAsync(first.data(), d_first, bins * 4, hipMemcpyDeviceToHost, ctx->stream));
-            KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            // First-occurrence order: every window start is the first occurrence of at
-            // most one k-mer, so scatter codes to their first position and scan.
-            std::vector<uint32_t> at(n ? n : 1, 0xFFFFFFFFu);
-            uint64_t distinct = 0;
-            for (size_t c = 0; c < bins; ++c) {
-                if (counts[c]) {
-                    if (first[c] >= n) return fail(ctx, KMH_ERR_HIP, "inconsistent first-occurrence table");
-                    at[first[c]] = (uint32_t)c;
-                    ++distinct;
-                }
-            }
-            r->codes.reserve(distinct);
-            r->counts.reserve(distinct);
-            r->first.reserve(distinct);
-            for (uint64_t p = 0; p < n; ++p) {
-                const uint32_t c = at[p];
-                if (c != 0xFFFFFFFFu) {
-                    r->codes.push_back(c);
-                    r->counts.push_back(counts[c]);
-                    r->first.push_back(p);
-                }
-            }
-            if (r->codes.size() != distinct) return fail(ctx, KMH_ERR_HIP, "duplicate first occurrence");
-        } else {
-            std::vector<uint64_t> codes, first;
-            std::vector<uint32_t> counts;
-            if ((rc = kmh::sparse_count(ctx, d_seq, n, k, canonical, codes, counts, first, ctx->stream)))
+            if ((rc = kmh::dense_order(ctx, d_counts, d_first, bins, n, r->codes, r->counts, r->first,
+                                       ctx->stream)))
                 return rc;
-            std::vector<uint64_t> idx(codes.size());
-            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
-            std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return first[a] < first[b]; });
-            r->codes.resize(idx.size());
-            r->counts.resize(idx.size());
-            r->first.resize(idx.size());
-            for (size_t i = 0; i < idx.size(); ++i) {
-                r->codes[i] = codes[idx[i]];
-                r->counts[i] = counts[idx[i]];
-                r->first[i] = first[idx[i]];
-            }
+
+        } else {
+            if ((rc = kmh::sparse_count(ctx, d_seq, n, k, canonical, r->codes, r->counts, r->first,
+                                        ctx->stream)))
+                return rc;
         }
     } catch (const std::bad_alloc&) {
         return fail(ctx, KMH_ERR_NOMEM, "out of host memory");

@@ -41,7 +41,7 @@ struct Ctx {
     hipEvent_t pipe_ev[5] = {};        // input-ready, partition-done x2, count-done x2
     std::string err;
     // device workspace
-    DevBuf seq, suf, toff, meta, out, out2, fix, sparse[8];
+    DevBuf seq, suf, toff, meta, out, out2, fix, sparse[8], order;
     // pinned staging for small host->device tables
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
@@ -106,11 +106,17 @@ int rows_decode_u8(Ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
 
 // ---- sparse path (kmh_sparse.hip) ----
 // Counts the windows of d_seq[0, n) for 13 <= k <= 32 (works for any 1 <= k <= 32).
-// On return the host vectors hold the distinct codes in ascending order, their counts
-// and their first window start.
+// On return the host vectors hold the distinct codes in first-occurrence order (sorted by
+// first window start on the device), their counts and their first window start.
 int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
                  std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
                  std::vector<uint64_t>& first, hipStream_t s);
+
+// First-occurrence order of a dense count row on the device (kmh_sparse.hip): the codes with
+// a nonzero count, sorted by their first window start, with counts and starts, to the host.
+int dense_order(Ctx* ctx, const uint32_t* d_counts, const uint32_t* d_first, size_t bins,
+                uint64_t n, std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
+                std::vector<uint64_t>& first, hipStream_t s);
 
 // ---- device-resident sparse path (kmh_hash.hip) ----
 // Windows per genome -> cumulative output offsets (out_off: G + 1 entries, nullable).

@@ -1,0 +1,86 @@
+// kmh_io.cpp -- file output of the k{k}.txt text (generate.py:68-91).
+//
+// The reference writes gzip with Python's gzip module at level 9 (generate.py:82-85) on one
+// core, the slowest stage of its pipeline at k = 12.  Here the text is
+// cut into blocks that are deflated concurrently, each as a complete gzip member; the members
+// are written in order.  A gzip file may hold several members and decompresses to their
+// concatenation (RFC 1952 section 2.2), so every reader sees the same text.  The compressed
+// bytes differ from the reference's, which embed a timestamp and are not reproducible anyway.
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kmh_internal.h"
+
+namespace {
+
+bool deflate_member(const uint8_t* src, size_t n, int level, std::vector<uint8_t>& out) {
+    z_stream z{};
+    // windowBits 15 + 16: gzip wrapper (header with mtime 0, CRC-32 and length trailer)
+    if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    out.resize(deflateBound(&z, (uLong)n) + 64);
+    z.next_in = const_cast<Bytef*>(src);
+    z.avail_in = (uInt)n;
+    z.next_out = out.data();
+    z.avail_out = (uInt)out.size();
+    const int r = deflate(&z, Z_FINISH);
+    out.resize(out.size() - z.avail_out);
+    deflateEnd(&z);
+    return r == Z_STREAM_END;
+}
+
+}  // namespace
+
+extern "C" int kmh_write_file(const char* path, const void* data, uint64_t n, int gzip_level,
+                              int threads) {
+    if (!path || (n && !data)) {
+        kmh::set_thread_error("kmh_write_file: NULL argument");
+        return KMH_ERR_INVALID;
+    }
+    if (gzip_level > 9) {
+        kmh::set_thread_error("kmh_write_file: gzip level must be <= 9");
+        return KMH_ERR_INVALID;
+    }
+    FILE* f = std::fopen(path, "wb");
+    if (!f) {
+        kmh::set_thread_error(std::string("cannot open ") + path + " for writing");
+        return KMH_ERR_IO;
+    }
+    const uint8_t* src = static_cast<const uint8_t*>(data);
+    bool ok = true;
+    if (gzip_level < 0) {
+        ok = n == 0 || std::fwrite(src, 1, n, f) == n;
+    } else {
+        constexpr size_t kBlock = 8u << 20;   // 8 MiB of text per member
+        const size_t nblk = n ? (n + kBlock - 1) / kBlock : 1;
+        unsigned nt = threads > 0 ? (unsigned)threads : std::thread::hardware_concurrency();
+        nt = std::max(1u, std::min<unsigned>({nt, 16u, (unsigned)nblk}));
+        std::vector<std::vector<uint8_t>> out(nblk);
+        std::atomic<size_t> next{0};
+        std::atomic<bool> good{true};
+        auto work = [&]() {
+            for (size_t b = next++; b < nblk; b = next++) {
+                const size_t lo = b * kBlock, len = std::min(kBlock, (size_t)n - lo);
+                if (!deflate_member(src + lo, n ? len : 0, gzip_level, out[b])) good = false;
+            }
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+        work();
+        for (auto& t : pool) t.join();
+        ok = good;
+        for (size_t b = 0; ok && b < nblk; ++b)
+            ok = out[b].empty() || std::fwrite(out[b].data(), 1, out[b].size(), f) == out[b].size();
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) {
+        kmh::set_thread_error(std::string("error writing ") + path);
+        return KMH_ERR_IO;
+    }
+    return KMH_OK;
+}

@@ -52,6 +52,44 @@ __global__ __launch_bounds__(256) void k_run_first(const uint32_t* __restrict__ 
     if (r < *nruns) first[r] = pos_sorted[run_start[r]];
 }
 
+__global__ __launch_bounds__(256) void k_iota(uint32_t* __restrict__ out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_gather_runs(const uint32_t* __restrict__ idx,
+                                                     const uint64_t* __restrict__ codes,
+                                                     const uint32_t* __restrict__ counts, uint64_t n,
+                                                     uint64_t* __restrict__ codes_out,
+                                                     uint32_t* __restrict__ counts_out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        codes_out[i] = codes[idx[i]];
+        counts_out[i] = counts[idx[i]];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_nonzero(const uint32_t* __restrict__ counts, uint64_t bins,
+                                                 uint8_t* __restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < bins) flags[i] = counts[i] ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_gather_first(const uint32_t* __restrict__ codes,
+                                                      const uint32_t* __restrict__ first,
+                                                      const uint64_t* __restrict__ n,
+                                                      uint32_t* __restrict__ keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < *n) keys[i] = first[codes[i]];
+}
+
+__global__ __launch_bounds__(256) void k_gather_counts(const uint32_t* __restrict__ codes,
+                                                       const uint32_t* __restrict__ counts,
+                                                       uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = counts[codes[i]];
+}
+
 void* carve(char*& p, size_t bytes) {
     void* r = p;
     p += (bytes + 255) & ~(size_t)255;
@@ -59,6 +97,64 @@ void* carve(char*& p, size_t bytes) {
 }
 
 }  // namespace
+
+// generate.py:36,58 keeps k-mers in first-occurrence order (the dict's insertion order, which
+// fixes the line order of k{k}.txt, :89-91).  Each k-mer's first start is unique, so sorting
+// the nonzero bins by it gives that order: compact, radix sort by start, gather the counts.
+int dense_order(Ctx* ctx, const uint32_t* d_counts, const uint32_t* d_first, size_t bins,
+                uint64_t n, std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
+                std::vector<uint64_t>& first, hipStream_t s) {
+    codes.clear();
+    counts.clear();
+    first.clear();
+    const int N = (int)bins;
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < n) ++bits;   // first starts are < n
+    size_t t_sel = 0, t_sort = 0;
+    uint32_t* nul = nullptr;
+    uint8_t* nulf = nullptr;
+    uint64_t* nuln = nullptr;
+    hipcub::CountingInputIterator<uint32_t> iota(0u);
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(nullptr, t_sel, iota, nulf, nul, nuln, N, s));
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, nul, nul, nul, nul, N, 0, bits, s));
+    const size_t temp = std::max(t_sel, t_sort);
+    const size_t a4 = ((bins * 4) + 255) & ~(size_t)255;
+    int rc = ensure(ctx, ctx->order, 5 * a4 + (((bins) + 255) & ~(size_t)255) + temp + 1024);
+    if (rc) return rc;
+    char* p = static_cast<char*>(ctx->order.ptr);
+    uint32_t* sel = static_cast<uint32_t*>(carve(p, bins * 4));
+    uint32_t* keys = static_cast<uint32_t*>(carve(p, bins * 4));
+    uint32_t* keys2 = static_cast<uint32_t*>(carve(p, bins * 4));
+    uint32_t* vals2 = static_cast<uint32_t*>(carve(p, bins * 4));
+    uint32_t* cnt2 = static_cast<uint32_t*>(carve(p, bins * 4));
+    uint8_t* flags = static_cast<uint8_t*>(carve(p, bins));
+    uint64_t* nsel = static_cast<uint64_t*>(carve(p, 64));
+    void* tmp = carve(p, temp);
+    const unsigned g = (unsigned)((bins + 255) / 256);
+    hipLaunchKernelGGL(k_nonzero, dim3(g), dim3(256), 0, s, d_counts, (uint64_t)bins, flags);
+    KMH_HIP(ctx, hipGetLastError());
+    size_t t = temp;
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(tmp, t, iota, flags, sel, nsel, N, s));
+    hipLaunchKernelGGL(k_gather_first, dim3(g), dim3(256), 0, s, sel, d_first, nsel, keys);
+    KMH_HIP(ctx, hipGetLastError());
+    uint64_t m = 0;
+    KMH_HIP(ctx, hipMemcpyAsync(&m, nsel, 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    if (m == 0) return KMH_OK;
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t, keys, keys2, sel, vals2, (int)m, 0, bits, s));
+    hipLaunchKernelGGL(k_gather_counts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, vals2, d_counts, m, cnt2);
+    KMH_HIP(ctx, hipGetLastError());
+    std::vector<uint32_t> c32(m), f32(m);
+    counts.resize(m);
+    KMH_HIP(ctx, hipMemcpyAsync(c32.data(), vals2, m * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(f32.data(), keys2, m * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(counts.data(), cnt2, m * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    codes.assign(c32.begin(), c32.end());
+    first.assign(f32.begin(), f32.end());
+    return KMH_OK;
+}
 
 int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
                  std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
@@ -130,12 +226,23 @@ int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonica
     hipLaunchKernelGGL(k_run_first, dim3((unsigned)((nruns + 255) / 256)), dim3(256), 0, s,
                        pos_b, pos_a, nruns_d, first_d);
     KMH_HIP(ctx, hipGetLastError());
+    // First-occurrence order (the reference dict's order, generate.py:36,58): sort the runs
+    // by their first start on the device, then gather codes and counts.
+    int bits = 1;
+    while (bits < 64 && (1ull << bits) < n) ++bits;
+    const unsigned gr = (unsigned)((nruns + 255) / 256);
+    hipLaunchKernelGGL(k_iota, dim3(gr), dim3(256), 0, s, pos_a, nruns);
+    KMH_HIP(ctx, hipGetLastError());
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t, first_d, keys_b, pos_a, pos_b, (int)nruns, 0, bits, s));
+    hipLaunchKernelGGL(k_gather_runs, dim3(gr), dim3(256), 0, s, pos_b, keys_a, cnt_d, nruns, codes_all, pos_a);
+    KMH_HIP(ctx, hipGetLastError());
     codes.resize(nruns);
     counts.resize(nruns);
     first.resize(nruns);
-    KMH_HIP(ctx, hipMemcpyAsync(codes.data(), keys_a, nruns * 8, hipMemcpyDeviceToHost, s));
-    KMH_HIP(ctx, hipMemcpyAsync(counts.data(), cnt_d, nruns * 4, hipMemcpyDeviceToHost, s));
-    KMH_HIP(ctx, hipMemcpyAsync(first.data(), first_d, nruns * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(codes.data(), codes_all, nruns * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(counts.data(), pos_a, nruns * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(first.data(), keys_b, nruns * 8, hipMemcpyDeviceToHost, s));
     KMH_HIP(ctx, hipStreamSynchronize(s));
     return KMH_OK;
 }

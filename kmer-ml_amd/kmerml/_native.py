@@ -49,6 +49,7 @@ SIGNATURES = [
     ("kmh_first_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
     ("kmh_synth_dev", _c.c_int, [_vp, _vp, _u64, _u64, _c.c_int, _u64, _vp]),
     ("kmh_format_lines", _c.c_int64, [_c.c_int, _vp, _vp, _u64, _vp, _u64]),
+    ("kmh_write_file", _c.c_int, [_c.c_char_p, _vp, _u64, _c.c_int, _c.c_int]),
     ("kmh_count_sparse_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp]),
     ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
@@ -278,6 +279,12 @@ class FastaFile:
             self.close()
         except Exception:
             pass
+
+
+def write_file(path, data, gzip_level=-1, threads=0):
+    """Write bytes to path (gzip_level 0..9: multi-member gzip deflated on several threads)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    _check(lib().kmh_write_file(os.fsencode(str(path)), _ptr(buf), len(data), int(gzip_level), int(threads)))
 
 
 def format_lines(k, codes, counts):

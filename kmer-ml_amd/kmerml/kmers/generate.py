@@ -22,7 +22,6 @@ Differences: 1 <= k <= 32 is supported (k >= 33 raises NotImplemente
 k <= 0 raises ValueError); counting never falls back to the CPU -- without the HIP
 library or a device it raises.
 """
-import gzip
 import os
 from pathlib import Path
 
@@ -84,12 +83,8 @@ class KmerExtractor:
         return organism_dir / (f"k{k}.txt.gz" if self.compress else f"k{k}.txt")
 
     def _write_bytes(self, path, data):
-        if self.compress:
-            with gzip.open(path, "wb") as f:
-                f.write(data)
-        else:
-            with open(path, "wb") as f:
-                f.write(data)
+        # gzip.open's default level 9 (generate.py:82-85), deflated on several host threads
+        _native.write_file(path, data, gzip_level=9 if self.compress else -1)
 
     def _write_kmer_file(self, organism_id, k, codes, counts):
         self._write_bytes(self._kmer_path(organism_id, k), _native.format_lines(k, codes, counts))

@@ -113,3 +113,55 @@ def test_format_lines_matches_reference_text(k):
 
 def test_format_lines_empty():
     assert _native.format_lines(8, np.empty(0, np.uint64), np.empty(0, np.uint64)) == b""
+
+
+def test_write_file_plain_and_parallel_gzip(tmp_path):
+    """kmh_write_file: plain bytes, and multi-member gzip that any reader decompresses to the
+    same bytes (blocks of 8 MiB deflated on several threads)."""
+    import gzip
+    rng = np.random.default_rng(0)
+    data = ("".join(f"{x}\t{y}\n" for x, y in zip(rng.integers(0, 10**12, 1_300_000),
+                                                 rng.integers(1, 99, 1_300_000)))).encode()
+    assert len(data) > 2 * (8 << 20)
+    p = tmp_path / "k12.txt"
+    _native.write_file(p, data)
+    assert p.read_bytes() == data
+    for level, threads in ((9, 0), (1, 3), (9, 1)):
+        g = tmp_path / f"k12_{level}_{threads}.txt.gz"
+        _native.write_file(g, data, gzip_level=level, threads=threads)
+        assert gzip.decompress(g.read_bytes()) == data
+        with gzip.open(g, "rt") as f:
+            assert f.read(20) == data[:20].decode()
+    e = tmp_path / "empty.txt.gz"
+    _native.write_file(e, b"", gzip_level=9)
+    assert gzip.decompress(e.read_bytes()) == b""
+    with pytest.raises(OSError):
+        _native.write_file(tmp_path / "no" / "such" / "dir.txt", b"x")
+
+
+def test_format_lines_many_blocks_and_partial_buffer():
+    """The threaded formatter (blocks of 2^18 lines) equals the reference's text
+    (generate.py:86-91, restated by oracle/kmers.py) across block boundaries, and a short
+    buffer receives the whole lines that fit."""
+    rng = np.random.default_rng(11)
+    k, n = 9, 700_000
+    codes = rng.integers(0, 1 << (2 * k), n, dtype=np.uint64)
+    counts = rng.integers(1, 10**7, n, dtype=np.uint64)
+    text = _native.format_lines(k, codes, counts)
+    want_head = "".join(okmers.DIGIT[b] for b in okmers.code_kmer(int(codes[0]), k)) + f"\t{counts[0]}\n"
+    assert text.startswith(want_head.encode())
+    for i in (262_143, 262_144, 524_288, n - 1):
+        line = "".join(okmers.DIGIT[b] for b in okmers.code_kmer(int(codes[i]), k)) + f"\t{counts[i]}\n"
+        assert line.encode() in text
+    lines = text.split(b"\n")[:-1]
+    assert len(lines) == n
+    assert lines[524_288] == ("".join(okmers.DIGIT[b] for b in okmers.code_kmer(int(codes[524_288]), k))
+                              + f"\t{counts[524_288]}").encode()
+    L = _native.lib()
+    cap = len(text) // 3
+    import ctypes
+    buf = ctypes.create_string_buffer(cap)
+    total = L.kmh_format_lines(k, codes.ctypes.data, counts.ctypes.data, n, buf, cap)
+    assert total == len(text)
+    cut = text[:cap].rfind(b"\n") + 1
+    assert buf.raw[:cut] == text[:cut]
