@@ -49,6 +49,14 @@ constexpr int kMaxPasses = 256;
 constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
 
+// Workgroup barrier for LDS only.  __syncthreads() is also a release fence for global
+// memory, i.e. it waits for every store the wave has in flight (s_waitcnt vmcnt(0)); the
+// persistent count kernel never reads back what it stores, so its barriers need only the
+// LDS operations to be complete and let one item's output stores drain under the next item.
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ __volatile__("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // 2-bit-group reversal of the low 2K bits of ~x: the reverse complement of a K-mer code.
 template <int K>
 __device__ __forceinline__ uint64_t revcomp(uint64_t x) {
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         nlist = 0u;
         fail = 0u;
     }
-    __syncthreads();
+    lds_barrier();
 
     // Each lane walks its own keys one probe per iteration: CAS(empty -> key|1) claims a
     // slot, a slot holding the key gets +1, anything else sends the key to the next slot.
@@ -476,7 +484,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         atomicAdd(&prof[3], iters);
         atomicAdd(&prof[4], calls);
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t used = nlist;
     const unsigned long long c1 = prof ? clock64() : 0ull;
     if (fail || used > cap) {
@@ -484,12 +492,12 @@ __global__ __launch_bounds__(NT) void k_sp_count(
             const uint32_t at = atomicAdd(&failed[0], 1u);
             failed[1 + at] = item;
         }
-        __syncthreads();
+        lds_barrier();
         continue;
     }
     if (tid == 0) obase = (abl & 8) ? (unsigned long long)(item & 255u) * 4096ull   // timing only
                                     : atomicAdd(&nk[it.g], (unsigned long long)used);
-    __syncthreads();
+    lds_barrier();
     const uint64_t at = out_off[it.g] + obase;
     const uint64_t hib = (uint64_t)it.b << R;
     if (!(abl & 2)) {
@@ -512,10 +520,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     }
     // The table is reused by the next item: wait for this item's LDS reads only (their
     // values fed the stores above), not for the stores to reach memory.
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    lds_barrier();
     if (prof && tid == 0) {
         const unsigned long long c2 = clock64();
         atomicAdd(&prof[0], c1 - c0);
