@@ -91,6 +91,29 @@ def cpu_baseline(sample, k):
             "seconds": dt, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
 
 
+def cpu_threads_baseline(k, bases_per_thread=25_000_000, threads=16):
+    """A stronger CPU reference point beside the 1-core loop: the C restatement of the
+    counting rule (oracle/kmer_oracle.c, dense 4^k table, one private table per thread) on
+    `threads` host threads, each counting its own synthetic genome (ctypes releases the GIL).
+    Not the reference's code path -- reported as kind "port"."""
+    sys.path.insert(0, HERE)
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import corac
+    from oracle import synth as osynth
+    if k > 12:
+        return None
+    seqs = [corac.synth(bases_per_thread, osynth.genome_seed(g)) for g in range(threads)]
+    corac.count_dense(seqs[0][:1000], k)       # load the library outside the timed region
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        tables = list(ex.map(lambda q: corac.count_dense(q, k), seqs))
+    dt = time.perf_counter() - t0
+    assert all(int(t.sum()) == bases_per_thread - k + 1 for t in tables)
+    return {"value": threads * bases_per_thread / dt, "unit": "bases/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} synthetic genomes x {bases_per_thread} bases, k={k}: C restatement of "
+                      f"generate.py:49-58 (oracle/kmer_oracle.c) on {threads} threads, {dt:.2f} s"}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -140,9 +163,10 @@ def main():
     bins = 1 << (2 * k)
 
     # CPU baseline first (rank 0, N = 1 only), so it never overlaps GPU timing.
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and a.cpu_sample > 0:
         cpu = cpu_baseline(a.cpu_sample, k)
+        cpu_mt = cpu_threads_baseline(k)
 
     ctx = _native.context(dev_index)
     stream = torch.cuda.current_stream(dev)
@@ -333,6 +357,7 @@ def main():
                         for n, (l, t) in kernels.items()},
             "rows_checked": ok,
             "cpu_baseline": cpu,
+            "cpu_threads_baseline": cpu_mt,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)

@@ -1,0 +1,51 @@
+"""Merge rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/r01_pmc_traffic.json.
+
+    python profiles/pmc_summary.py FETCH_CSV WRITE_CSV KEY_SUFFIX [NOTE]
+
+For each kernel: mean FETCH_SIZE and WRITE_SIZE (KB) per dispatch and
+hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (FETCH_SIZE doubled: gfx950
+reports half the bytes of 16-B-per-lane loads, MI355X_MICROARCH.md HBM section).  Entries are
+stored under "<kernel><KEY_SUFFIX>", e.g. "k_sp_count:k21:L250000000", which bench.py reads.
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "r01_pmc_traffic.json")
+
+
+def per_kernel(path, counter):
+    vals = defaultdict(list)
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] != counter:
+            continue
+        name = row["Kernel_Name"].replace("(anonymous namespace)", "")
+        short = re.sub(r"<.*", "", name.split("(")[0]).split("::")[-1].split()[-1]
+        vals[short].append(float(row["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in vals.items()}
+
+
+def main():
+    fetch_csv, write_csv, suffix = sys.argv[1:4]
+    note = sys.argv[4] if len(sys.argv) > 4 else ""
+    f = per_kernel(fetch_csv, "FETCH_SIZE")
+    w = per_kernel(write_csv, "WRITE_SIZE")
+    d = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    for k in sorted(set(f) & set(w)):
+        fk, n = f[k]
+        wk, _ = w[k]
+        entry = {"FETCH_SIZE_KB": round(fk, 1), "WRITE_SIZE_KB": round(wk, 1), "dispatches": n,
+                 "hbm_bytes_per_launch": int(round((2 * fk + wk) * 1024))}
+        if note:
+            entry["note"] = note
+        d[k + suffix] = entry
+        print(k + suffix, entry)
+    json.dump(d, open(OUT, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
