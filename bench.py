@@ -147,7 +147,10 @@ def main():
     dev_index = 0 if a.single_device else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    # A process group for N > 1, or when torch.distributed.run launched a single rank with an
+    # explicit assembly mode (exercises the RCCL code path on one GPU).
+    use_dist = world > 1 or (a.assemble in ("u8", "u32") and "RANK" in os.environ)
+    if use_dist:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
         else:
@@ -362,7 +365,7 @@ def main():
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     if not ok:

@@ -415,3 +415,49 @@ def test_sparse_dev_rejects_k(ctx, dev):
     with pytest.raises(NotImplementedError):
         ctx.count_sparse_dev(d.data_ptr(), np.array([0, 64], np.uint64), 12, 0, o.data_ptr(), o.data_ptr(),
                              o.data_ptr())
+
+
+# ---------------------------------------------------------------- RCCL code paths, one GPU
+def _torchrun(args, timeout=600):
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def test_count_matrix_rccl_u8_assembly(tmp_path, oracle_lib):
+    """count_matrix under an RCCL process group (world size 1 on the test box): encode u8 +
+    escapes, all-reduce, all-gather, decode -- bit-identical to counting directly."""
+    files = []
+    for i in range(3):
+        p = tmp_path / f"g{i}.fa"
+        seq = osynth.synth_bases(200_000 + 1000 * i, osynth.genome_seed(i)).tobytes()
+        if i == 1:   # a k-mer repeated > 255 times: exercises the escape list
+            seq = b"ACGTTGCA" * 2000 + seq
+        osynth.write_fasta(p, [(f"SYN_{i}", seq)])
+        files.append(str(p))
+    out = tmp_path / "m.npy"
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = _torchrun([os.path.join(here, "rccl_probe.py"), str(out), "8"] + files)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = np.load(out).view(np.uint32)
+    want = np.stack([kmatrix._hip_count_block([f], 8, 0).cpu().numpy().view(np.uint32)[0] for f in files])
+    assert got.shape == want.shape and got.max() > 255
+    assert np.array_equal(got, want)
+
+
+def test_bench_pipelined_u8_assembly_rccl():
+    """bench.py's pipelined u8 all-gather path (the N > 1 default) through RCCL, one rank."""
+    r = _torchrun(["bench.py", "--assemble", "u8", "--genomes", "3", "--genome-len", "3000000",
+                   "--steps", "3", "--warmup", "1", "--cpu-sample", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["rows_checked"] is True and d["config"]["assembly"] == "u8"
