@@ -285,7 +285,7 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
         uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)CAP);
         const uint4* src = reinterpret_cast<const uint4*>(sorted);
         const uint32_t nchunk = total >> 3;
-        for (uint32_t c = tid; c < nchunk; c += TPB) dst[c] = src[c];
+        for (uint32_t c = tid; c < nchunk; c += TPB) store_nt(&dst[c], src[c]);
     }
 }
 
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     uint32_t* orow = out + (uint64_t)g * (1ull << (2 * K)) + (uint64_t)b * kSubBins;
     if (S == 1) {
         uint4* o4 = reinterpret_cast<uint4*>(orow);
-        for (int i = threadIdx.x; i < kSubBins / 4; i += kCountThreads) o4[i] = tbl4[i];
+        for (int i = threadIdx.x; i < kSubBins / 4; i += kCountThreads) store_nt(&o4[i], tbl4[i]);
     } else if (ta < tb) {
         for (int i = threadIdx.x; i < kSubBins; i += kCountThreads) {
             const uint32_t x = tbl[i];

@@ -77,4 +77,13 @@ __device__ __forceinline__ uint32_t xcd_work_id() {
     return x * q + (x < rem ? x : rem) + b / 8u;
 }
 
+// 16-byte store with the non-temporal policy: streamed output that this XCD never reads back
+// leaves no dirty lines in L2, so the write-back at the next kernel boundary (which stalls the
+// dependent kernel, MI355X_MICROARCH.md "boundary") stays small.
+typedef unsigned int kmh_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_nt(uint4* dst, const uint4& v) {
+    kmh_u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<kmh_u32x4*>(dst));
+}
+
 }  // namespace kmh

@@ -181,8 +181,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     uint32_t* dst = ent + lt * (uint64_t)kSpTile;
     const uint32_t n4 = total / 4;
     for (uint32_t i = tid; i < n4; i += kSpThreads)
-        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(sorted)[i];
-    if (tid < (int)(total & 3u)) dst[4 * n4 + tid] = sorted[4 * n4 + tid];
+        store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
+    if (tid < (int)(total & 3u)) __builtin_nontemporal_store(sorted[4 * n4 + tid], dst + 4 * n4 + tid);
 }
 
 // Entries of every (genome, bucket) of a batch: one workgroup per pair.
@@ -338,8 +338,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     uint32_t* dst = out + (uint64_t)item * kCaps;
     const uint32_t n4 = total / 4;
     for (uint32_t i = tid; i < n4; i += kSpThreads)
-        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(sorted)[i];
-    if (tid < (int)(total & 3u)) dst[4 * n4 + tid] = sorted[4 * n4 + tid];
+        store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
+    if (tid < (int)(total & 3u)) __builtin_nontemporal_store(sorted[4 * n4 + tid], dst + 4 * n4 + tid);
 }
 
 // Count work item: pass p of bucket b of genome g; its entries are segment p of split items
@@ -512,8 +512,8 @@ __global__ __launch_bounds__(NT) void k_sp_count(
             for (int u = 0; u < 4; ++u) {
                 const uint32_t i = i0 + u * NT + tid;
                 if (i < used) {
-                    codes[at + i] = hib | (x[u] >> 32);
-                    counts[at + i] = (uint32_t)x[u];
+                    __builtin_nontemporal_store(hib | (x[u] >> 32), codes + at + i);
+                    __builtin_nontemporal_store((uint32_t)x[u], counts + at + i);
                 }
             }
         }
