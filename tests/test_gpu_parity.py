@@ -461,3 +461,13 @@ def test_bench_pipelined_u8_assembly_rccl():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["rows_checked"] is True and d["config"]["assembly"] == "u8"
+
+
+def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
+    """One full config-5 genome: 250 Mbp synthetic genome 0, k = 21 canonical, every distinct
+    k-mer and count against the C oracle (≈ 250 M sort pairs on the host, ≈ 9 GB)."""
+    seq = oracle_lib.synth(250_000_000, osynth.genome_seed(0))
+    got = _sparse_dev(ctx, dev, [seq], 21, 1)[0]
+    wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
+    assert got[0].size == wc.size
+    assert np.array_equal(got[0], wc) and np.array_equal(got[1], wn)
