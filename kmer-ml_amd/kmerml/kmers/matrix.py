@@ -148,3 +148,48 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
     rows = [gathered[r * B: r * B + (shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0])]
             for r in range(world)]
     return torch.cat(rows, 0) if rows else gathered[:0]
+
+
+def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
+    """Sparse k-mer counts of this rank's block of `genome_files` (BASELINE config 5).
+
+    For 13 <= k <= 21 the genomes are counted on the GPU with the partitioned hash-table path
+    (kmh_count_sparse_dev).  The 4^k columns cannot be assembled densely (4^21 ~ 4.4e12), so
+    nothing is exchanged: with a torch.distributed process group, rank r counts block
+    shard_bounds(G, W, r) and keeps it.  Returns (lo, rows) where rows[i] is
+    (codes uint64 ascending, counts uint32) of genome lo + i.
+    """
+    import torch
+    import torch.distributed as dist
+
+    if not 13 <= k <= 21:
+        raise NotImplementedError("device sparse counting needs 13 <= k <= 21")
+    files = list(genome_files)
+    world, rank = 1, 0
+    if dist.is_available() and dist.is_initialized():
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_bounds(len(files), world, rank)
+    if device is None:
+        device = torch.cuda.current_device()
+    if hi == lo:
+        return lo, []
+    buf, offsets = pack_genomes(files[lo:hi], k)
+    dev = torch.device("cuda", device)
+    d_seq = torch.from_numpy(buf).to(dev) if buf.size else torch.zeros(16, dtype=torch.uint8, device=dev)
+    out_off = _native.sparse_out_offsets(offsets, k)
+    cap = max(int(out_off[-1]), 1)
+    d_codes = torch.empty(cap, dtype=torch.int64, device=dev)
+    d_counts = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_n = torch.empty(hi - lo, dtype=torch.int64, device=dev)
+    ctx = _native.context(device)
+    ctx.count_sparse_dev(d_seq.data_ptr(), offsets, k, canonical, d_codes.data_ptr(), d_counts.data_ptr(),
+                         d_n.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    n = d_n.cpu().numpy()
+    rows = []
+    for g in range(hi - lo):
+        a = int(out_off[g])
+        c = d_codes[a:a + int(n[g])]
+        order = torch.argsort(c)
+        rows.append((c[order].cpu().numpy().view(np.uint64),
+                     d_counts[a:a + int(n[g])][order].cpu().numpy().view(np.uint32)))
+    return lo, rows

@@ -471,3 +471,19 @@ def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
     wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
     assert got[0].size == wc.size
     assert np.array_equal(got[0], wc) and np.array_equal(got[1], wn)
+
+
+def test_sparse_rows_from_fasta(tmp_path, oracle_lib):
+    """kmerml.kmers.matrix.sparse_rows: FASTA files -> per-genome sorted sparse counts."""
+    files, seqs = [], []
+    for i in range(3):
+        p = tmp_path / f"g{i}.fa"
+        seq = osynth.synth_bases(150_000 + 7_000 * i, osynth.genome_seed(10 + i)).tobytes()
+        osynth.write_fasta(p, [(f"SYN_{i}", seq), (f"short_{i}", b"ACGT")])   # short record dropped
+        files.append(str(p))
+        seqs.append(seq)
+    lo, rows = kmatrix.sparse_rows(files, 21, canonical=True)
+    assert lo == 0 and len(rows) == 3
+    for (codes, counts), seq in zip(rows, seqs):
+        wc, wn, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), 21, canonical=True)
+        assert np.array_equal(codes, wc) and np.array_equal(counts, wn)
