@@ -59,6 +59,8 @@ def parse():
                         "all-gather of the u32 rows after each count")
     p.add_argument("--cpu-sample", type=int, default=16_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
+    p.add_argument("--no-kernel-events", action="store_true",
+                   help="experiments: no per-kernel HIP events in the timed region (roofline = null)")
     p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="process-group backend (gloo + --single-device: multi-rank logic check on one GPU)")
@@ -278,7 +280,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ctx.timing(True)
+    ctx.timing(not a.no_kernel_events)
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(i, record=True)
@@ -316,17 +318,16 @@ def main():
         value = total_bases / (elapsed / a.steps)
         # per GPU: its genomes read once + the count rows it must end up holding written once
         algo_step = g_local * L + (G if assemble else g_local) * bins * 4
-        budget = int(os.environ.get("KMH_SUF_BUDGET_MB", "256")) << 20   # kmh_dense.hip batching
-        genomes_per_batch = max(1, min(g_local, budget // max(1, ((L - k + 1 + 16383) // 16384) * 32768)))
         dom = max(kernels.items(), key=lambda kv: kv[1][1]) if kernels else None
         roof = None
         if dom:
             name, (launches, tot) = dom
             per_launch_ms = tot / launches
-            if name == "k_partition":
-                algo = genomes_per_batch * L                 # bases read once (1 B each)
+            per_step = launches / a.steps                    # launches of this kernel per step
+            if name.startswith("k_partition"):
+                algo = g_local * L / per_step                # bases read once (1 B each)
             elif name == "k_bucket_count":
-                algo = genomes_per_batch * bins * 4          # count row slice written once
+                algo = g_local * bins * 4 / per_step         # count rows written once
             elif name == "k_encode_u8":
                 algo = B * bins * 5                          # u32 rows read, u8 rows written
             elif name == "k_decode_u8":

@@ -289,6 +289,262 @@ __global__ __launch_bounds__(TPB) void k_partition(const uint8_t* __restrict__ s
     }
 }
 
+// ---------------------------------------------------------------- k >= 10: persistent partition
+// Same output as k_partition (bucket-ordered, chunk-padded 15-bit suffixes + bucket-major
+// offsets, one 32768-window tile at a time), with fewer and cheaper LDS operations:
+//
+//  * Bank-replicated counters.  Lane l of every wave counts into replica (l & 31) of its
+//    bucket, rep[bucket][replica] at word 32 * bucket + replica, so the 32 lanes of a lane
+//    group always hit 32 different banks (MI355X_MICROARCH.md §LDS: random 4-byte LDS
+//    operations run at ~9 lanes/clk/CU, conflict-free atomics at ~15).
+//  * One returning add per k-mer.  ds_add_rtn gives the k-mer its rank inside (bucket,
+//    replica); a scan turns the counters into segment starts (bucket start + replica
+//    prefix), and the scatter reads its start (conflict-free) and writes the suffix (the
+//    one random LDS operation left).  k_partition needs three random operations per k-mer.
+//  * Persistent with prefetch.  One 1024-thread workgroup per CU walks a contiguous run of
+//    tiles; the next tile's 48 bytes per thread are loaded while this tile is scanned,
+//    scattered and written out, so the LDS phases of one workgroup overlap its HBM reads.
+//
+// Experiment (KMH_PART=1), not the default: measured 134 us per 100 Mbp genome against 79 us
+// for k_partition at 18 genomes per launch (profiles/r01_rep_bench.txt).  The 140 KiB of LDS
+// leave one workgroup per CU, so its seven barriers per tile serialise the phases, and vmcnt
+// counts stores as well as loads: waiting for the prefetched bytes also waits for the
+// previous tile's 72 KiB of output to drain.  Two co-resident k_partition workgroups hide
+// both for free.
+template <int K>
+__device__ __forceinline__ void visit_raw(uint4 a, uint4 b, uint4 n, uint32_t tm_a, uint32_t tm_b,
+                                          uint32_t tm_n, uint32_t (&km)[kTileBpt]) {
+    uint32_t cA, iA, cB, iB, cN, iN;
+    enc16(a, cA, iA);
+    enc16(b, cB, iB);
+    enc16(n, cN, iN);
+    iA |= tm_a;
+    iB |= tm_b;
+    iN |= tm_n;
+    constexpr uint32_t KM = (1u << (2 * K)) - 1u;
+    constexpr uint32_t VM = (1u << K) - 1u;
+    const uint64_t wAB = ((uint64_t)cA << 32) | cB;
+    const uint32_t vAB = (iA << 16) | iB;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t code = (uint32_t)(wAB >> (64 - 2 * (j + K))) & KM;
+        km[j] = (((vAB >> (32 - (j + K))) & VM) == 0u) ? code : 0xFFFFFFFFu;
+    }
+    const uint64_t wBN = ((uint64_t)cB << 32) | cN;
+    const uint32_t vBN = (iB << 16) | iN;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t code = (uint32_t)(wBN >> (64 - 2 * (j + K))) & KM;
+        km[16 + j] = (((vBN >> (32 - (j + K))) & VM) == 0u) ? code : 0xFFFFFFFFu;
+    }
+}
+
+constexpr int kRepThreads = 1024;
+constexpr int kRepTile = kRepThreads * kTileBpt;   // 32768 windows, as k_partition<12, 512, ., 2>
+constexpr int kRep = 32;                            // counter replicas = banks per lane group
+
+template <int K>
+__global__ __launch_bounds__(kRepThreads) void k_partition_rep(const uint8_t* __restrict__ seq,
+                                                               GenomeMap m, uint16_t* __restrict__ suf,
+                                                               uint16_t* __restrict__ toff, uint32_t ldt,
+                                                               uint32_t ntiles) {
+    constexpr int NBK = num_buckets<K>();
+    constexpr int CAP = tile_cap<K>(kRepTile);
+    constexpr int NW = kRepThreads / 64;
+    static_assert(NBK >= 2 * NW && NBK <= kRepThreads, "scan layout needs 32 <= buckets <= 1024");
+    __shared__ __attribute__((aligned(16))) uint16_t sorted[CAP + 64];    // + dummy slots
+    __shared__ __attribute__((aligned(16))) uint32_t rep[(NBK + 1) * kRep];  // + dummy row
+    __shared__ uint32_t bst[NBK];
+    __shared__ uint32_t wsum[NW];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31;
+    const uint32_t w = xcd_work_id();
+    const uint64_t tlo = (uint64_t)ntiles * w / gridDim.x, thi = (uint64_t)ntiles * (w + 1) / gridDim.x;
+
+    uint4* rep4 = reinterpret_cast<uint4*>(rep);
+    for (int i = tid; i < (NBK + 1) * kRep / 4; i += kRepThreads) rep4[i] = make_uint4(0u, 0u, 0u, 0u);
+
+    // Where the current tile lies: genome g spans batch tiles [tf, tn) and bytes [gs, ge).
+    // Advanced tile by tile; the genome table is read only when the run crosses a genome (a
+    // per-tile lookup would be a vector load, and waiting for it would also wait for the
+    // previous tile's output stores: vmcnt counts both).
+    // (readfirstlane: the values are uniform; keep them in scalar registers)
+    auto uni = [](uint64_t x) -> uint64_t {
+        // (the builtin returns int: zero-extend through uint32_t, never sign-extend)
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+    };
+    int g = __builtin_amdgcn_readfirstlane(find_genome(m, m.tile_lo + tlo));
+    uint64_t tf = uni(m.tbase[g] - m.tile_lo), tn = uni(m.tbase[g + 1] - m.tile_lo);
+    uint64_t gs = uni(m.goff[g]), ge = uni(m.goff[g + 1]);
+    auto advance = [&](uint64_t t) {
+        while (t >= tn) {
+            ++g;
+            tf = tn;
+            tn = uni(m.tbase[g + 1] - m.tile_lo);
+            gs = uni(m.goff[g]);
+            ge = uni(m.goff[g + 1]);
+        }
+    };
+
+    uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra, rn = ra;   // this tile's 48 bytes
+    uint4 pa = ra, pb = ra, pn = ra;                            // the next tile's (prefetch)
+    bool have = false;   // pa/pb/pn hold the current tile
+    for (uint64_t lt = tlo; lt < thi; ++lt) {
+        const uint64_t tstart = gs + (lt - tf) * (uint64_t)kRepTile, gend = ge;
+        const uint64_t base = tstart + (uint64_t)tid * kTileBpt;
+        if (have) {
+            ra = pa;
+            rb = pb;
+            rn = pn;
+        } else if (tstart + (uint64_t)kRepTile + 16 <= m.data_end) {
+            ra = *reinterpret_cast<const uint4*>(seq + base);
+            rb = *reinterpret_cast<const uint4*>(seq + base + 16);
+            rn = *reinterpret_cast<const uint4*>(seq + base + 32);
+        } else {
+            ra = load16(seq, base, gend);
+            rb = load16(seq, base + 16, gend);
+            rn = load16(seq, base + 32, gend);
+        }
+        const uint32_t tma = tail_mask(base, gend), tmb = tail_mask(base + 16, gend),
+                       tmn = tail_mask(base + 32, gend);
+        lds_barrier();   // rep zeroed, previous tile's copy-out done with `sorted`
+
+        // 1. rank every k-mer inside (bucket, replica).  Branch-free: a window with a
+        //    non-ACGT byte (code ~0) counts in the dummy row NBK and is scattered into the
+        //    dummy slots past CAP.  The codes are recomputed from the 48 bytes in the scatter
+        //    instead of being kept (register pressure).
+        uint32_t rk[kTileBpt / 2];   // ranks (< 1024), two per register
+        {
+            uint32_t km[kTileBpt];
+            visit_raw<K>(ra, rb, rn, tma, tmb, tmn, km);
+#pragma unroll
+            for (int j = 0; j < kTileBpt; j += 2) {
+                const uint32_t b0 = min(km[j] >> kSubBits, (uint32_t)NBK);
+                const uint32_t b1 = min(km[j + 1] >> kSubBits, (uint32_t)NBK);
+                const uint32_t x0 = atomicAdd(&rep[b0 * kRep + r], 1u);
+                const uint32_t x1 = atomicAdd(&rep[b1 * kRep + r], 1u);
+                rk[j >> 1] = x0 | (x1 << 16);
+            }
+        }
+        // opaque to the compiler: the scatter recomputes the codes instead of keeping 32
+        // registers alive across the scan
+        __asm__ __volatile__("" : "+v"(ra.x), "+v"(ra.y), "+v"(ra.z), "+v"(ra.w), "+v"(rb.x), "+v"(rb.y),
+                             "+v"(rb.z), "+v"(rb.w), "+v"(rn.x), "+v"(rn.y), "+v"(rn.z), "+v"(rn.w));
+        // prefetch the next tile behind this tile's LDS phases
+        have = false;
+        if (lt + 1 < thi) {
+            advance(lt + 1);
+            const uint64_t ns = gs + (lt + 1 - tf) * (uint64_t)kRepTile;
+            if (ns + (uint64_t)kRepTile + 16 <= m.data_end) {
+                const uint64_t nb = ns + (uint64_t)tid * kTileBpt;
+                pa = *reinterpret_cast<const uint4*>(seq + nb);
+                pb = *reinterpret_cast<const uint4*>(seq + nb + 16);
+                pn = *reinterpret_cast<const uint4*>(seq + nb + 32);
+                have = true;
+            }
+        }
+        lds_barrier();
+
+        // 2a. per bucket: exclusive replica prefixes in place, bucket sizes to bst.  Thread
+        //     t owns replicas 16 (t & 1) .. + 15 of bucket t >> 1 (four 16-byte reads).
+        constexpr int HALF = kRep / 2;
+        uint4* mine = rep4 + (size_t)tid * (HALF / 4);
+        if (tid < 2 * NBK) {
+            uint4 q[HALF / 4];
+            uint32_t run = 0u;
+#pragma unroll
+            for (int c = 0; c < HALF / 4; ++c) {
+                q[c] = mine[c];
+                const uint32_t x0 = q[c].x, x1 = q[c].y, x2 = q[c].z, x3 = q[c].w;
+                q[c] = make_uint4(run, run + x0, run + x0 + x1, run + x0 + x1 + x2);
+                run += x0 + x1 + x2 + x3;
+            }
+            const uint32_t other = __shfl_xor(run, 1);          // the partner half's total
+            const uint32_t add = (tid & 1) ? other : 0u;
+#pragma unroll
+            for (int c = 0; c < HALF / 4; ++c)
+                mine[c] = make_uint4(q[c].x + add, q[c].y + add, q[c].z + add, q[c].w + add);
+            if (!(tid & 1)) bst[tid >> 1] = run + other;
+        }
+        lds_barrier();
+
+        // 2b. bucket starts: exclusive scan of the chunk-padded bucket sizes
+        const uint32_t nbk = tid < NBK ? bst[tid] : 0u;
+        const uint32_t v = (nbk + 7u) & ~7u;
+        uint32_t incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        lds_barrier();
+        uint32_t pre = 0u, total = 0u;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            pre += (q < wave) ? wsum[q] : 0u;
+            total += wsum[q];
+        }
+        const uint32_t start = pre + incl - v;
+        if (tid < NBK) {
+            bst[tid] = start;
+            toff[(uint64_t)tid * ldt + lt] = (uint16_t)(start >> 3);
+        }
+        if (tid == 0) toff[(uint64_t)NBK * ldt + lt] = (uint16_t)(total >> 3);
+        lds_barrier();
+
+        // 2c. segment start of every (bucket, replica)
+        if (tid < 2 * NBK) {
+            const uint32_t add = bst[tid >> 1];
+#pragma unroll
+            for (int c = 0; c < HALF / 4; ++c) {
+                const uint4 x = mine[c];
+                mine[c] = make_uint4(x.x + add, x.y + add, x.z + add, x.w + add);
+            }
+        }
+        lds_barrier();
+
+        // 3. scatter the suffixes; pad every bucket's segment to its chunk boundary
+        //    (groups of 8: eight start reads in flight, then eight stores -- the compiler
+        //    would otherwise wait for every read, stores included, one k-mer at a time)
+        uint32_t km[kTileBpt];
+        visit_raw<K>(ra, rb, rn, tma, tmb, tmn, km);
+#pragma unroll
+        for (int j0 = 0; j0 < kTileBpt; j0 += 8) {
+            uint32_t pos[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t b = min(km[j0 + j] >> kSubBits, (uint32_t)NBK);
+                pos[j] = rep[b * kRep + r];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t c = km[j0 + j];
+                const uint32_t rank = (rk[(j0 + j) >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                sorted[(c >> kSubBits) < (uint32_t)NBK ? pos[j] + rank : (uint32_t)CAP + (uint32_t)lane] =
+                    (uint16_t)(c & (kSubBins - 1));
+            }
+        }
+        if (tid < NBK) {
+#pragma unroll
+            for (uint32_t q = 0; q < 7u; ++q) {
+                const uint32_t at = start + nbk + q;
+                if (nbk + q < v) sorted[at] = (uint16_t)(kPadBase + ((8u * (uint32_t)tid + at) & (kPadBins - 1)));
+            }
+        }
+        lds_barrier();
+
+        // 4. write the tile out; zero the counters for the next tile
+        uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)CAP);
+        const uint4* src = reinterpret_cast<const uint4*>(sorted);
+        const uint32_t nchunk = total >> 3;
+#pragma unroll 1
+        for (uint32_t c = tid; c < nchunk; c += kRepThreads) store_nt(&dst[c], src[c]);
+        for (int i = tid; i < (NBK + 1) * kRep / 4; i += kRepThreads) rep4[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
 // Fixed-capacity variant (k = 12 default): every bucket owns a row of FC suffix slots in
 // LDS, so one returning LDS add per k-mer yields both the bucket count and the k-mer's
 // rank, and the suffix is stored at row[bucket][rank] -- two LDS operations per k-mer
@@ -809,22 +1065,27 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
 }
 
 template <int K, int TPB, int PABL, int CABL, int GSX = 0, int UX = 0, int PIPE = 0, int SUBT = 1,
-          int FCAP = 0>
+          int FCAP = 0, int REP = 0>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int TILE = TPB * kTileBpt * SUBT;
+    constexpr int TILE = REP ? kRepTile : TPB * kTileBpt * SUBT;
     constexpr int CAP = tile_cap<K>(TILE);
     constexpr int GS0 = TILE / NBK / 8;   // lanes per segment: one 16-B chunk each
     constexpr int GS1 = GS0 < 1 ? 1 : (GS0 > 64 ? 64 : GS0);
     constexpr int GS = GSX ? GSX : GS1;
     constexpr int U = UX ? UX : 6;        // chunk loads in flight per lane (queue = 64 U)
     const size_t row = (size_t)1 << (2 * K);
-    // Genomes per batch: keep the suffix buffer of one batch within the budget (it is
-    // written and re-read, so a budget inside the 256 MiB Infinity Cache can keep it
-    // on-die).  KMH_SUF_BUDGET_MB overrides.
-    const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 256) << 20;
+    // Genomes per batch: keep the suffix buffer of one batch within the budget.  Measured
+    // (profiles/r01_batch.txt): batches larger than the 256 MiB Infinity Cache are faster --
+    // the exchange re-read from HBM costs less than the launch tails and kernel boundaries
+    // of one-genome launches (config 3: 11.0 ms per step at 256 MiB, 9.2 ms at 4 GiB = 18
+    // genomes per launch).  KMH_SUF_BUDGET_MB overrides.
+    const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 4096) << 20;
     const size_t tile_bytes = (size_t)CAP * sizeof(uint16_t);
+    // Two suffix/offset buffers when KMH_OVERLAP=1 (experiment): the partition of batch i+1
+    // (side stream) overlaps the count of batch i (caller's stream).
+    const bool overlap = env_long("KMH_OVERLAP", 0) != 0;
     uint64_t max_batch_tiles = 0;
     {
         int g = 0;
@@ -839,15 +1100,13 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
             g = h;
         }
     }
-    // Two suffix/offset buffers: the partition of batch i+1 (side stream) overlaps the
-    // count of batch i (caller's stream).  KMH_OVERLAP=0 runs both on the caller's stream.
-    const bool overlap = env_long("KMH_OVERLAP", 0) != 0;
     const size_t slot_tiles = std::max<uint64_t>(max_batch_tiles, 1);
-    int rc = ensure(ctx, ctx->suf, 2 * slot_tiles * tile_bytes);
+    const size_t nslots = overlap ? 2 : 1;
+    int rc = ensure(ctx, ctx->suf, nslots * slot_tiles * tile_bytes);
     if (rc) return rc;
     const uint32_t ldt = (uint32_t)((slot_tiles + 63) / 64 * 64);
     const size_t toff_slot = (size_t)ldt * (NBK + 1);
-    rc = ensure(ctx, ctx->toff, 2 * toff_slot * sizeof(uint16_t));
+    rc = ensure(ctx, ctx->toff, nslots * toff_slot * sizeof(uint16_t));
     if (rc) return rc;
     // u16-packed count tables (KMH_COUNT16=1; KMH_COUNT16_NT=512|1024): half the LDS, same
     // speed here; kept for co-residency experiments.  Default: the u32 kernel.
@@ -894,13 +1153,20 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
         if (S > 1) KMH_HIP(ctx, hipMemsetAsync(d_out + (size_t)g * row, 0, (size_t)nG * row * sizeof(uint32_t), s));
         if (overlap && batch >= 2) KMH_HIP(ctx, hipStreamWaitEvent(sp, ctx->pipe_ev[3 + slot], 0));
         if (tiles) {
-            time_begin(ctx, sp, "k_partition");
-            if constexpr (FCAP > 0)
+            if constexpr (REP) {
+                const unsigned pgrid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)std::max(1, ctx->num_cu));
+                time_begin(ctx, sp, "k_partition_rep");
+                hipLaunchKernelGGL((k_partition_rep<K>), dim3(pgrid), dim3(kRepThreads), 0, sp,
+                                   d_seq, m, suf, toff, ldt, (uint32_t)tiles);
+            } else if constexpr (FCAP > 0) {
+                time_begin(ctx, sp, "k_partition");
                 hipLaunchKernelGGL((k_partition_fc<K, TPB, FCAP>), dim3((unsigned)tiles), dim3(TPB), 0, sp,
                                    d_seq, m, suf, toff, ldt);
-            else
+            } else {
+                time_begin(ctx, sp, "k_partition");
                 hipLaunchKernelGGL((k_partition<K, TPB, PABL, SUBT>), dim3((unsigned)tiles), dim3(TPB), 0, sp,
                                    d_seq, m, suf, toff, ldt);
+            }
             time_end(ctx, sp);
             KMH_HIP(ctx, hipGetLastError());
         }
@@ -951,6 +1217,14 @@ int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
         // k = 12: two 16384-window sub-tiles per partition tile (64-entry segments) unless
         // KMH_SUBT=1.
         const int subt = (K == 12 && tpb == 512 && env_long("KMH_SUBT", 2) == 2) ? 2 : 1;
+        // KMH_PART=1 (experiment): the persistent replica-counter partition k_partition_rep.
+        // Parity-tested, measured slower (134 vs 79 us per 100 Mbp genome).
+        if (env_long("KMH_PART", 0) != 0) {
+            int rc = make_layout(ctx, offsets, G, K, (uint64_t)kRepTile, L);
+            if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+            if (rc) return rc;
+            return run_partitioned<K, 1024, 0, 0, 0, 0, 0, 1, 0, 1>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+        }
         int rc = make_layout(ctx, offsets, G, K, (uint64_t)tpb * kTileBpt * subt, L);
         if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
         if (rc) return rc;

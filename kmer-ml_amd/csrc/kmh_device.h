@@ -77,6 +77,15 @@ __device__ __forceinline__ uint32_t xcd_work_id() {
     return x * q + (x < rem ? x : rem) + b / 8u;
 }
 
+// Workgroup barrier for LDS only.  __syncthreads() is also a release fence for global
+// memory, i.e. it waits for every store the wave has in flight (s_waitcnt vmcnt(0)); the
+// persistent kernels never read back what they store, so their barriers need only the LDS
+// operations to be complete: one item's stores drain, and the next item's prefetched loads
+// stay in flight, across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+    __asm__ __volatile__("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // 16-byte store with the non-temporal policy: streamed output that this XCD never reads back
 // leaves no dirty lines in L2, so the write-back at the next kernel boundary (which stalls the
 // dependent kernel, MI355X_MICROARCH.md "boundary") stays small.

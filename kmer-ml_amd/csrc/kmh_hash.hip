@@ -49,14 +49,6 @@ constexpr int kMaxPasses = 256;
 constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
 
-// Workgroup barrier for LDS only.  __syncthreads() is also a release fence for global
-// memory, i.e. it waits for every store the wave has in flight (s_waitcnt vmcnt(0)); the
-// persistent count kernel never reads back what it stores, so its barriers need only the
-// LDS operations to be complete and let one item's output stores drain under the next item.
-__device__ __forceinline__ void lds_barrier() {
-    __asm__ __volatile__("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
 // 2-bit-group reversal of the low 2K bits of ~x: the reverse complement of a K-mer code.
 template <int K>
 __device__ __forceinline__ uint64_t revcomp(uint64_t x) {

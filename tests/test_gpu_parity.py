@@ -89,6 +89,57 @@ def test_dense_low_complexity(ctx, dev, oracle_lib, k):
         assert np.array_equal(rows[g], oracle_lib.count_dense(seq, k)), (k, g)
 
 
+@pytest.mark.parametrize("part", ["0", "1"])
+@pytest.mark.parametrize("k", [10, 11, 12])
+def test_dense_partition_many_genomes(ctx, dev, oracle_lib, monkeypatch, part, k):
+    """Both partition kernels (KMH_PART=0: one tile per workgroup, the default; 1: the
+    persistent k_partition_rep experiment) on 120 ragged genomes -- empty ones, one spanning ~60 tiles -- so that
+    a persistent workgroup's run of tiles crosses genome boundaries; then again with one
+    genome per launch (KMH_SUF_BUDGET_MB=1)."""
+    monkeypatch.setenv("KMH_PART", part)
+    rng = np.random.default_rng(7000 + k)
+    lens = rng.integers(0, 90_000, 120)
+    lens[::29] = 0
+    lens[7] = 2_000_003
+    lens[8] = 32_768 + k - 1          # exactly one full tile of windows
+    genomes = [_rand_seq(rng, int(n)) for n in lens]
+    want = [oracle_lib.count_dense(seq, k) for seq in genomes]
+    rows, _, _ = _dense_rows(ctx, dev, genomes, k)
+    for g in range(len(genomes)):
+        assert np.array_equal(rows[g], want[g]), (k, g)
+    monkeypatch.setenv("KMH_SUF_BUDGET_MB", "1")
+    rows, _, _ = _dense_rows(ctx, dev, genomes[:12], k)
+    for g in range(12):
+        assert np.array_equal(rows[g], want[g]), (k, g, "batched")
+
+
+@pytest.mark.parametrize("part", ["0", "1"])
+@pytest.mark.parametrize("k", [11, 12])
+def test_dense_partition_long_runs_large_offsets(ctx, dev, oracle_lib, monkeypatch, part, k):
+    """Every persistent partition workgroup walks several tiles that cross genome
+    boundaries, and the genomes lie past byte 2^31 of the buffer (a 2.2 GB genome of 'N'
+    -- tiles but no valid window -- comes first): 40 ragged genomes, ~40 Mbp."""
+    monkeypatch.setenv("KMH_PART", part)
+    rng = np.random.default_rng(900 + k)
+    lens = rng.integers(0, 2_000_000, 40)
+    lens[3] = 0
+    lens[10] = 5_000_017
+    genomes = [_rand_seq(rng, int(n), b"ACGTACGTACGTacgtN") for n in lens]
+    lead = (2**31 + 2**22 + 15) // 16 * 16
+    buf, offs = _layout(genomes)
+    d_seq = torch.empty(lead + buf.size, dtype=torch.uint8, device=dev)
+    d_seq[:lead].fill_(ord("N"))
+    d_seq[lead:].copy_(torch.from_numpy(buf))
+    offs = np.concatenate([[0], offs + lead]).astype(np.uint64)
+    out = torch.full((len(genomes) + 1, 1 << (2 * k)), -7, dtype=torch.int32, device=dev)
+    ctx.count_dense_dev(d_seq.data_ptr(), offs, k, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rows = out.cpu().numpy().view(np.uint32)
+    assert not rows[0].any()
+    for g, seq in enumerate(genomes):
+        assert np.array_equal(rows[g + 1], oracle_lib.count_dense(seq, k)), (k, g)
+
+
 def test_dense_rejects_misaligned_offsets(ctx, dev):
     d_seq = torch.zeros(64, dtype=torch.uint8, device=dev)
     out = torch.zeros((2, 256), dtype=torch.int32, device=dev)
