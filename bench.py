@@ -7,8 +7,8 @@ Workload (BASELINE.json configs): N = 1 is config 3 -- 64 synthetic 100 Mbp geno
 k = 12, dense 4^12 histogram per genome on one MI355X.  N > 1 is config 4 -- the same 64
 genomes sharded in contiguous blocks of 64/N per GPU (one process per GPU, launched by
 torch.distributed.run) with an RCCL all-gather that assembles the [64, 4^12] u32 matrix on
-every rank inside each step (sent as saturating u8 rows + an exact escape list, step i's
-all-gather overlapped with step i+1's count; --assemble u32 sends plain rows instead).  A step is one pass of the count path over every genome
+every rank inside each step (sent as saturating u4 rows + an exact escape list, step i's
+all-gather overlapped with step i+1's count; --assemble u8 / u32 send u8 / plain rows).  A step is one pass of the count path over every genome
 (plus the all-gather for N > 1); the genomes are generated on the device before timing,
 so inputs are resident in HBM when the timed region starts.
 
@@ -53,10 +53,11 @@ def parse():
                    help="total genomes over all ranks (default 64 dense / 16 per GPU sparse)")
     p.add_argument("--genome-len", type=int, default=None, help="default 100 Mbp dense / 250 Mbp sparse")
     p.add_argument("--forward", action="store_true", help="sparse: forward-strand codes instead of canonical")
-    p.add_argument("--assemble", choices=["auto", "u8", "u32", "none"], default="auto",
-                   help="N > 1 matrix assembly: u8 = saturating u8 rows + exact escape list, "
-                        "all-gather overlapped with the next step's count (default); u32 = plain "
-                        "all-gather of the u32 rows after each count")
+    p.add_argument("--assemble", choices=["auto", "u4", "u8", "u32", "none"], default="auto",
+                   help="N > 1 matrix assembly: u4 (default) / u8 = saturating 4- / 8-bit rows + "
+                        "exact escape list on the wire, all-gather overlapped with the next step's "
+                        "count, widened to the u32 matrix on every rank; u32 = plain all-gather of "
+                        "the u32 rows after each count")
     p.add_argument("--cpu-sample", type=int, default=16_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
     p.add_argument("--no-kernel-events", action="store_true",
@@ -151,7 +152,7 @@ def main():
     dev = torch.device("cuda", dev_index)
     # A process group for N > 1, or when torch.distributed.run launched a single rank with an
     # explicit assembly mode (exercises the RCCL code path on one GPU).
-    use_dist = world > 1 or (a.assemble in ("u8", "u32") and "RANK" in os.environ)
+    use_dist = world > 1 or (a.assemble in ("u4", "u8", "u32") and "RANK" in os.environ)
     if use_dist:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
@@ -163,7 +164,7 @@ def main():
     lo, hi = (G * rank) // world, (G * (rank + 1)) // world
     g_local = hi - lo
     B = -(-G // world)
-    mode = ("u8" if world > 1 else "none") if a.assemble == "auto" else a.assemble
+    mode = ("u4" if world > 1 else "none") if a.assemble == "auto" else a.assemble
     assemble = mode != "none"
     bins = 1 << (2 * k)
 
@@ -184,7 +185,7 @@ def main():
         ctx.synth_dev(d_seq.data_ptr(), L, stride, g_local, SEED_BASE + lo, s)
     offsets = np.arange(g_local + 1, dtype=np.uint64) * np.uint64(stride)
     gloo = a.backend == "gloo"
-    full = torch.empty((world * B, bins), dtype=torch.int32, device=dev) if assemble else None
+    full = torch.empty((world * B, bins), dtype=torch.int32, device=dev) if mode == "u32" else None
     t_count = []
 
     def count_into(buf, record):
@@ -198,7 +199,7 @@ def main():
             e1.record(stream)
             t_count.append((e0, e1))
 
-    if mode != "u8":
+    if mode not in ("u4", "u8"):
         local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
         locals_ = [local]
 
@@ -215,15 +216,22 @@ def main():
         def drain():
             pass
     else:
-        # One all-gather per step of a packed slot per rank:
-        #   [B * bins u8 rows][esc_n u32, 12 B pad][cap escape triples (row, col, value) u32]
-        # Step i's all-gather (RCCL stream) overlaps step i+1's count (compute stream); the
-        # widening to u32 rows runs on a side stream once the gather lands.  Everything is
-        # double-buffered and ordered by events, so each step's matrix is complete and exact.
-        from kmerml.kmers.matrix import slot_layout
-        cap, P = slot_layout(B, bins)
-        u8_bytes = B * bins
-        locals_ = [torch.zeros((B, bins), dtype=torch.int32, device=dev) for _ in range(2)]
+        # One all-gather per step of a packed slot per rank, u4 (default) or u8:
+        #   [B * bins counts, saturated][esc_n u32, 12 B pad][cap escapes]
+        # Step i counts straight into this rank's rows of the full matrix fulls[i % 2], encodes
+        # them, and all-gathers the slots (RCCL stream); step i's other ranks' rows are widened
+        # into fulls[i % 2] on a side stream while step i+1 counts.  Double-buffered and ordered
+        # by events (step i+2 waits for step i's widening), so every step's matrix is complete
+        # and exact.
+        from kmerml.kmers.matrix import slot_layout, slot_layout_u4
+        if mode == "u4":
+            cap, P = slot_layout_u4(B, bins)
+            payload = B * bins // 2
+        else:
+            cap, P = slot_layout(B, bins)
+            payload = B * bins
+        fulls = [torch.zeros((world * B, bins), dtype=torch.int32, device=dev) for _ in range(2)]
+        locals_ = [f[rank * B:(rank + 1) * B] for f in fulls]
         send = [torch.zeros(P, dtype=torch.uint8, device=dev) for _ in range(2)]
         recv = [torch.empty(world * P, dtype=torch.uint8, device=dev) for _ in range(2)]
         esc_max = torch.zeros(world, dtype=torch.int32, device=dev)
@@ -232,7 +240,7 @@ def main():
         pending = []
 
         def finish(j, work):
-            """Widen step j's gathered slots into `full` on the side stream."""
+            """Widen step j's gathered slots of the other ranks into fulls[j % 2] (side stream)."""
             if work is None:
                 side.wait_stream(stream)
             with torch.cuda.stream(side):
@@ -240,11 +248,18 @@ def main():
                     work.wait()
                 r = recv[j % 2]
                 base = r.data_ptr()
+                dst = fulls[j % 2]
                 for q in range(world):
+                    if q == rank:
+                        continue
                     slot = base + q * P
-                    ctx.rows_decode_u8(slot, B, bins, slot + u8_bytes + 16, cap, slot + u8_bytes,
-                                       1, B, full[q * B:].data_ptr(), side.cuda_stream)
-                n = r.view(world, P)[:, u8_bytes:u8_bytes + 4].view(torch.int32)[:, 0]
+                    if mode == "u4":
+                        ctx.rows_decode_u4(slot, B, bins, slot + payload + 16, cap, slot + payload,
+                                           dst[q * B:].data_ptr(), side.cuda_stream)
+                    else:
+                        ctx.rows_decode_u8(slot, B, bins, slot + payload + 16, cap, slot + payload,
+                                           1, B, dst[q * B:].data_ptr(), side.cuda_stream)
+                n = r.view(world, P)[:, payload:payload + 4].view(torch.int32)[:, 0]
                 torch.maximum(esc_max, n, out=esc_max)
                 ev = torch.cuda.Event()
                 ev.record(side)
@@ -252,12 +267,16 @@ def main():
 
         def step(i, record=False):
             b = i % 2
-            count_into(locals_[b], record)
             if dec_done[b] is not None:      # step i-2's gather (send[b] -> recv[b]) and widening
                 stream.wait_event(dec_done[b])
+            count_into(locals_[b], record)
             sb = send[b]
-            ctx.rows_encode_u8(locals_[b].data_ptr(), B, bins, sb.data_ptr(), sb[u8_bytes + 16:].data_ptr(),
-                               cap, sb[u8_bytes:].data_ptr(), s)
+            if mode == "u4":
+                ctx.rows_encode_u4(locals_[b].data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
+                                   cap, sb[payload:].data_ptr(), s)
+            else:
+                ctx.rows_encode_u8(locals_[b].data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
+                                   cap, sb[payload:].data_ptr(), s)
             if not gloo:
                 work = dist.all_gather_into_tensor(recv[b], sb, async_op=True)
             else:  # gloo validation path: host staging, synchronous
@@ -301,11 +320,13 @@ def main():
 
     # sanity: every row sums to the number of valid windows (all-ACGT genomes)
     last = locals_[(a.steps - 1) % len(locals_)]
+    if mode in ("u4", "u8"):
+        full = fulls[(a.steps - 1) % 2]
     rows = full[:G] if (assemble and G % world == 0) else last[:g_local]
     ok = bool(torch.all(rows.sum(1, dtype=torch.int64) == max(L - k + 1, 0)).item())
-    if assemble:   # this rank's block of the assembled matrix is bit-identical to its own count
+    if mode == "u32":   # this rank's block of the assembled matrix is bit-identical to its own count
         ok = ok and bool(torch.equal(full[rank * B:rank * B + g_local], last[:g_local]))
-    if mode == "u8" and int(esc_max.max().item()) > cap:
+    if mode in ("u4", "u8") and int(esc_max.max().item()) > cap:
         raise SystemExit(f"escape list overflow ({int(esc_max.max().item())} > {cap}): use --assemble u32")
     if world > 1:
         okt = torch.tensor([int(ok)], dtype=torch.int32, device=dev if not gloo else "cpu")
@@ -332,6 +353,10 @@ def main():
                 algo = B * bins * 5                          # u32 rows read, u8 rows written
             elif name == "k_decode_u8":
                 algo = B * bins * 5                          # u8 rows read, u32 rows written
+            elif name == "k_encode_u4":
+                algo = B * bins * 4.5                        # u32 rows read, u4 rows written
+            elif name == "k_decode_u4":
+                algo = B * bins * 4.5                        # u4 rows read, u32 rows written
             else:
                 algo = g_local * (L + bins * 4) / max(1, launches / a.steps)
             achieved = algo / (per_launch_ms * 1e-3) / 1e9

@@ -170,6 +170,20 @@ int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uin
                            const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
                            int ranks, uint64_t rows_per_rank, uint32_t* d_rows, void* stream);
 
+/* u4 wire format (the multi-GPU default, 8x fewer bytes than u32 rows): two counts per byte,
+ * element 2i in the low nibble of byte i; values >= 15 are stored as 15 and appended to
+ * d_esc as an exact (index, value) u32 pair, index = row * cols + col within the block.
+ * Needs cols % 32 == 0 and rows * cols < 2^32 - 1.  *d_esc_n (device) receives the number of
+ * escapes; if it exceeds cap the encoding is incomplete (send u32 rows instead). */
+int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
+                           uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
+                           void* stream);
+/* Widen one block of u4 rows (rows x cols) to u32 at d_rows and apply its escapes (pairs with an
+ * index outside the block are ignored: a slot that came off the wire never writes elsewhere). */
+int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
+                           const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
+                           uint32_t* d_rows, void* stream);
+
 /* ---- file output (host) -------------------------------------------------------- */
 /* Write n bytes to `path`: plain when gzip_level < 0, else gzip at that level (0..9; the
  * reference uses 9 via gzip.open, generate.py:82-85) as independently deflated 8 MiB members

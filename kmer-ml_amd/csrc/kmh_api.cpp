@@ -262,6 +262,24 @@ int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uin
                                d_rows, pick_stream(ctx, stream));
 }
 
+int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
+                           uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
+                           void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::rows_encode_u4(ctx, d_rows, rows, cols, d_u4, d_esc, cap, d_esc_n, pick_stream(ctx, stream));
+}
+
+int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
+                           const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
+                           uint32_t* d_rows, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::rows_decode_u4(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, pick_stream(ctx, stream));
+}
+
 // Host sequence -> device (padded with one non-base byte so loads past the end are safe).
 static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t** d_seq) {
     int rc = kmh::ensure(ctx, ctx->seq, (size_t)n + 64);

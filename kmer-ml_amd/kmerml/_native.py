@@ -53,6 +53,8 @@ SIGNATURES = [
     ("kmh_count_sparse_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp]),
     ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
+    ("kmh_rows_encode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
+    ("kmh_rows_decode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _vp, _vp]),
     ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
                                           _u64, _vp, _vp]),
 ]
@@ -200,6 +202,18 @@ class Context:
         _check(lib().kmh_rows_decode_u8_dev(self._h, ctypes.c_void_p(d_u8), int(rows), int(cols),
                                             ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
                                             int(ranks), int(rows_per_rank), ctypes.c_void_p(d_rows),
+                                            ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def rows_encode_u4(self, d_rows, rows, cols, d_u4, d_esc, cap, d_esc_n, stream=None):
+        _check(lib().kmh_rows_encode_u4_dev(self._h, ctypes.c_void_p(d_rows), int(rows), int(cols),
+                                            ctypes.c_void_p(d_u4), ctypes.c_void_p(d_esc), int(cap),
+                                            ctypes.c_void_p(d_esc_n),
+                                            ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def rows_decode_u4(self, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, stream=None):
+        _check(lib().kmh_rows_decode_u4_dev(self._h, ctypes.c_void_p(d_u4), int(rows), int(cols),
+                                            ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
+                                            ctypes.c_void_p(d_rows),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- kernel timing --

@@ -6,7 +6,7 @@ file order of find_files, features.py:46).  Here every rank (one process per GPU
 ``torch.distributed`` with the "nccl" backend = RCCL over xGMI) counts a contiguous
 block of the genome list straight into its rows of a dense ``[G, 4^k]`` uint32 matrix in
 HBM, and one ``all_gather_into_tensor`` assembles the full matrix on every rank (rows
-travel as saturating u8 plus an exact escape list, 4x fewer bytes over xGMI).  Row g
+travel as saturating u4 plus an exact escape list, 8x fewer bytes over xGMI).  Row g
 is genome g of the input order; column c is the k-mer with 2-bit code c (A0 C1 G2 T3,
 first base most significant, i.e. lexicographic order).  Counting follows
 generate.py:39-58 exactly (records shorter than k skipped, non-ACGT windows dropped).
@@ -77,6 +77,52 @@ def slot_layout(rows, cols):
     return cap, (rows * cols + 16 + cap * 12 + 255) // 256 * 256
 
 
+def slot_layout_u4(rows, cols):
+    """Packed per-rank all-gather slot of the u4 assembly (the multi-GPU default).
+
+    [rows * cols / 2 bytes: two counts per byte, values >= 15 stored as 15][escape count u32 +
+    12 B pad][cap (index, value) u32 pairs, index = row * cols + col]; returns (cap,
+    slot_bytes).  cap allows one escape (count >= 15) per 256 cells: uniform 100 Mbp genomes at
+    k = 12 (Poisson, mean ~6) need ~1.4 per 1000.
+    """
+    cap = max(4096, rows * cols // 256)
+    return cap, (rows * cols // 2 + 16 + cap * 8 + 255) // 256 * 256
+
+
+def gather_rows_u4(padded, group=None):
+    """All-gather [B, cols] u32 rows (device int32 tensor) from every rank as u4 + escapes.
+
+    Exact for any counts: values >= 15 travel in the escape list.  If any rank has more
+    escapes than the slot holds, every rank falls back to the u8 path (and from there, if
+    needed, to the plain u32 all-gather).
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    B, cols = padded.shape
+    dev = padded.device
+    ctx = _native.context(dev.index)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    cap, P = slot_layout_u4(B, cols)
+    nib = B * cols // 2
+    send = torch.empty(P, dtype=torch.uint8, device=dev)
+    ctx.rows_encode_u4(padded.data_ptr(), B, cols, send.data_ptr(), send[nib + 16:].data_ptr(),
+                       cap, send[nib:].data_ptr(), s)
+    n = send[nib:nib + 4].view(torch.int32).clone()
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    if int(n.item()) > cap:
+        return gather_rows_u8(padded, group)
+    recv = torch.empty(world * P, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    out = torch.empty((world * B, cols), dtype=padded.dtype, device=dev)
+    base = recv.data_ptr()
+    for q in range(world):
+        slot = base + q * P
+        ctx.rows_decode_u4(slot, B, cols, slot + nib + 16, cap, slot + nib, out[q * B:].data_ptr(), s)
+    return out
+
+
 def gather_rows_u8(padded, group=None):
     """All-gather [B, cols] u32 rows (device int32 tensor) from every rank as u8 + escapes.
 
@@ -118,7 +164,8 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
 
     Without an initialised torch.distributed process group this counts every genome on
     one device.  With one, rank r counts block shard_bounds(G, W, r) and the blocks are
-    all-gathered, so every rank returns the full matrix in input order.
+    all-gathered (u4 rows + exact escapes on the wire for k >= 3, u8 for k = 2), so every rank
+    returns the full matrix in input order.
     count_fn(files, k) -> tensor [len(files), 4^k] replaces the HIP counter (tests).
     """
     import torch
@@ -140,7 +187,9 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
     B = block_rows(G, world)
     padded = torch.zeros((B, 1 << (2 * k)), dtype=local.dtype, device=local.device)
     padded[: hi - lo] = local
-    if padded.is_cuda and B and padded.shape[1] % 16 == 0:
+    if padded.is_cuda and B and padded.shape[1] % 32 == 0 and B * padded.shape[1] < 2**32 - 1:
+        gathered = gather_rows_u4(padded, group)
+    elif padded.is_cuda and B and padded.shape[1] % 16 == 0:
         gathered = gather_rows_u8(padded, group)
     else:
         gathered = torch.empty((world * B, 1 << (2 * k)), dtype=local.dtype, device=local.device)

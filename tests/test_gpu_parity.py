@@ -361,6 +361,61 @@ def test_rows_u8_round_trip_with_escapes(ctx, dev, ranks):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), np.concatenate(blocks))
 
 
+def _encode_u4(ctx, d_rows, cap):
+    rows, cols = d_rows.shape
+    s = torch.cuda.current_stream().cuda_stream
+    u4 = torch.full((rows * cols // 2,), 0x5A, dtype=torch.uint8, device=d_rows.device)
+    esc = torch.full((max(cap, 1) * 2,), 0x7777, dtype=torch.int32, device=d_rows.device)
+    n = torch.full((1,), -1, dtype=torch.int32, device=d_rows.device)
+    ctx.rows_encode_u4(d_rows.data_ptr(), rows, cols, u4.data_ptr(), esc.data_ptr(), cap, n.data_ptr(), s)
+    return u4, esc, n
+
+
+def test_rows_u4_round_trip_with_escapes(ctx, dev):
+    """u4 rows (two counts per byte, >= 15 saturated) + (index, value) escapes widen back to
+    the exact u32 rows -- the default wire format of the multi-GPU assembly."""
+    rng = np.random.default_rng(15)
+    rows, cols, cap = 5, 8192, 8192
+    m = rng.poisson(6, (rows, cols)).astype(np.uint32)
+    hot = rng.integers(0, m.size, 700)
+    m.reshape(-1)[hot] = rng.choice(np.array([14, 15, 16, 255, 256, 65536, 2**32 - 1], np.uint64),
+                                    hot.size).astype(np.uint32)
+    u4, esc, n = _encode_u4(ctx, torch.from_numpy(m.view(np.int32)).to(dev), cap)
+    torch.cuda.synchronize()
+    assert int(n.item()) == int((m >= 15).sum()) <= cap
+    sat = np.minimum(m, 15).astype(np.uint8).reshape(-1)
+    assert np.array_equal(u4.cpu().numpy(), sat[0::2] | (sat[1::2] << 4))
+    e = esc.cpu().numpy().view(np.uint32)[:2 * int(n.item())].reshape(-1, 2)
+    assert np.array_equal(np.sort(e[:, 0]), np.flatnonzero(m.reshape(-1) >= 15))
+    assert np.array_equal(e[:, 1], m.reshape(-1)[e[:, 0]])
+    out = torch.full((rows, cols), -3, dtype=torch.int32, device=dev)
+    ctx.rows_decode_u4(u4.data_ptr(), rows, cols, esc.data_ptr(), cap, n.data_ptr(), out.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), m)
+
+
+def test_rows_u4_escape_bounds_and_overflow(ctx, dev):
+    """A slot off the wire whose escape index points outside its block writes nothing; more
+    escapes than cap are counted, not stored (the caller falls back to another format)."""
+    m = torch.full((2, 64), 300, dtype=torch.int32, device=dev)
+    _, _, n = _encode_u4(ctx, m, 16)
+    torch.cuda.synchronize()
+    assert int(n.item()) == 128
+    rows, cols = 2, 64
+    u4 = torch.zeros(rows * cols // 2, dtype=torch.uint8, device=dev)
+    esc = torch.tensor([3, 99, rows * cols, 7, -2**31, 8], dtype=torch.int32, device=dev)  # 2^31 as u32
+    n = torch.tensor([3], dtype=torch.int32, device=dev)
+    guard = torch.full((3, cols), -1, dtype=torch.int32, device=dev)   # rows 0-1 block, row 2 guard
+    ctx.rows_decode_u4(u4.data_ptr(), rows, cols, esc.data_ptr(), 3, n.data_ptr(), guard.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    g = guard.cpu().numpy()
+    assert g[0, 3] == 99 and g[0].sum() == 99 and (g[2] == -1).all()
+    with pytest.raises(ValueError):
+        _encode_u4(ctx, torch.zeros((2, 48), dtype=torch.int32, device=dev), 16)
+
+
 def test_rows_u8_overflow_is_reported(ctx, dev):
     m = torch.full((2, 64), 300, dtype=torch.int32, device=dev)
     _, _, n = _encode(ctx, m, 16)
@@ -469,7 +524,7 @@ def test_sparse_dev_rejects_k(ctx, dev):
 
 
 # ---------------------------------------------------------------- RCCL code paths, one GPU
-def _torchrun(args, timeout=600):
+def _torchrun(args, timeout=600, nproc=1):
     import socket
     import subprocess
     import sys
@@ -477,14 +532,14 @@ def _torchrun(args, timeout=600):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def test_count_matrix_rccl_u8_assembly(tmp_path, oracle_lib):
-    """count_matrix under an RCCL process group (world size 1 on the test box): encode u8 +
+def test_count_matrix_rccl_assembly(tmp_path, oracle_lib):
+    """count_matrix under an RCCL process group (world size 1 on the test box): encode u4 +
     escapes, all-reduce, all-gather, decode -- bit-identical to counting directly."""
     files = []
     for i in range(3):
@@ -512,6 +567,29 @@ def test_bench_pipelined_u8_assembly_rccl():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["rows_checked"] is True and d["config"]["assembly"] == "u8"
+
+
+def test_bench_pipelined_u4_assembly_rccl():
+    """bench.py's pipelined u4 all-gather path (the N > 1 default) through RCCL, one rank."""
+    r = _torchrun(["bench.py", "--assemble", "u4", "--genomes", "3", "--genome-len", "3000000",
+                   "--steps", "3", "--warmup", "1", "--cpu-sample", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["rows_checked"] is True and d["config"]["assembly"] == "u4"
+
+
+@pytest.mark.parametrize("wire", ["u4", "u8"])
+def test_bench_pipelined_assembly_two_ranks(wire):
+    """Two ranks on the one GPU (gloo for the collectives, --single-device): every rank widens
+    the other rank's slot, so the assembled matrices pass the row-sum check only if decoding,
+    escapes and the double-buffered pipeline are right (6 Mbp at k = 10 averages ~5.7 per bin:
+    ~0.1 % of the cells reach 15 and travel in the u4 escape list)."""
+    r = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--single-device", "--assemble", wire,
+                   "--genomes", "4", "--genome-len", "6000000", "--k", "10", "--steps", "3", "--warmup", "1",
+                   "--cpu-sample", "0"], nproc=2)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["rows_checked"] is True and d["n_gpus"] == 2 and d["config"]["assembly"] == wire
 
 
 def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
