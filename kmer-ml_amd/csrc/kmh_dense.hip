@@ -1250,6 +1250,14 @@ int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint
                 if (rc2) return rc2;
                 return run_partitioned<K, 1024, 0, 0, 0, 0, 0, 1, 112>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
             }
+            // KMH_FC=2: fixed-capacity partition on 512-thread, 16384-window tiles (64-entry
+            // rows, 71 KiB of LDS: two workgroups per CU)
+            if (env_long("KMH_FC", 0) == 2) {
+                int rc2 = make_layout(ctx, offsets, G, K, (uint64_t)512 * kTileBpt, L);
+                if (!rc2) rc2 = upload_layout(ctx, L, s, &d_goff, &d_tbase);
+                if (rc2) return rc2;
+                return run_partitioned<K, 512, 0, 0, 0, 0, 0, 1, 64>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+            }
             if (subt == 2) return run_partitioned<K, 512, 0, 0, 0, 0, 0, 2>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
         }
         if constexpr (K == 12) {  // sweep (experiments): KMH_GSU=6 unpipelined, 4 = U 4 pipelined

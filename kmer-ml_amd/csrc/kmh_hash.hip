@@ -19,8 +19,8 @@
 //                     stores them contiguously with per-pass offsets toff2[item][pass].
 //  4. k_sp_count      one workgroup per (genome, bucket, pass): reads that pass's segment of
 //                     every split item of the bucket, inserts it into a 16384-slot LDS hash
-//                     table (linear probing, 64-bit key|count slots) and appends the distinct
-//                     k-mers to the genome's output through one atomic cursor.
+//                     table (linear probing, 64-bit key|count slots), then scans the table and
+//                     appends the distinct k-mers to the genome's output (one atomic cursor).
 //  5. fallback        a split item whose entries exceed its staging, or a pass whose distinct
 //                     keys exceed the table limit, emits nothing; those passes are counted by
 //                     gather + hipCUB radix sort + run-length encode from the step-1 entries
@@ -28,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -351,20 +352,22 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed, int abl,
     unsigned long long* __restrict__ prof) {
     // Slot = key << 32 | count; a slot is empty iff its count is 0, so every 32-bit residue
-    // (k = 21 uses all 32 bits) is a valid key.  `list` holds the slot of every key in the
-    // order it was first inserted: emission reads only those slots and stores contiguously.
+    // (k = 21 uses all 32 bits) is a valid key.  Emission scans the table: for each of the
+    // kSlots / NT slot rows a wave reads 64 consecutive slots (conflict-free) and compacts
+    // the occupied ones to consecutive output positions (ballot + mbcnt), so the stores are
+    // coalesced and the insert loop keeps no record of the slots it claimed.
     constexpr int kSlots = 1 << SB, kSlotBits = SB, kNW = NT / 64;
-    constexpr int kList = kSlots * 3 / 4;          // distinct keys one table may hold
+    constexpr int kRows = kSlots / NT;             // slot rows per thread in the scan
+    constexpr int kCap = kSlots * 3 / 4;           // distinct keys one table may hold
     __shared__ unsigned long long tbl[kSlots];
-    __shared__ uint16_t list[kList];
-    __shared__ uint32_t nlist, fail;
+    __shared__ uint32_t wtot[kNW], fail;
     __shared__ unsigned long long obase;
     constexpr int kMaxProbe = 1024;
     constexpr uint32_t SM = kSlots - 1u;
-    static_assert(kSlots <= 65536, "slot indices are u16");
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t cap = limit < (uint32_t)kList ? limit : (uint32_t)kList;
+    const uint32_t cap = limit < (uint32_t)kCap ? limit : (uint32_t)kCap;
+    const uint64_t below = (1ull << lane) - 1ull;   // lanes before this one
     // Persistent: NT-thread workgroups walk the items.
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
     const CountItem it = items[item];
@@ -373,20 +376,14 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     unsigned long long iters = 0, calls = 0;
     uint4* t4 = reinterpret_cast<uint4*>(tbl);
     for (int i = tid; i < kSlots / 2; i += NT) t4[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid == 0) {
-        nlist = 0u;
-        fail = 0u;
-    }
+    if (tid == 0) fail = 0u;
     lds_barrier();
 
     // Each lane walks its own keys one probe per iteration: CAS(empty -> key|1) claims a
-    // slot, a slot holding the key gets +1, anything else sends the key to the next slot.
-    // The slots a lane claims stay in registers and are appended to `list` once per call
-    // (one LDS add per wave), so an iteration waits on a single LDS round trip.
+    // slot, a slot holding the key gets +1, anything else sends the key to the next slot,
+    // so an iteration waits on a single LDS round trip.
     auto insert_keys = [&](uint32_t (&r)[8], int n) {
         ++calls;
-        uint32_t w[8];
-        int nw = 0;
         uint32_t s = (r[0] * 0x9E3779B1u) >> (32 - kSlotBits);
         int probes = 0;
         while (__ballot(n > 0)) {
@@ -397,12 +394,6 @@ __global__ __launch_bounds__(NT) void k_sp_count(
                 const bool won = old == 0ull;
                 const bool match = !won && (uint32_t)(old >> 32) == r[0];
                 if (match) atomicAdd(&tbl[s], 1ull);
-                if (won) {
-#pragma unroll
-                    for (int i = 7; i > 0; --i) w[i] = w[i - 1];
-                    w[0] = s;
-                    ++nw;
-                }
                 if (won || match) {
 #pragma unroll
                     for (int i = 0; i < 7; ++i) r[i] = r[i + 1];
@@ -417,20 +408,6 @@ __global__ __launch_bounds__(NT) void k_sp_count(
                 }
             }
         }
-        // append this lane's claimed slots: wave prefix sum, one LDS add per wave
-        uint32_t incl = (uint32_t)nw;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
-        }
-        const uint32_t tot = __shfl(incl, 63);
-        uint32_t base = 0u;
-        if (lane == 0 && tot) base = atomicAdd(&nlist, tot);
-        base = __shfl(base, 0) + incl - (uint32_t)nw;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (i < nw && base + i < (uint32_t)kList) list[base + i] = (uint16_t)w[i];
     };
 
     // Wave w owns split items s0 + w and s0 + w + kNW (and further ones when a bucket has
@@ -477,8 +454,22 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         atomicAdd(&prof[4], calls);
     }
     lds_barrier();
-    const uint32_t used = nlist;
     const unsigned long long c1 = prof ? clock64() : 0ull;
+
+    // Emission, pass 1: occupied slots per wave (slot rows q * NT + 64 * wave + lane).
+    uint32_t mine = 0u;
+#pragma unroll
+    for (int q = 0; q < kRows; ++q)
+        mine += (uint32_t)__builtin_popcountll(__ballot((uint32_t)tbl[q * NT + tid] != 0u));
+    if (lane == 0) wtot[wave] = mine;
+    lds_barrier();
+    uint32_t before = 0u, used = 0u;
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) {
+        const uint32_t x = wtot[w];
+        before += w < wave ? x : 0u;
+        used += x;
+    }
     if (fail || used > cap) {
         if (tid == 0) {
             const uint32_t at = atomicAdd(&failed[0], 1u);
@@ -490,24 +481,22 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     if (tid == 0) obase = (abl & 8) ? (unsigned long long)(item & 255u) * 4096ull   // timing only
                                     : atomicAdd(&nk[it.g], (unsigned long long)used);
     lds_barrier();
-    const uint64_t at = out_off[it.g] + obase;
-    const uint64_t hib = (uint64_t)it.b << R;
+    // Pass 2: this wave's occupied slots, in slot-row order, to consecutive positions.
     if (!(abl & 2)) {
-        for (uint32_t i0 = 0; i0 < used; i0 += 4u * NT) {
-            unsigned long long x[4];
+        const uint64_t at = out_off[it.g] + obase + before;
+        const uint64_t hib = (uint64_t)it.b << R;
+        uint32_t run = 0u;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t i = i0 + u * NT + tid;
-                x[u] = tbl[list[i < used ? i : 0u]];
+        for (int q = 0; q < kRows; ++q) {
+            const unsigned long long x = tbl[q * NT + tid];
+            const bool occ = (uint32_t)x != 0u;
+            const uint64_t m = __ballot(occ);
+            if (occ) {
+                const uint64_t i = at + run + (uint32_t)__builtin_popcountll(m & below);
+                __builtin_nontemporal_store(hib | (x >> 32), codes + i);
+                __builtin_nontemporal_store((uint32_t)x, counts + i);
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t i = i0 + u * NT + tid;
-                if (i < used) {
-                    __builtin_nontemporal_store(hib | (x[u] >> 32), codes + at + i);
-                    __builtin_nontemporal_store((uint32_t)x[u], counts + at + i);
-                }
-            }
+            run += (uint32_t)__builtin_popcountll(m);
         }
     }
     // The table is reused by the next item: wait for this item's LDS reads only (their
@@ -695,7 +684,14 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     uint32_t* ent = static_cast<uint32_t*>(ctx->sparse[2].ptr);
     uint16_t* toff = static_cast<uint16_t*>(ctx->sparse[3].ptr);
 
+    // KMH_SP_PROF=1 or 2 prints the host phases of every batch (2: without the kernel's own
+    // cycle counters, which slow it down; experiments)
+    const bool hprof = env_long("KMH_SP_PROF", 0) != 0;
+    auto now_ms = [] {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    };
     for (const auto& bt : batches) {
+        const double h0 = hprof ? now_ms() : 0.0;
         const int g0 = bt.first, g1 = bt.second, nG = g1 - g0;
         const uint64_t tiles = L.tbase[g1] - L.tbase[g0];
         if (tiles == 0) continue;
@@ -718,6 +714,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         std::vector<uint32_t> nb(ngb);
         KMH_HIP(ctx, hipMemcpyAsync(nb.data(), d_nb, ngb * 4, hipMemcpyDeviceToHost, s));
         KMH_HIP(ctx, hipStreamSynchronize(s));
+        const double h1 = hprof ? now_ms() : 0.0;
         std::vector<SplitItem> sitems;
         std::vector<CountItem> citems;
         sitems.reserve(ngb * 2);
@@ -742,6 +739,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
             }
         }
         if (citems.empty()) continue;
+        const double h2 = hprof ? now_ms() : 0.0;
         // split output + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
         const size_t nsi = sitems.size();
         const size_t sbytes = nsi * (size_t)kCaps * 4;
@@ -774,7 +772,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         const unsigned cgrid = (unsigned)std::min<size_t>(citems.size(), (size_t)std::max(1, ctx->num_cu) * wg_per_cu);
         // KMH_SP_PROF=1: per-phase cycle counters of k_sp_count on stderr (experiments)
         unsigned long long* d_prof = nullptr;
-        const bool prof = env_long("KMH_SP_PROF", 0) != 0;
+        const bool prof = env_long("KMH_SP_PROF", 0) == 1;
         if (prof) {
             rc = ensure(ctx, ctx->sparse[7], 256);
             if (rc) return rc;
@@ -800,6 +798,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
                          "iterations/call %.2f calls/item %.1f\n", h[5], (double)h[0] / h[5],
                          (double)h[1] / h[5], (double)h[3] / (h[4] ? h[4] : 1), (double)h[4] / h[5]);
         }
+        const double h3 = hprof ? now_ms() : 0.0;
         // passes left to the fallback: count items whose table overflowed, and every pass of
         // a bucket whose split overflowed
         uint32_t nfail = 0;
@@ -814,6 +813,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         }
         for (const CountItem& it : citems)
             if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
+        const double h4 = hprof ? now_ms() : 0.0;
         for (uint32_t id : ids) {
             const CountItem& it = citems[id];
             rc = fallback_pass(ctx, it.g, it.b, it.p, it.np, it.n, ent, toff, ldt, L.tbase[it.g] - L.tbase[g0],
@@ -821,6 +821,10 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
                                reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, s);
             if (rc) return rc;
         }
+        if (hprof)
+            std::fprintf(stderr, "sparse batch host phases (ms): partition+sizes wait %.2f, items %.2f (%zu split, "
+                         "%zu count), uploads+launches %.2f, split+count wait %.2f, fallback %.2f (%zu passes)\n",
+                         h1 - h0, h2 - h1, sitems.size(), citems.size(), h3 - h2, h4 - h3, now_ms() - h4, ids.size());
     }
     return KMH_OK;
 }
