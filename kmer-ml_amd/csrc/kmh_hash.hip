@@ -343,6 +343,99 @@ struct CountItem {
     uint32_t gb, n;
 };
 
+// Work items of one (genome, bucket) with n entries over nt tiles: P = ceil(n / target)
+// passes (at most kMaxPasses), split items of ts tiles each (about split_target entries).
+struct GbRule {
+    uint32_t np, per, ts, nsplit;
+    __device__ GbRule(uint32_t n, uint32_t nt, uint32_t target, uint32_t split_target) {
+        np = (n + target - 1u) / target;
+        np = np < (uint32_t)kMaxPasses ? np : (uint32_t)kMaxPasses;
+        per = nt ? (n + nt - 1u) / nt : 0u;
+        ts = split_target / (per + 1u);
+        ts = ts < 1u ? 1u : ts;
+        nsplit = n ? (nt + ts - 1u) / ts : 0u;
+        if (!n) np = 0u;
+    }
+};
+
+__device__ __forceinline__ uint32_t gb_tiles(const uint64_t* tbase, int g0, int gb) {
+    const int g = g0 + gb / kSpBuckets;
+    return (uint32_t)(tbase[g + 1] - tbase[g]);
+}
+
+// Item plan of a batch on the device (one workgroup): split and count items per
+// (genome, bucket) pair, exclusive offsets of both in pair order, and the two totals.
+__global__ __launch_bounds__(1024) void k_sp_plan(const uint32_t* __restrict__ nb, int ngb,
+                                                  const uint64_t* __restrict__ tbase, int g0,
+                                                  uint32_t target, uint32_t split_target,
+                                                  uint32_t* __restrict__ sofs, uint32_t* __restrict__ cofs,
+                                                  uint32_t* __restrict__ totals) {
+    __shared__ uint32_t ws[16], wc[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int per_t = (ngb + 1023) / 1024;
+    const int a = tid * per_t, e = min(ngb, a + per_t);
+    uint32_t ns = 0u, nc = 0u;
+    for (int gb = a; gb < e; ++gb) {
+        const GbRule r(nb[gb], gb_tiles(tbase, g0, gb), target, split_target);
+        ns += r.nsplit;
+        nc += r.np;
+    }
+    uint32_t is = ns, ic = nc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(is, d), y = __shfl_up(ic, d);
+        if (lane >= d) {
+            is += x;
+            ic += y;
+        }
+    }
+    if (lane == 63) {
+        ws[wave] = is;
+        wc[wave] = ic;
+    }
+    __syncthreads();
+    uint32_t bs = 0u, bc = 0u;
+    for (int w = 0; w < wave; ++w) {
+        bs += ws[w];
+        bc += wc[w];
+    }
+    uint32_t os = bs + is - ns, oc = bc + ic - nc;
+    for (int gb = a; gb < e; ++gb) {
+        const GbRule r(nb[gb], gb_tiles(tbase, g0, gb), target, split_target);
+        sofs[gb] = os;
+        cofs[gb] = oc;
+        os += r.nsplit;
+        oc += r.np;
+    }
+    if (tid == 1023) {
+        totals[0] = os;
+        totals[1] = oc;
+    }
+}
+
+// Writes the items planned by k_sp_plan: one 64-thread workgroup per (genome, bucket).
+__global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
+                                                const uint64_t* __restrict__ tbase, int g0,
+                                                uint64_t tile_lo, uint32_t target, uint32_t split_target,
+                                                const uint32_t* __restrict__ sofs,
+                                                const uint32_t* __restrict__ cofs,
+                                                SplitItem* __restrict__ sitems, CountItem* __restrict__ citems) {
+    const int gb = blockIdx.x;
+    const uint32_t n = nb[gb];
+    if (!n) return;
+    const int g = g0 + gb / kSpBuckets;
+    const uint32_t b = (uint32_t)(gb % kSpBuckets);
+    const uint32_t ta = (uint32_t)(tbase[g] - tile_lo), tb = (uint32_t)(tbase[g + 1] - tile_lo);
+    const GbRule r(n, tb - ta, target, split_target);
+    const uint32_t s0 = sofs[gb], s1 = s0 + r.nsplit;
+    for (uint32_t i = threadIdx.x; i < r.nsplit; i += 64u) {
+        const uint32_t t = ta + i * r.ts;
+        sitems[s0 + i] = SplitItem{b, t, min(t + r.ts, tb), r.np, (uint32_t)gb, r.per};
+    }
+    for (uint32_t p = threadIdx.x; p < r.np; p += 64u)
+        citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, s0, s1, (uint32_t)gb, n};
+}
+
 template <int SB, int NT>
 __global__ __launch_bounds__(NT) void k_sp_count(
     const uint32_t* __restrict__ split, const uint16_t* __restrict__ toff2,
@@ -362,8 +455,13 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     __shared__ unsigned long long tbl[kSlots];
     __shared__ uint32_t wtot[kNW], fail;
     __shared__ unsigned long long obase;
-    constexpr int kMaxProbe = 1024;
+    constexpr uint32_t kMaxIter = 8u * 1024u;     // probes of one call (8 keys per lane)
     constexpr uint32_t SM = kSlots - 1u;
+    // slot hash: top bits of the low 32 bits of a 24 x 24-bit product (v_mul_u32_u24, full
+    // rate; v_mul_lo_u32 is quarter rate) of the key folded to 24 bits
+    auto slot_of = [](uint32_t x) -> uint32_t {
+        return (uint32_t)__umul24(x ^ (x >> 15), 0x9E3779u) >> (32 - kSlotBits);
+    };
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t cap = limit < (uint32_t)kCap ? limit : (uint32_t)kCap;
@@ -381,31 +479,30 @@ __global__ __launch_bounds__(NT) void k_sp_count(
 
     // Each lane walks its own keys one probe per iteration: CAS(empty -> key|1) claims a
     // slot, a slot holding the key gets +1, anything else sends the key to the next slot,
-    // so an iteration waits on a single LDS round trip.
+    // so an iteration waits on a single LDS round trip.  The loop is VALU-issue-bound
+    // (SQ counters), so it is written for few vector instructions: the key
+    // list advances by an unconditional select (a conditional shift compiled to phi
+    // copies), the slot hash is a full-rate 24-bit multiply, and the runaway guard is a
+    // wave-uniform (scalar) iteration count instead of a per-lane probe counter.
     auto insert_keys = [&](uint32_t (&r)[8], int n) {
         ++calls;
-        uint32_t s = (r[0] * 0x9E3779B1u) >> (32 - kSlotBits);
-        int probes = 0;
-        while (__ballot(n > 0)) {
+        uint32_t s = slot_of(r[0]);
+        for (uint32_t guard = 0; __ballot(n > 0); ++guard) {
             ++iters;
+            if (guard == kMaxIter) {  // wave-uniform: a table this full goes to the fallback
+                if (n > 0) fail = 1u;
+                break;
+            }
             if (n > 0) {
-                const unsigned long long mine = ((unsigned long long)r[0] << 32) | 1ull;
-                const unsigned long long old = atomicCAS(&tbl[s], 0ull, mine);
+                const unsigned long long old = atomicCAS(&tbl[s], 0ull, ((unsigned long long)r[0] << 32) | 1ull);
                 const bool won = old == 0ull;
                 const bool match = !won && (uint32_t)(old >> 32) == r[0];
                 if (match) atomicAdd(&tbl[s], 1ull);
-                if (won || match) {
+                const bool done = won || match;
 #pragma unroll
-                    for (int i = 0; i < 7; ++i) r[i] = r[i + 1];
-                    --n;
-                    probes = 0;
-                    s = (r[0] * 0x9E3779B1u) >> (32 - kSlotBits);
-                } else if (++probes == kMaxProbe) {
-                    fail = 1u;
-                    n = 0;
-                } else {
-                    s = (s + 1u) & SM;
-                }
+                for (int i = 0; i < 7; ++i) r[i] = done ? r[i + 1] : r[i];
+                n -= done ? 1 : 0;
+                s = done ? slot_of(r[0]) : ((s + 1u) & SM);
             }
         }
     };
@@ -437,6 +534,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
 #pragma unroll
                 for (int u = 0; u < 16; ++u) sink ^= u < cnt ? r[u] : 0u;
             } else {
+                // two calls of 8 keys (a lane's valid keys are a prefix of r)
                 uint32_t a8[8], b8[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -651,7 +749,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     if (L.ntiles == 0) return KMH_OK;
 
     const size_t tile_bytes = (size_t)kSpTile * sizeof(uint32_t);
-    const size_t budget = env_mb("KMH_SP_BUDGET_MB", 8192) << 20;
+    const size_t budget = env_mb("KMH_SP_BUDGET_MB", 16384) << 20;
     // LDS hash table of the count kernel: 2^table_bits slots (KMH_SP_TABLE_BITS 12..14);
     // smaller tables let several count workgroups share a CU and overlap their latencies.
     const int table_bits = (int)std::min<long>(14, std::max<long>(12, env_long("KMH_SP_TABLE_BITS", 14)));
@@ -701,47 +799,31 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 
-        // bucket sizes -> split and count work items
+        // bucket sizes -> split and count work items, planned and written on the device;
+        // the host reads back only the two item totals to size the buffers
         const size_t ngb = (size_t)nG * kSpBuckets;
-        rc = ensure(ctx, ctx->sparse[4], ngb * 8 + 4096);
+        rc = ensure(ctx, ctx->sparse[4], ngb * 16 + 4096);
         if (rc) return rc;
         uint32_t* d_nb = static_cast<uint32_t*>(ctx->sparse[4].ptr);
         uint32_t* d_gbfail = d_nb + ngb;
+        uint32_t* d_sofs = d_gbfail + ngb;
+        uint32_t* d_cofs = d_sofs + ngb;
+        uint32_t* d_totals = d_cofs + ngb;
         KMH_HIP(ctx, hipMemsetAsync(d_gbfail, 0, ngb * 4, s));
         hipLaunchKernelGGL(k_sp_sizes, dim3((unsigned)ngb), dim3(256), 0, s, toff, ldt, d_tbase, g0,
                            L.tbase[g0], d_nb);
         KMH_HIP(ctx, hipGetLastError());
-        std::vector<uint32_t> nb(ngb);
-        KMH_HIP(ctx, hipMemcpyAsync(nb.data(), d_nb, ngb * 4, hipMemcpyDeviceToHost, s));
+        hipLaunchKernelGGL(k_sp_plan, dim3(1), dim3(1024), 0, s, d_nb, (int)ngb, d_tbase, g0, target,
+                           split_target, d_sofs, d_cofs, d_totals);
+        KMH_HIP(ctx, hipGetLastError());
+        uint32_t totals[2] = {0u, 0u};
+        KMH_HIP(ctx, hipMemcpyAsync(totals, d_totals, 8, hipMemcpyDeviceToHost, s));
         KMH_HIP(ctx, hipStreamSynchronize(s));
         const double h1 = hprof ? now_ms() : 0.0;
-        std::vector<SplitItem> sitems;
-        std::vector<CountItem> citems;
-        sitems.reserve(ngb * 2);
-        citems.reserve(ngb * 4);
-        for (int gl = 0; gl < nG; ++gl) {
-            const int g = g0 + gl;
-            const uint64_t ta = L.tbase[g] - L.tbase[g0], tb = L.tbase[g + 1] - L.tbase[g0];
-            const uint64_t nt = tb - ta;
-            for (int b = 0; b < kSpBuckets; ++b) {
-                const uint32_t n = nb[(size_t)gl * kSpBuckets + b];
-                if (!n) continue;
-                const uint32_t gb = (uint32_t)(gl * kSpBuckets + b);
-                const uint32_t np = std::min<uint32_t>(kMaxPasses, (n + target - 1) / target);
-                const uint32_t per = (uint32_t)((n + nt - 1) / nt);
-                const uint64_t ts = std::max<uint64_t>(1, split_target / (per + 1));
-                const uint32_t s0 = (uint32_t)sitems.size();
-                for (uint64_t t = ta; t < tb; t += ts)
-                    sitems.push_back(SplitItem{(uint32_t)b, (uint32_t)t, (uint32_t)std::min(t + ts, tb), np, gb, per});
-                const uint32_t s1 = (uint32_t)sitems.size();
-                for (uint32_t p = 0; p < np; ++p)
-                    citems.push_back(CountItem{(uint32_t)g, (uint32_t)b, p, np, s0, s1, gb, n});
-            }
-        }
-        if (citems.empty()) continue;
+        const size_t nsi = totals[0], nci = totals[1];
+        if (nci == 0) continue;
         const double h2 = hprof ? now_ms() : 0.0;
         // split output + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
-        const size_t nsi = sitems.size();
         const size_t sbytes = nsi * (size_t)kCaps * 4;
         const size_t t2bytes = (nsi * kT2 * 2 + 255) & ~(size_t)255;
         rc = ensure(ctx, ctx->sparse[6], sbytes + t2bytes);
@@ -749,9 +831,9 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         uint32_t* d_split = static_cast<uint32_t*>(ctx->sparse[6].ptr);
         uint16_t* d_toff2 = reinterpret_cast<uint16_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes);
         const size_t sib = (nsi * sizeof(SplitItem) + 255) & ~(size_t)255;
-        const size_t cib = (citems.size() * sizeof(CountItem) + 255) & ~(size_t)255;
+        const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
-        const size_t fb = (citems.size() + 1) * 4;
+        const size_t fb = (nci + 1) * 4;
         rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb);
         if (rc) return rc;
         char* base = static_cast<char*>(ctx->sparse[1].ptr);
@@ -759,8 +841,9 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         CountItem* d_citems = reinterpret_cast<CountItem*>(base + sib);
         uint64_t* d_out_off = reinterpret_cast<uint64_t*>(base + sib + cib);
         uint32_t* d_failed = reinterpret_cast<uint32_t*>(base + sib + cib + ob);
-        KMH_HIP(ctx, hipMemcpyAsync(d_sitems, sitems.data(), nsi * sizeof(SplitItem), hipMemcpyHostToDevice, s));
-        KMH_HIP(ctx, hipMemcpyAsync(d_citems, citems.data(), citems.size() * sizeof(CountItem), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_sp_fill, dim3((unsigned)ngb), dim3(64), 0, s, d_nb, d_tbase, g0, L.tbase[g0],
+                           target, split_target, d_sofs, d_cofs, d_sitems, d_citems);
+        KMH_HIP(ctx, hipGetLastError());
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         time_begin(ctx, s, "k_sp_split");
@@ -769,7 +852,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
         time_begin(ctx, s, "k_sp_count");
-        const unsigned cgrid = (unsigned)std::min<size_t>(citems.size(), (size_t)std::max(1, ctx->num_cu) * wg_per_cu);
+        const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * wg_per_cu);
         // KMH_SP_PROF=1: per-phase cycle counters of k_sp_count on stderr (experiments)
         unsigned long long* d_prof = nullptr;
         const bool prof = env_long("KMH_SP_PROF", 0) == 1;
@@ -781,7 +864,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         }
 #define KMH_SP_COUNT(SB, NT)                                                                         \
     hipLaunchKernelGGL((k_sp_count<SB, NT>), dim3(cgrid), dim3(NT), 0, s, d_split, d_toff2, d_citems,   \
-                       (uint32_t)citems.size(), R, limit, d_out_off, d_codes, d_counts,                     \
+                       (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts,                               \
                        reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed,                  \
                        (int)env_long("KMH_SP_ABL", 0), d_prof)
         if (table_bits == 14) KMH_SP_COUNT(14, 1024);
@@ -811,8 +894,16 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
             KMH_HIP(ctx, hipMemcpyAsync(ids.data(), d_failed + 1, (size_t)nfail * 4, hipMemcpyDeviceToHost, s));
             KMH_HIP(ctx, hipStreamSynchronize(s));
         }
-        for (const CountItem& it : citems)
-            if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
+        bool any_gbf = false;
+        for (uint32_t f : gbf) any_gbf |= f != 0u;
+        std::vector<CountItem> citems;
+        if (nfail || any_gbf) {  // items are only needed on the host to recount failed passes
+            citems.resize(nci);
+            KMH_HIP(ctx, hipMemcpyAsync(citems.data(), d_citems, nci * sizeof(CountItem), hipMemcpyDeviceToHost, s));
+            KMH_HIP(ctx, hipStreamSynchronize(s));
+            for (const CountItem& it : citems)
+                if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
+        }
         const double h4 = hprof ? now_ms() : 0.0;
         for (uint32_t id : ids) {
             const CountItem& it = citems[id];
@@ -824,7 +915,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         if (hprof)
             std::fprintf(stderr, "sparse batch host phases (ms): partition+sizes wait %.2f, items %.2f (%zu split, "
                          "%zu count), uploads+launches %.2f, split+count wait %.2f, fallback %.2f (%zu passes)\n",
-                         h1 - h0, h2 - h1, sitems.size(), citems.size(), h3 - h2, h4 - h3, now_ms() - h4, ids.size());
+                         h1 - h0, h2 - h1, nsi, nci, h3 - h2, h4 - h3, now_ms() - h4, ids.size());
     }
     return KMH_OK;
 }

@@ -490,6 +490,21 @@ def test_sparse_dev_passes_and_fallback(ctx, dev, oracle_lib, monkeypatch):
             assert np.array_equal(got[g][1], want[g][1]), (target, limit, g)
 
 
+def test_sparse_dev_multi_batch(ctx, dev, oracle_lib, monkeypatch):
+    """A 1 MB entry budget puts every genome in a batch of its own (each batch plans its items
+    on the device), with and without overflowing tables in the later batches."""
+    rng = np.random.default_rng(11)
+    genomes = _ragged_genomes(rng, [300_000, 70_001, 150_000])
+    want = [oracle_lib.count_sparse(s, 21, canonical=True)[:2] for s in genomes]
+    monkeypatch.setenv("KMH_SP_BUDGET_MB", "1")
+    for limit in ("16384", "50"):
+        monkeypatch.setenv("KMH_SP_LIMIT", limit)
+        got = _sparse_dev(ctx, dev, genomes, 21, 1)
+        for g in range(len(genomes)):
+            assert np.array_equal(got[g][0], want[g][0]), (limit, g)
+            assert np.array_equal(got[g][1], want[g][1]), (limit, g)
+
+
 def test_sparse_dev_low_complexity(ctx, dev, oracle_lib):
     # poly-T: at k = 21 the forward code's low 32 bits are all ones (a residue that must not
     # be mistaken for an empty slot)
