@@ -453,7 +453,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     constexpr int kRows = kSlots / NT;             // slot rows per thread in the scan
     constexpr int kCap = kSlots * 3 / 4;           // distinct keys one table may hold
     __shared__ unsigned long long tbl[kSlots];
-    __shared__ uint32_t wtot[kNW], fail;
+    __shared__ uint32_t wtot[kNW], fail[2];
     __shared__ unsigned long long obase;
     constexpr uint32_t kMaxIter = 8u * 1024u;     // probes of one call (8 keys per lane)
     constexpr uint32_t SM = kSlots - 1u;
@@ -466,31 +466,29 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t cap = limit < (uint32_t)kCap ? limit : (uint32_t)kCap;
     const uint64_t below = (1ull << lane) - 1ull;   // lanes before this one
-    // Persistent: NT-thread workgroups walk the items.
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-    const CountItem it = items[item];
-    if (gb_fail[it.gb]) continue;  // the split overflowed: the fallback counts this bucket
-    const unsigned long long c0 = prof ? clock64() : 0ull;
-    unsigned long long iters = 0, calls = 0;
+    // The table is zero at the top of every item: zeroed once here, then by the emission of
+    // each item (every thread clears the slots it has just read).  fail[par] collects the
+    // probe-guard failures of the current item; the other flag is cleared for the next one.
     uint4* t4 = reinterpret_cast<uint4*>(tbl);
     for (int i = tid; i < kSlots / 2; i += NT) t4[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid == 0) fail = 0u;
+    if (tid < 2) fail[tid] = 0u;
     lds_barrier();
+    uint32_t par = 0u;
 
     // Each lane walks its own keys one probe per iteration: CAS(empty -> key|1) claims a
     // slot, a slot holding the key gets +1, anything else sends the key to the next slot,
-    // so an iteration waits on a single LDS round trip.  The loop is VALU-issue-bound
-    // (SQ counters), so it is written for few vector instructions: the key
-    // list advances by an unconditional select (a conditional shift compiled to phi
-    // copies), the slot hash is a full-rate 24-bit multiply, and the runaway guard is a
-    // wave-uniform (scalar) iteration count instead of a per-lane probe counter.
+    // so an iteration waits on a single LDS round trip.  The key list advances by an
+    // unconditional select (a conditional shift compiled to phi copies), the slot hash is
+    // a full-rate 24-bit multiply, and the runaway guard is a wave-uniform (scalar)
+    // iteration count instead of a per-lane probe counter.
+    unsigned long long iters = 0, calls = 0;
     auto insert_keys = [&](uint32_t (&r)[8], int n) {
         ++calls;
         uint32_t s = slot_of(r[0]);
         for (uint32_t guard = 0; __ballot(n > 0); ++guard) {
             ++iters;
             if (guard == kMaxIter) {  // wave-uniform: a table this full goes to the fallback
-                if (n > 0) fail = 1u;
+                if (n > 0) fail[par] = 1u;
                 break;
             }
             if (n > 0) {
@@ -507,28 +505,64 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         }
     };
 
-    // Wave w owns split items s0 + w and s0 + w + kNW (and further ones when a bucket has
-    // more split items): it reads both segment bounds first, then issues the loads of up
-    // to 16 entries per lane before inserting any of them.
+    // Persistent: NT-thread workgroups walk the items.
+    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
+    const CountItem it = items[item];
+    if (gb_fail[it.gb]) continue;  // the split overflowed: the fallback counts this bucket
+    const unsigned long long c0 = prof ? clock64() : 0ull;
+
+    // The item's entries are segment p of each split item in [s0, s1).  Per group of up to
+    // 64 split items every wave reads the segment bounds (lane j: split item g + j), scans
+    // their lengths, and takes an equal share of the group's entries (concatenated in
+    // split-item order): entry e lies in the last segment whose exclusive start is <= e.
+    // Equal shares matter: the workgroup waits at the barrier for its slowest wave.
     uint32_t sink = 0u;
-    for (uint32_t jA = it.s0 + (uint32_t)wave; jA < it.s1 && !(abl & 4); jA += 2u * kNW) {
-        const uint32_t jB = jA + kNW;
-        const bool hasB = jB < it.s1;
-        const uint32_t loA = toff2[(uint64_t)jA * kT2 + it.p], hiA = toff2[(uint64_t)jA * kT2 + it.p + 1];
-        const uint32_t loB = hasB ? toff2[(uint64_t)jB * kT2 + it.p] : 0u;
-        const uint32_t hiB = hasB ? toff2[(uint64_t)jB * kT2 + it.p + 1] : 0u;
-        const uint32_t nA = hiA - loA, n = nA + (hiB - loB);
-        const uint32_t* segA = split + (uint64_t)jA * kCaps + loA;
-        const uint32_t* segB = split + (uint64_t)(hasB ? jB : jA) * kCaps + loB;
-        for (uint32_t t0 = 0; t0 < n; t0 += 1024u) {
+    for (uint32_t g = it.s0; g < it.s1 && !(abl & 4); g += 64u) {
+        const uint32_t ns = min(64u, it.s1 - g);
+        const uint32_t j = g + (uint32_t)lane;
+        uint32_t lo = 0u, len = 0u;
+        if ((uint32_t)lane < ns) {
+            lo = toff2[(uint64_t)j * kT2 + it.p];
+            len = (uint32_t)toff2[(uint64_t)j * kT2 + it.p + 1] - lo;
+        }
+        uint32_t incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        const uint32_t n = __shfl(incl, 63), excl = incl - len;
+        // segment base in entries of `split`, minus the segment's exclusive start
+        const uint64_t sb = (uint64_t)j * kCaps + lo - excl;
+        const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
+        const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
+        const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
+        for (uint32_t c = ea; c < eb; c += 1024u) {
             uint32_t r[16];
             int cnt = 0;
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const uint32_t e = t0 + 64u * u + (uint32_t)lane;
-                const uint32_t* src = e < nA ? segA + e : (e < n ? segB + (e - nA) : segA);
-                r[u] = n ? *src : 0u;
-                cnt += e < n ? 1 : 0;   // valid entries of a lane are a prefix of r
+                const uint32_t e0 = c + 64u * (uint32_t)u;        // entry of lane 0
+                const uint32_t e = e0 + (uint32_t)lane;
+                const bool ok = e < eb;
+                // Lanes past the share read a valid entry instead (lane 0's, or entry c)
+                // so every load is in bounds; es >= e1 on every lane.
+                const uint32_t e1 = e0 < eb ? e0 : c;
+                const uint32_t es = ok ? e : e1;
+                // segment of e1 (wave-uniform), then step each lane forward to the segment
+                // of es; the loop is wave-uniform so every lane takes part in each shuffle
+                int sj = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
+                for (;;) {
+                    const uint32_t nx = __shfl(excl, sj < 63 ? sj + 1 : 63);
+                    const bool adv = sj + 1 < (int)ns && nx <= es;
+                    if (!__ballot(adv)) break;
+                    sj += adv ? 1 : 0;
+                }
+                const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
+                                      (uint32_t)__shfl((int)sb_lo, sj);
+                const uint32_t v = split[base + es];
+                r[u] = ok ? v : 0u;
+                cnt += ok ? 1 : 0;   // valid entries of a lane are a prefix of r
             }
             if (abl & 1) {
 #pragma unroll
@@ -547,65 +581,70 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         }
     }
     if (abl & 1) asm volatile("" ::"v"(sink));
-    if (prof && lane == 0) {
-        atomicAdd(&prof[3], iters);
-        atomicAdd(&prof[4], calls);
-    }
     lds_barrier();
     const unsigned long long c1 = prof ? clock64() : 0ull;
 
-    // Emission, pass 1: occupied slots per wave (slot rows q * NT + 64 * wave + lane).
+    // Emission.  Each thread reads its kRows slots (rows q * NT + 64 * wave + lane,
+    // conflict-free) into registers once, clears them for the next item, and the wave
+    // counts its occupied slots; after the output base is known the registers are stored
+    // (occupied slots compacted with ballot + mbcnt, so the stores are coalesced).
+    unsigned long long x[kRows];
     uint32_t mine = 0u;
 #pragma unroll
-    for (int q = 0; q < kRows; ++q)
-        mine += (uint32_t)__builtin_popcountll(__ballot((uint32_t)tbl[q * NT + tid] != 0u));
+    for (int q = 0; q < kRows; ++q) {
+        x[q] = tbl[q * NT + tid];
+        mine += (uint32_t)__builtin_popcountll(__ballot((uint32_t)x[q] != 0u));
+    }
+#pragma unroll
+    for (int q = 0; q < kRows; ++q) tbl[q * NT + tid] = 0ull;
     if (lane == 0) wtot[wave] = mine;
+    if (tid == 0) fail[par ^ 1u] = 0u;   // read by the previous item before this one began
     lds_barrier();
     uint32_t before = 0u, used = 0u;
 #pragma unroll
     for (int w = 0; w < kNW; ++w) {
-        const uint32_t x = wtot[w];
-        before += w < wave ? x : 0u;
-        used += x;
+        const uint32_t v = wtot[w];
+        before += w < wave ? v : 0u;
+        used += v;
     }
-    if (fail || used > cap) {
-        if (tid == 0) {
+    const bool bad = fail[par] || used > cap;
+    if (tid == 0) {
+        if (bad) {
             const uint32_t at = atomicAdd(&failed[0], 1u);
             failed[1 + at] = item;
+        } else {
+            obase = (abl & 8) ? (unsigned long long)(item & 255u) * 4096ull   // timing only
+                              : atomicAdd(&nk[it.g], (unsigned long long)used);
         }
-        lds_barrier();
-        continue;
     }
-    if (tid == 0) obase = (abl & 8) ? (unsigned long long)(item & 255u) * 4096ull   // timing only
-                                    : atomicAdd(&nk[it.g], (unsigned long long)used);
     lds_barrier();
-    // Pass 2: this wave's occupied slots, in slot-row order, to consecutive positions.
-    if (!(abl & 2)) {
+    if (!bad && !(abl & 2)) {
         const uint64_t at = out_off[it.g] + obase + before;
         const uint64_t hib = (uint64_t)it.b << R;
         uint32_t run = 0u;
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
-            const unsigned long long x = tbl[q * NT + tid];
-            const bool occ = (uint32_t)x != 0u;
+            const bool occ = (uint32_t)x[q] != 0u;
             const uint64_t m = __ballot(occ);
             if (occ) {
                 const uint64_t i = at + run + (uint32_t)__builtin_popcountll(m & below);
-                __builtin_nontemporal_store(hib | (x >> 32), codes + i);
-                __builtin_nontemporal_store((uint32_t)x, counts + i);
+                __builtin_nontemporal_store(hib | (x[q] >> 32), codes + i);
+                __builtin_nontemporal_store((uint32_t)x[q], counts + i);
             }
             run += (uint32_t)__builtin_popcountll(m);
         }
     }
-    // The table is reused by the next item: wait for this item's LDS reads only (their
-    // values fed the stores above), not for the stores to reach memory.
-    lds_barrier();
+    par ^= 1u;
     if (prof && tid == 0) {
         const unsigned long long c2 = clock64();
         atomicAdd(&prof[0], c1 - c0);
         atomicAdd(&prof[1], c2 - c1);
         atomicAdd(&prof[5], 1ull);
     }
+    }
+    if (prof && lane == 0) {
+        atomicAdd(&prof[3], iters);
+        atomicAdd(&prof[4], calls);
     }
 }
 
