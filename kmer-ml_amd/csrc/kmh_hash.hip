@@ -453,6 +453,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     constexpr int kRows = kSlots / NT;             // slot rows per thread in the scan
     constexpr int kCap = kSlots * 3 / 4;           // distinct keys one table may hold
     __shared__ unsigned long long tbl[kSlots];
+    __shared__ unsigned long long dummy[NT];     // CAS target of lanes without a key
     __shared__ uint32_t wtot[kNW], fail[2];
     __shared__ unsigned long long obase;
     constexpr uint32_t kMaxIter = 8u * 1024u;     // probes of one call (8 keys per lane)
@@ -491,17 +492,22 @@ __global__ __launch_bounds__(NT) void k_sp_count(
                 if (n > 0) fail[par] = 1u;
                 break;
             }
-            if (n > 0) {
-                const unsigned long long old = atomicCAS(&tbl[s], 0ull, ((unsigned long long)r[0] << 32) | 1ull);
-                const bool won = old == 0ull;
-                const bool match = !won && (uint32_t)(old >> 32) == r[0];
-                if (match) atomicAdd(&tbl[s], 1ull);
-                const bool done = won || match;
+            // Branch-free body: every lane issues the CAS and the add (a lane without keys
+            // works on its own dummy slot, a lane without a match adds 0), and all updates
+            // are selects, so the only branches are the uniform guard and the loop edge.
+            const bool act = n > 0;
+            unsigned long long* slot = act ? &tbl[s] : &dummy[tid];
+            const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)r[0] << 32) | 1ull);
+            const bool won = old == 0ull;
+            const bool match = !won && (uint32_t)(old >> 32) == r[0];
+            atomicAdd(slot, match ? 1ull : 0ull);
+            const bool done = act && (won || match);
 #pragma unroll
-                for (int i = 0; i < 7; ++i) r[i] = done ? r[i + 1] : r[i];
-                n -= done ? 1 : 0;
-                s = done ? slot_of(r[0]) : ((s + 1u) & SM);
-            }
+            for (int i = 0; i < 7; ++i) r[i] = done ? r[i + 1] : r[i];
+            n -= done ? 1 : 0;
+            uint32_t h = slot_of(r[0]);
+            asm volatile("" : "+v"(h));   // keep the hash unconditional (no branch around it)
+            s = done ? h : ((s + 1u) & SM);
         }
     };
 
