@@ -634,8 +634,11 @@ __global__ __launch_bounds__(NT) void k_sp_count(
             const uint64_t m = __ballot(occ);
             if (occ) {
                 const uint64_t i = at + run + (uint32_t)__builtin_popcountll(m & below);
-                __builtin_nontemporal_store(hib | (x[q] >> 32), codes + i);
-                __builtin_nontemporal_store((uint32_t)x[q], counts + i);
+                // plain stores: the wave's rows form one contiguous run, and write-back
+                // stores merge the partial lines at row boundaries in L2 (exactly 12 B per
+                // distinct k-mer reach HBM); non-temporal stores wrote 32 % more bytes
+                codes[i] = hib | (x[q] >> 32);
+                counts[i] = (uint32_t)x[q];
             }
             run += (uint32_t)__builtin_popcountll(m);
         }
