@@ -211,7 +211,8 @@ struct SplitItem {
     uint32_t per;      // expected entries per tile of this bucket
 };
 
-// f(r) for every entry of bucket b in tiles [ta, tb), read as 16-byte chunks through a
+// f(r, true) for every entry of bucket b in tiles [ta, tb) (and f(x, false) for the other
+// entries of the chunks read, so the caller can stay branch-free), read as 16-byte chunks through a
 // per-wave queue: a wave takes bt tiles at a time (one per lane), lists the chunks that
 // cover their segments (tile-in-batch << 13 | chunk-in-tile) and streams them with kQU
 // loads in flight per lane; entries outside a segment are masked by position.
@@ -256,19 +257,19 @@ __device__ __forceinline__ void walk_bucket(const uint32_t* __restrict__ ent,
                 }
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
-                    if (qe[u] == kEmpty) continue;
-                    const uint32_t tl = qe[u] >> 13, p0 = (qe[u] & 8191u) * 4u;
-                    const uint32_t l = slo[tl], h = shi[tl];
+                    const bool live = qe[u] != kEmpty;   // idle lanes: every entry invalid
+                    const uint32_t qv = live ? qe[u] : 0u;
+                    const uint32_t tl = qv >> 13, p0 = (qv & 8191u) * 4u;
+                    const uint32_t l = slo[tl], h = live ? shi[tl] : 0u;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if (p0 + i >= l && p0 + i < h) f(lane_of(v[u], i));
+                    for (int i = 0; i < 4; ++i) f(lane_of(v[u], i), p0 + i >= l && p0 + i < h);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {  // skewed batch: each lane walks its own segment
-            for (uint32_t j = lo; j < hi; ++j) f(ent[t * (uint64_t)kSpTile + j]);
+            for (uint32_t j = lo; j < hi; ++j) f(ent[t * (uint64_t)kSpTile + j], true);
         }
     }
 }
@@ -277,8 +278,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     const uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, uint32_t ldt,
     const SplitItem* __restrict__ items, int R, uint32_t* __restrict__ out,
     uint16_t* __restrict__ toff2, uint32_t* __restrict__ gb_fail) {
-    __shared__ __attribute__((aligned(16))) uint32_t sorted[kCaps];
-    __shared__ uint32_t hist[kMaxPasses];
+    __shared__ __attribute__((aligned(16))) uint32_t sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
+    __shared__ uint32_t hist[kMaxPasses + 32];   // + dummy passes
     __shared__ uint32_t q[kNW][kQueue];
     __shared__ uint32_t slo[kNW][64], shi[kNW][64];
     __shared__ uint32_t wsum[4], total_sh;
@@ -291,8 +292,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     uint32_t bt = (uint32_t)kQueue / 2u / (it.per / 4u + 2u);
     bt = bt < 1u ? 1u : (bt > 64u ? 64u : bt);
     const uint32_t np = it.np;
+    // Branch-free LDS atomics: an entry outside its segment counts into one of 32 dummy
+    // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
+    // tail of `sorted`, so no exec-mask branch surrounds an atomic.
+    const uint32_t dpass = (uint32_t)kMaxPasses + (uint32_t)(lane & 31);
     walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave],
-                [&](uint32_t r) { atomicAdd(&hist[pass_of(r, np, R)], 1u); });
+                [&](uint32_t r, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
     __syncthreads();
     // exclusive scan of the pass histogram (threads 0..255)
     uint32_t n0 = 0u, incl = 0u;
@@ -323,9 +328,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     __syncthreads();
     const uint32_t total = total_sh;
     if (total > (uint32_t)kCaps) return;  // staging overflow: the bucket goes to the fallback
-    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], [&](uint32_t r) {
-        const uint32_t slot = atomicAdd(&hist[pass_of(r, np, R)], 1u);
-        sorted[slot] = r;
+    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], [&](uint32_t r, bool ok) {
+        const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
+        sorted[ok ? slot : (uint32_t)kCaps + (uint32_t)lane] = r;
     });
     __syncthreads();
     uint32_t* dst = out + (uint64_t)item * kCaps;
