@@ -44,6 +44,8 @@ extern "C" {
 
 #define KMH_MAX_DENSE_K  12     /* dense 4^k tables: 1 <= k <= 12        */
 #define KMH_MAX_SPARSE_K 32     /* sorted sparse path: 13 <= k <= 32     */
+#define KMH_MAX_LONG_K   1024   /* long k-mers (forward strand): 33 <= k <= 1024, sorted by
+                                   ceil(k / 32) code words                      */
 
 typedef struct kmh_ctx kmh_ctx;
 typedef struct kmh_fasta kmh_fasta;
@@ -95,9 +97,12 @@ void kmh_fasta_free(kmh_fasta* f);
  * `seq` whose k bytes are all bases.  Result = distinct k-mers in FIRST-OCCURRENCE
  * order (the insertion order of the reference's dict, which fixes the line order of
  * k{k}.txt, generate.py:89-91), with exact counts and the first window start.
- * 1 <= k <= 12: dense 4^k table on the GPU; 13 <= k <= 32: GPU sort + run-length.
+ * 1 <= k <= 12: dense 4^k table on the GPU; 13 <= k <= 32: GPU sort + run-length;
+ * 33 <= k <= KMH_MAX_LONG_K: GPU sort of ceil(k / 32) code words per window + run-length,
+ * and codes[i] then holds only the k-mer's first 32 bases (the whole k-mer is
+ * seq[first[i] .. first[i] + k); kmh_format_lines_seq writes its text).
  * canonical != 0 counts min(forward, reverse complement) codes (not in the reference,
- * which is forward-strand only; used for BASELINE config 5). */
+ * which is forward-strand only; used for BASELINE config 5; k <= 32 only). */
 int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int canonical,
                    kmh_kmers** out);
 uint64_t kmh_kmers_size(const kmh_kmers* r);
@@ -198,6 +203,14 @@ int kmh_write_file(const char* path, const void* data, uint64_t n, int gzip_leve
  * call with out == NULL sizes the buffer), or a negative error code. */
 int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, uint64_t n,
                          char* out, uint64_t cap);
+
+/* Same text for any k, with the digits taken from the sequence the k-mers were counted in:
+ * line i is seq[first[i] .. first[i] + k) in digits, a tab, counts[i] (the form used for
+ * k > 32, where a code no longer fits 64 bits; seq = the buffer given to kmh_count_host and
+ * first = its kmh_kmers_export first positions).  KMH_ERR_INVALID if a k-mer lies outside
+ * seq[0, seq_len). */
+int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const uint64_t* first,
+                             const uint64_t* counts, uint64_t n, char* out, uint64_t cap);
 
 #ifdef __cplusplus
 }

@@ -317,8 +317,10 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
     ctx->err.clear();
     if (!out || (n && !seq)) return fail(ctx, KMH_ERR_INVALID, "NULL argument");
     *out = nullptr;
-    if (k < 1 || k > KMH_MAX_SPARSE_K)
-        return fail(ctx, KMH_ERR_UNSUPPORTED, "k must be in [1, 32] (k = " + std::to_string(k) + ")");
+    if (k < 1 || k > KMH_MAX_LONG_K)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "k must be in [1, 1024] (k = " + std::to_string(k) + ")");
+    if (canonical && k > KMH_MAX_SPARSE_K)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "canonical counting needs k <= 32 (k = " + std::to_string(k) + ")");
     if (n >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "sequence must be shorter than 2^32 - 1 bytes");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     std::unique_ptr<kmh_kmers> r(new (std::nothrow) kmh_kmers);
@@ -340,9 +342,12 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
                                        ctx->stream)))
                 return rc;
 
-        } else {
+        } else if (k <= KMH_MAX_SPARSE_K) {
             if ((rc = kmh::sparse_count(ctx, d_seq, n, k, canonical, r->codes, r->counts, r->first,
                                         ctx->stream)))
+                return rc;
+        } else {
+            if ((rc = kmh::sparse_count_long(ctx, d_seq, n, k, r->codes, r->counts, r->first, ctx->stream)))
                 return rc;
         }
     } catch (const std::bad_alloc&) {

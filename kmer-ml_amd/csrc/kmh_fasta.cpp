@@ -244,14 +244,15 @@ int kmh_fasta_pack(const kmh_fasta* f, uint64_t min_len, uint8_t* out, uint64_t 
 
 void kmh_fasta_free(kmh_fasta* f) { delete f; }
 
-int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, uint64_t n,
-                         char* out, uint64_t cap) {
-    if (k < 1 || k > 32 || (n && (!codes || !counts))) {
-        kmh::set_thread_error("kmh_format_lines: bad arguments");
-        return KMH_ERR_INVALID;
-    }
-    // Blocks of lines are sized, prefix-summed and written on up to 16 threads (a k = 12
-    // file is ~16.7 M lines, ~250 MB).
+}  // extern "C"
+
+namespace {
+
+// Writes n lines with line(i, out) (out == NULL: return the length only) into out: blocks
+// of lines are sized, prefix-summed and written on up to 16 threads (a k = 12 file is
+// ~16.7 M lines, ~250 MB).  Returns the bytes the full text needs.
+template <typename Line>
+int64_t format_blocks(uint64_t n, char* out, uint64_t cap, Line&& line) {
     const uint64_t per = 1u << 18;
     const uint64_t nblk = n ? (n + per - 1) / per : 0;
     std::vector<uint64_t> start(nblk + 1, 0);
@@ -268,7 +269,7 @@ int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, u
     };
     parallel([&](uint64_t b) {
         uint64_t bytes = 0;
-        for (uint64_t i = b * per, e = std::min(n, (b + 1) * per); i < e; ++i) bytes += format_line(k, codes[i], counts[i], nullptr);
+        for (uint64_t i = b * per, e = std::min(n, (b + 1) * per); i < e; ++i) bytes += line(i, nullptr);
         start[b + 1] = bytes;
     });
     for (uint64_t b = 0; b < nblk; ++b) start[b + 1] += start[b];
@@ -276,17 +277,71 @@ int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, u
     if (out && total <= cap) {
         parallel([&](uint64_t b) {
             char* o = out + start[b];
-            for (uint64_t i = b * per, e = std::min(n, (b + 1) * per); i < e; ++i) o += format_line(k, codes[i], counts[i], o);
+            for (uint64_t i = b * per, e = std::min(n, (b + 1) * per); i < e; ++i) o += line(i, o);
         });
     } else if (out) {   // partial buffer: whole lines that fit, in order
         uint64_t pos = 0;
         for (uint64_t i = 0; i < n; ++i) {
-            const uint64_t len = format_line(k, codes[i], counts[i], nullptr);
-            if (pos + len <= cap) format_line(k, codes[i], counts[i], out + pos);
+            const uint64_t len = line(i, nullptr);
+            if (pos + len <= cap) line(i, out + pos);
             pos += len;
         }
     }
     return (int64_t)total;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, uint64_t n,
+                         char* out, uint64_t cap) {
+    if (k < 1 || k > 32 || (n && (!codes || !counts))) {
+        kmh::set_thread_error("kmh_format_lines: bad arguments");
+        return KMH_ERR_INVALID;
+    }
+    return format_blocks(n, out, cap, [&](uint64_t i, char* o) { return format_line(k, codes[i], counts[i], o); });
+}
+
+int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const uint64_t* first,
+                             const uint64_t* counts, uint64_t n, char* out, uint64_t cap) {
+    if (k < 1 || (n && (!seq || !first || !counts))) {
+        kmh::set_thread_error("kmh_format_lines_seq: bad arguments");
+        return KMH_ERR_INVALID;
+    }
+    for (uint64_t i = 0; i < n; ++i)
+        if (first[i] > seq_len || seq_len - first[i] < (uint64_t)k) {
+            kmh::set_thread_error("kmh_format_lines_seq: a k-mer lies outside the sequence");
+            return KMH_ERR_INVALID;
+        }
+    // digit of every byte that can start a counted window (either case); others never occur
+    static const struct Tab {
+        char d[256];
+        Tab() {
+            memset(d, '?', sizeof d);
+            d['A'] = d['a'] = '0';
+            d['T'] = d['t'] = '1';
+            d['C'] = d['c'] = '2';
+            d['G'] = d['g'] = '3';
+        }
+    } tab;
+    return format_blocks(n, out, cap, [&](uint64_t i, char* o) -> uint64_t {
+        uint64_t count = counts[i];
+        char num[24];
+        int nd = 0;
+        do {
+            num[nd++] = (char)('0' + count % 10);
+            count /= 10;
+        } while (count);
+        if (o) {
+            const uint8_t* w = seq + first[i];
+            for (int j = 0; j < k; ++j) o[j] = tab.d[w[j]];
+            o[k] = '\t';
+            for (int d = 0; d < nd; ++d) o[k + 1 + d] = num[nd - 1 - d];
+            o[k + 1 + nd] = '\n';
+        }
+        return (uint64_t)k + 2 + (uint64_t)nd;
+    });
 }
 
 }  // extern "C"

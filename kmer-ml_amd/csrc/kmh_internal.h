@@ -116,6 +116,9 @@ int rows_decode_u4(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, 
 int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
                  std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
                  std::vector<uint64_t>& first, hipStream_t s);
+// 33 <= k <= KMH_MAX_LONG_K, forward strand: sort by ceil(k / 32) code words (kmh_sparse.hip).
+int sparse_count_long(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, std::vector<uint64_t>& codes,
+                      std::vector<uint32_t>& counts, std::vector<uint64_t>& first, hipStream_t s);
 
 // First-occurrence order of a dense count row on the device (kmh_sparse.hip): the codes with
 // a nonzero count, sorted by their first window start, with counts and starts, to the host.

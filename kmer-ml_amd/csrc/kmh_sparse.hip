@@ -90,6 +90,82 @@ __global__ __launch_bounds__(256) void k_gather_counts(const uint32_t* __restric
     if (i < n) out[i] = counts[codes[i]];
 }
 
+// ---- long k-mers (33 <= k <= KMH_MAX_LONG_K), forward strand ----
+// Word w of window i holds bases [32 w, 32 w + 32) of the window, 2 bits each, first base
+// most significant, the last word left-aligned: comparing the words in order compares the
+// k-mer strings.  words is word-major (words[w * stride + i], stride >= nwin).
+__global__ __launch_bounds__(256) void k_window_words(const uint8_t* __restrict__ seq, uint64_t nwin,
+                                                      uint64_t stride, int k, int W,
+                                                      uint64_t* __restrict__ words,
+                                                      uint8_t* __restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nwin) return;
+    bool ok = true;
+    for (int w = 0; w < W; ++w) {
+        const int b0 = 32 * w, len = min(32, k - b0);
+        uint64_t v = 0;
+        for (int j = 0; j < len; ++j) {
+            const int b = base_code(seq[i + b0 + j]);
+            ok &= b >= 0;
+            v = (v << 2) | (uint64_t)(b & 3);
+        }
+        if (len < 32) v <<= 2 * (32 - len);
+        words[(uint64_t)w * stride + i] = v;
+    }
+    flags[i] = ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_gather_word(const uint64_t* __restrict__ word,
+                                                     const uint32_t* __restrict__ perm, uint64_t m,
+                                                     uint64_t* __restrict__ keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) keys[i] = word[perm[i]];
+}
+
+// 1 where sorted window i starts a run (its k-mer differs from window i - 1's).
+__global__ __launch_bounds__(256) void k_run_heads(const uint64_t* __restrict__ words, uint64_t stride,
+                                                   int W, const uint32_t* __restrict__ perm, uint64_t m,
+                                                   uint8_t* __restrict__ head) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    bool h = i == 0;
+    if (!h) {
+        const uint32_t a = perm[i], b = perm[i - 1];
+        for (int w = 0; w < W && !h; ++w) h = words[(uint64_t)w * stride + a] != words[(uint64_t)w * stride + b];
+    }
+    head[i] = h ? 1 : 0;
+}
+
+// Run r: count, first window start (the smallest: the sorts are stable and start from
+// ascending positions), and the code of its first 32 bases.
+__global__ __launch_bounds__(256) void k_long_runs(const uint32_t* __restrict__ run_start,
+                                                   const uint64_t* __restrict__ nruns, uint64_t m,
+                                                   const uint32_t* __restrict__ perm,
+                                                   const uint64_t* __restrict__ word0,
+                                                   uint32_t* __restrict__ counts, uint64_t* __restrict__ first,
+                                                   uint64_t* __restrict__ prefix) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nr = *nruns;
+    if (r >= nr) return;
+    const uint32_t s0 = run_start[r];
+    const uint64_t e = r + 1 < nr ? run_start[r + 1] : m;
+    counts[r] = (uint32_t)(e - s0);
+    first[r] = perm[s0];
+    prefix[r] = word0[perm[s0]];
+}
+
+__global__ __launch_bounds__(256) void k_gather_long(const uint32_t* __restrict__ idx,
+                                                     const uint64_t* __restrict__ prefix,
+                                                     const uint32_t* __restrict__ counts, uint64_t n,
+                                                     uint64_t* __restrict__ prefix_out,
+                                                     uint32_t* __restrict__ counts_out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        prefix_out[i] = prefix[idx[i]];
+        counts_out[i] = counts[idx[i]];
+    }
+}
+
 void* carve(char*& p, size_t bytes) {
     void* r = p;
     p += (bytes + 255) & ~(size_t)255;
@@ -247,4 +323,102 @@ int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonica
     return KMH_OK;
 }
 
+// Long k-mers: every valid window's k-mer as W = ceil(k / 32) code words; an LSD sequence of
+// W stable radix sorts (least significant word first) carrying the window positions orders
+// the windows by k-mer string, runs of equal words give the distinct k-mers with their
+// counts and first starts, and the runs are put in first-occurrence order as in
+// sparse_count (generate.py:36,58).
+int sparse_count_long(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, std::vector<uint64_t>& codes,
+                      std::vector<uint32_t>& counts, std::vector<uint64_t>& first, hipStream_t s) {
+    codes.clear();
+    counts.clear();
+    first.clear();
+    if (k <= KMH_MAX_SPARSE_K || k > KMH_MAX_LONG_K)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "long k-mer counting needs 33 <= k <= 1024");
+    if (n >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "sequence must be shorter than 2^32 - 1 bytes");
+    if (n < (uint64_t)k) return KMH_OK;
+    const uint64_t nwin = n - (uint64_t)k + 1;
+    if (nwin > 0x7FFFFFFFull) return fail(ctx, KMH_ERR_UNSUPPORTED, "sparse path supports < 2^31 windows per call");
+    const int N = (int)nwin, W = (k + 31) / 32;
+
+    size_t t_sel = 0, t_sort = 0;
+    uint64_t *k64 = nullptr, *nsel = nullptr;
+    uint32_t* v32 = nullptr;
+    uint8_t* fl = nullptr;
+    hipcub::CountingInputIterator<uint32_t> iota(0u);
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(nullptr, t_sel, iota, fl, v32, nsel, N, s));
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, k64, k64, v32, v32, N, 0, 64, s));
+    const size_t temp = std::max(t_sel, t_sort);
+    auto rup = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t bytes = (size_t)W * rup(nwin * 8) + 5 * rup(nwin * 8) + 4 * rup(nwin * 4) + rup(nwin) +
+                         temp + 4096;
+    int rc = ensure(ctx, ctx->sparse[0], bytes);
+    if (rc) return rc;
+    char* p = static_cast<char*>(ctx->sparse[0].ptr);
+    uint64_t* words = static_cast<uint64_t*>(carve(p, (size_t)W * rup(nwin * 8)));
+    const uint64_t wstride = rup(nwin * 8) / 8;   // words of one code word row
+    uint64_t* keys_a = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* keys_b = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* first_d = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* prefix_d = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint64_t* prefix_o = static_cast<uint64_t*>(carve(p, nwin * 8));
+    uint32_t* perm_a = static_cast<uint32_t*>(carve(p, nwin * 4));
+    uint32_t* perm_b = static_cast<uint32_t*>(carve(p, nwin * 4));
+    uint32_t* runs = static_cast<uint32_t*>(carve(p, nwin * 4));
+    uint32_t* cnt_d = static_cast<uint32_t*>(carve(p, nwin * 4));
+    uint8_t* flags = static_cast<uint8_t*>(carve(p, nwin));
+    uint64_t* small = static_cast<uint64_t*>(carve(p, 64));
+    void* tmp = carve(p, temp);
+    const unsigned gw = (unsigned)((nwin + 255) / 256);
+
+    time_begin(ctx, s, "k_window_words");
+    hipLaunchKernelGGL(k_window_words, dim3(gw), dim3(256), 0, s, d_seq, nwin, wstride, k, W, words, flags);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    size_t t = temp;
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(tmp, t, iota, flags, perm_a, small, N, s));
+    uint64_t m = 0;
+    KMH_HIP(ctx, hipMemcpyAsync(&m, small, 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    if (m == 0) return KMH_OK;
+    const int M = (int)m;
+    const unsigned gm = (unsigned)((m + 255) / 256);
+    for (int w = W - 1; w >= 0; --w) {   // least significant word first; stable sorts
+        hipLaunchKernelGGL(k_gather_word, dim3(gm), dim3(256), 0, s, words + (uint64_t)w * wstride, perm_a, m, keys_a);
+        KMH_HIP(ctx, hipGetLastError());
+        t = temp;
+        KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t, keys_a, keys_b, perm_a, perm_b, M, 0, 64, s));
+        std::swap(perm_a, perm_b);
+    }
+    hipLaunchKernelGGL(k_run_heads, dim3(gm), dim3(256), 0, s, words, wstride, W, perm_a, m, flags);
+    KMH_HIP(ctx, hipGetLastError());
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceSelect::Flagged(tmp, t, iota, flags, runs, small + 1, M, s));
+    hipLaunchKernelGGL(k_long_runs, dim3(gm), dim3(256), 0, s, runs, small + 1, m, perm_a, words, cnt_d,
+                       first_d, prefix_d);
+    KMH_HIP(ctx, hipGetLastError());
+    uint64_t nruns = 0;
+    KMH_HIP(ctx, hipMemcpyAsync(&nruns, small + 1, 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    // first-occurrence order: sort the runs by first start, gather prefix codes and counts
+    int bits = 1;
+    while (bits < 64 && (1ull << bits) < n) ++bits;
+    const unsigned gr = (unsigned)((nruns + 255) / 256);
+    hipLaunchKernelGGL(k_iota, dim3(gr), dim3(256), 0, s, perm_b, nruns);
+    KMH_HIP(ctx, hipGetLastError());
+    t = temp;
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t, first_d, keys_b, perm_b, runs, (int)nruns, 0, bits, s));
+    hipLaunchKernelGGL(k_gather_long, dim3(gr), dim3(256), 0, s, runs, prefix_d, cnt_d, nruns, prefix_o, perm_b);
+    KMH_HIP(ctx, hipGetLastError());
+    codes.resize(nruns);
+    counts.resize(nruns);
+    first.resize(nruns);
+    KMH_HIP(ctx, hipMemcpyAsync(codes.data(), prefix_o, nruns * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(counts.data(), perm_b, nruns * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(first.data(), keys_b, nruns * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    return KMH_OK;
+}
+
 }  // namespace kmh
+

@@ -49,6 +49,7 @@ SIGNATURES = [
     ("kmh_first_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
     ("kmh_synth_dev", _c.c_int, [_vp, _vp, _u64, _u64, _c.c_int, _u64, _vp]),
     ("kmh_format_lines", _c.c_int64, [_c.c_int, _vp, _vp, _u64, _vp, _u64]),
+    ("kmh_format_lines_seq", _c.c_int64, [_c.c_int, _vp, _u64, _vp, _vp, _u64, _vp, _u64]),
     ("kmh_write_file", _c.c_int, [_c.c_char_p, _vp, _u64, _c.c_int, _c.c_int]),
     ("kmh_count_sparse_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp]),
     ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
@@ -309,6 +310,19 @@ def format_lines(k, codes, counts):
     need = _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, None, 0))
     out = ctypes.create_string_buffer(max(need, 1))
     _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, out, need))
+    return out.raw[:need]
+
+
+def format_lines_seq(k, seq, first, counts):
+    """k{k}.txt bytes for any k, the digits of line i taken from seq[first[i] : first[i] + k]
+    (``seq`` = the buffer the k-mers were counted in; the form used for k > 32)."""
+    buf = _as_u8(seq)
+    first = np.ascontiguousarray(first, dtype=np.uint64)
+    counts = np.ascontiguousarray(counts, dtype=np.uint64)
+    n = first.size
+    need = _check(lib().kmh_format_lines_seq(int(k), _ptr(buf), buf.size, _ptr(first), _ptr(counts), n, None, 0))
+    out = ctypes.create_string_buffer(max(need, 1))
+    _check(lib().kmh_format_lines_seq(int(k), _ptr(buf), buf.size, _ptr(first), _ptr(counts), n, out, need))
     return out.raw[:need]
 
 

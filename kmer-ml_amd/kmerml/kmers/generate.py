@@ -18,9 +18,10 @@ the reference itself, tests/golden/):
   distinct k-mer, digits A=0 T=1 C=2 G=3, lines in first-occurrence order (:68-91); an
   empty result still creates the file.
 
-Differences: 1 <= k <= 32 is supported (k >= 33 raises NotImplementedError,
-k <= 0 raises ValueError); counting never falls back to the CPU -- without the HIP
-library or a device it raises.
+Differences: 1 <= k <= 1024 is supported (k > 1024 raises NotImplementedError,
+k <= 0 raises ValueError; k >= 33 is counted by sorting ceil(k / 32) code words per window
+and its lines are written from the sequence); counting never falls back to the CPU --
+without the HIP library or a device it raises.
 """
 import os
 from pathlib import Path
@@ -54,6 +55,7 @@ class KmerExtractor:
             multiplicity[k] += 1
         fasta = _native.FastaFile(fasta_file)
         results = {}
+        packed = np.zeros(0, np.uint8)
         if len(fasta):
             longest = max(k_values)
             for k in k_order:
@@ -73,9 +75,14 @@ class KmerExtractor:
                     print(f"Skipping {rid}: too short for k-mer extraction")
         fasta.close()
         for k in k_order:
-            codes, counts, _ = results.get(k, (np.empty(0, np.uint64), np.empty(0, np.uint32), None))
-            self._write_kmer_file(organism_id, k, codes,
-                                  counts.astype(np.uint64) * np.uint64(multiplicity[k]))
+            codes, counts, first = results.get(k, (np.empty(0, np.uint64), np.empty(0, np.uint32),
+                                                   np.empty(0, np.uint64)))
+            counts = counts.astype(np.uint64) * np.uint64(multiplicity[k])
+            if k > 32:   # a code holds 32 bases: the line digits come from the sequence
+                self._write_bytes(self._kmer_path(organism_id, k),
+                                  _native.format_lines_seq(k, packed, first, counts))
+            else:
+                self._write_kmer_file(organism_id, k, codes, counts)
         return organism_id
 
     def _kmer_path(self, organism_id, k):

@@ -214,6 +214,38 @@ def test_sparse_vs_oracle(ctx, oracle_lib, k, canonical):
     assert np.array_equal(first, wf[order])
 
 
+@pytest.mark.parametrize("k", [33, 40, 63, 64, 65, 100])
+def test_long_kmers_vs_python_oracle(ctx, k):
+    """k > 32 (the reference's dict takes any k): word-sorted on the GPU, first-occurrence
+    order, and the k{k}.txt text written from the sequence, byte-identical to the pure-Python
+    restatement of generate.py:49-58 + :86-91 (oracle/kmers.py).  Repeated segments give
+    counts > 1; lowercase, N and newlines break or fold windows as in the reference."""
+    from oracle import kmers as okmers
+    rng = np.random.default_rng(4000 + k)
+    seg = _rand_seq(rng, 700, b"ACGTACGTACGTacgt")
+    parts = []
+    for _ in range(12):
+        parts += [_rand_seq(rng, int(rng.integers(50, 5000)), b"ACGTACGTACGTACGTacgtN\n"), seg]
+    seq = np.concatenate(parts)
+    codes, counts, first = ctx.count(seq, k)
+    text = _native.format_lines_seq(k, seq, first, counts.astype(np.uint64))
+    want = okmers.count_sequence(seq.tobytes().decode(), k)
+    assert text.decode() == okmers.kmer_text(want)
+    assert counts.max() >= 12
+    prefix = [okmers.kmer_code(km[:32]) for km in want]
+    assert np.array_equal(codes, np.array(prefix, np.uint64))
+
+
+def test_long_kmers_limits(ctx):
+    seq = np.frombuffer(b"ACGT" * 300, np.uint8)
+    with pytest.raises(NotImplementedError):
+        ctx.count(seq, 1025)
+    with pytest.raises(NotImplementedError):
+        ctx.count(seq, 33, canonical=True)
+    codes, counts, first = ctx.count(seq, 1024)   # 177 windows, 4 distinct
+    assert codes.size == 4 and counts.sum() == 1200 - 1024 + 1 and list(first) == [0, 1, 2, 3]
+
+
 @pytest.mark.parametrize("k", [1, 7, 12])
 def test_count_host_dense_first_order(ctx, oracle_lib, k):
     rng = np.random.default_rng(k)
@@ -243,12 +275,9 @@ def _run_extractor(tmp_path, fasta, ks, compress=False, org="org"):
 
 
 def test_dropin_edge_cases_byte_identical(tmp_path, golden_dir, edge_cases):
+    # every case, k = 33 and k = 40 included (long k-mers: word-sorted on the GPU, lines
+    # written from the sequence)
     for i, case in enumerate(edge_cases):
-        if max(case["k_values"]) > 32:
-            with pytest.raises(NotImplementedError):
-                _run_extractor(tmp_path / f"c{i}", os.path.join(golden_dir, "inputs", case["input"]),
-                               case["k_values"])
-            continue
         ret, out, files = _run_extractor(tmp_path / f"c{i}", os.path.join(golden_dir, "inputs", case["input"]),
                                          case["k_values"])
         assert ret == case["returned"]

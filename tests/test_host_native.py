@@ -111,6 +111,28 @@ def test_format_lines_matches_reference_text(k):
     assert lines[0] == "".join(okmers.DIGIT[b] for b in c0) + f"\t{int(counts[0])}"
 
 
+@pytest.mark.parametrize("k", [3, 32, 33, 40, 100])
+def test_format_lines_seq_matches_reference_text(k):
+    """kmh_format_lines_seq (the k > 32 writer): digits from the sequence at each k-mer's
+    first start, equal to the reference's text for the same table (oracle/kmers.py)."""
+    rng = np.random.default_rng(k)
+    unit = "".join("ACGTacgt"[i] for i in rng.integers(0, 8, 300))
+    seq = (unit + "N" + unit[:150] + "\n" + unit).encode()
+    table = okmers.count_sequence(seq.decode(), k)
+    firsts = {}
+    up = seq.decode().upper()
+    for i in range(len(up) - k + 1):
+        firsts.setdefault(up[i:i + k], i)
+    first = np.array([firsts[km] for km in table], np.uint64)
+    counts = np.array(list(table.values()), np.uint64)
+    got = _native.format_lines_seq(k, np.frombuffer(seq, np.uint8), first, counts)
+    assert got.decode() == okmers.kmer_text(table)
+    assert counts.max() >= 2
+    with pytest.raises(ValueError):
+        _native.format_lines_seq(k, np.frombuffer(seq, np.uint8), np.array([len(seq) - k + 1], np.uint64),
+                                 np.array([1], np.uint64))
+
+
 def test_format_lines_empty():
     assert _native.format_lines(8, np.empty(0, np.uint64), np.empty(0, np.uint64)) == b""
 
