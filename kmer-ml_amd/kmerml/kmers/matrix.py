@@ -203,7 +203,8 @@ def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
     """Sparse k-mer counts of this rank's block of `genome_files` (BASELINE config 5).
 
     For 13 <= k <= 21 the genomes are counted on the GPU with the partitioned hash-table path
-    (kmh_count_sparse_dev).  The 4^k columns cannot be assembled densely (4^21 ~ 4.4e12), so
+    (kmh_count_sparse_dev); any other 1 <= k <= 32 genome by genome with the GPU sort path of
+    kmh_count_host (dense table for k <= 12).  The 4^k columns cannot be assembled densely (4^21 ~ 4.4e12), so
     nothing is exchanged: with a torch.distributed process group, rank r counts block
     shard_bounds(G, W, r) and keeps it.  Returns (lo, rows) where rows[i] is
     (codes uint64 ascending, counts uint32) of genome lo + i.
@@ -211,8 +212,8 @@ def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
     import torch
     import torch.distributed as dist
 
-    if not 13 <= k <= 21:
-        raise NotImplementedError("device sparse counting needs 13 <= k <= 21")
+    if not 1 <= k <= 32:
+        raise NotImplementedError("sparse rows need 1 <= k <= 32 (a 64-bit code per k-mer)")
     files = list(genome_files)
     world, rank = 1, 0
     if dist.is_available() and dist.is_initialized():
@@ -223,6 +224,14 @@ def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
     if hi == lo:
         return lo, []
     buf, offsets = pack_genomes(files[lo:hi], k)
+    if not 13 <= k <= 21:   # outside the batched hash-table path: one GPU count per genome
+        ctx = _native.context(device)
+        rows = []
+        for g in range(hi - lo):
+            codes, counts, _ = ctx.count(buf[int(offsets[g]):int(offsets[g + 1])], k, canonical=canonical)
+            order = np.argsort(codes, kind="stable")
+            rows.append((codes[order], counts[order]))
+        return lo, rows
     dev = torch.device("cuda", device)
     d_seq = torch.from_numpy(buf).to(dev) if buf.size else torch.zeros(16, dtype=torch.uint8, device=dev)
     out_off = _native.sparse_out_offsets(offsets, k)

@@ -646,8 +646,10 @@ def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
     assert np.array_equal(got[0], wc) and np.array_equal(got[1], wn)
 
 
-def test_sparse_rows_from_fasta(tmp_path, oracle_lib):
-    """kmerml.kmers.matrix.sparse_rows: FASTA files -> per-genome sorted sparse counts."""
+@pytest.mark.parametrize("k,canonical", [(21, True), (9, False), (25, True), (32, False)])
+def test_sparse_rows_from_fasta(tmp_path, oracle_lib, k, canonical):
+    """kmerml.kmers.matrix.sparse_rows: FASTA files -> per-genome sorted sparse counts (the
+    batched hash-table path for 13 <= k <= 21, per-genome GPU counts otherwise)."""
     files, seqs = [], []
     for i in range(3):
         p = tmp_path / f"g{i}.fa"
@@ -655,8 +657,8 @@ def test_sparse_rows_from_fasta(tmp_path, oracle_lib):
         osynth.write_fasta(p, [(f"SYN_{i}", seq), (f"short_{i}", b"ACGT")])   # short record dropped
         files.append(str(p))
         seqs.append(seq)
-    lo, rows = kmatrix.sparse_rows(files, 21, canonical=True)
+    lo, rows = kmatrix.sparse_rows(files, k, canonical=canonical)
     assert lo == 0 and len(rows) == 3
     for (codes, counts), seq in zip(rows, seqs):
-        wc, wn, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), 21, canonical=True)
+        wc, wn, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), k, canonical=canonical)
         assert np.array_equal(codes, wc) and np.array_equal(counts, wn)
