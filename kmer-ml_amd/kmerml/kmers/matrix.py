@@ -251,3 +251,63 @@ def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
         rows.append((c[order].cpu().numpy().view(np.uint64),
                      d_counts[a:a + int(n[g])][order].cpu().numpy().view(np.uint32)))
     return lo, rows
+
+
+def split_bounds(n, world, rank, k, align=16):
+    """Rank `rank`'s slice of a packed genome of n bytes split across `world` ranks.
+
+    Returns (a, b, e): the rank counts the windows that start in [a, b) from the bytes [a, e),
+    e = min(n, b + k - 1) (a (k - 1)-byte halo past b).  a and b are multiples of `align` (the
+    device counter wants 16-byte aligned starts), the last rank ends at n, so the ranks' [a, b)
+    tile [0, n) and every window is counted by exactly one rank.
+    """
+    a = (n * rank // world) // align * align
+    b = n if rank == world - 1 else (n * (rank + 1) // world) // align * align
+    return a, b, min(n, b + k - 1)
+
+
+def _hip_count_slice(sl, k, device):
+    import torch
+
+    dev = torch.device("cuda", device)
+    out = torch.zeros((1, 1 << (2 * k)), dtype=torch.int32, device=dev)
+    if sl.size >= k:
+        d_seq = torch.from_numpy(np.ascontiguousarray(sl)).to(dev)
+        ctx = _native.context(device)
+        ctx.count_dense_dev(d_seq.data_ptr(), np.array([0, sl.size], dtype=np.uint64), k, out.data_ptr(),
+                            torch.cuda.current_stream(dev).cuda_stream)
+    return out[0]
+
+
+def count_genome_split(genome_file, k, device=None, group=None, count_fn=None):
+    """Dense [4^k] count row of ONE genome counted by every rank together (SURVEY.md 8(e),
+    the optional split of a genome too large for one GPU's share of the work).
+
+    The genome is packed as for count_matrix (records shorter than k dropped, records joined
+    by a non-base byte, generate.py:39-56); rank r counts the windows that start in its slice
+    split_bounds(n, W, r, k) -- the slice plus a (k - 1)-byte halo -- and one all-reduce(SUM)
+    over the process group (RCCL over xGMI with the "nccl" backend) adds the partial rows, so
+    every rank returns the genome's full row (int32 storage of u32: the sum wraps exactly like
+    u32).  Without a process group the whole genome is counted on one device.
+    count_fn(uint8 slice, k) -> tensor [4^k] replaces the HIP counter (CPU tests).
+    """
+    import torch
+    import torch.distributed as dist
+
+    if not 1 <= k <= _native.MAX_DENSE_K:
+        raise NotImplementedError("the dense count row needs 1 <= k <= 12")
+    if device is None:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+    counter = count_fn or (lambda sl, kk: _hip_count_slice(sl, kk, device))
+    buf, _ = pack_genomes([genome_file], k)
+    if not (dist.is_available() and dist.is_initialized()):
+        return counter(buf, k)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    a, _, e = split_bounds(buf.size, world, rank, k)
+    row = counter(buf[a:e], k).clone()
+    if dist.get_backend(group) == "gloo" and row.is_cuda:   # gloo reduces host tensors
+        host = row.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+        return host.to(row.device)
+    dist.all_reduce(row, op=dist.ReduceOp.SUM, group=group)
+    return row

@@ -603,6 +603,25 @@ def test_count_matrix_rccl_assembly(tmp_path, oracle_lib):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("backend,nproc", [("nccl", 1), ("gloo", 2), ("gloo", 3)])
+def test_count_genome_split(tmp_path, oracle_lib, backend, nproc):
+    """One genome counted by several ranks (slices + (k - 1)-byte halos on the GPU, all-reduce of
+    the rows; RCCL with one rank, gloo with 2-3 ranks sharing cuda:0): every rank's row equals
+    the oracle's count of the whole genome (3 records incl. lowercase, N runs, a short record)."""
+    seq = osynth.synth_bases(3_000_017, osynth.genome_seed(5)).tobytes()
+    recs = [("a", seq[:1_000_000].lower()), ("b", b"ACGTN" * 3), ("c", seq[1_000_000:2_000_000] + b"NN" + seq[2_000_000:])]
+    fa = tmp_path / "g.fa"
+    osynth.write_fasta(fa, recs)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = _torchrun([os.path.join(here, "split_probe.py"), str(tmp_path), "12", str(fa), backend], nproc=nproc)
+    assert r.returncode == 0, r.stderr[-3000:]
+    buf, _ = kmatrix.pack_genomes([str(fa)], 12)
+    want = oracle_lib.count_dense(bytes(buf), 12)
+    for q in range(nproc):
+        got = np.load(tmp_path / f"row{q}.npy").view(np.uint32)
+        assert np.array_equal(got, want)
+
+
 def test_bench_pipelined_u8_assembly_rccl():
     """bench.py's pipelined u8 all-gather path (the N > 1 default) through RCCL, one rank."""
     r = _torchrun(["bench.py", "--assemble", "u8", "--genomes", "3", "--genome-len", "3000000",

@@ -70,3 +70,61 @@ def test_shard_bounds_cover_in_order():
             assert spans[0][0] == 0 and spans[-1][1] == G
             assert all(spans[i][1] == spans[i + 1][0] for i in range(W - 1))
             assert all(hi - lo <= kmatrix.block_rows(G, W) for lo, hi in spans)
+
+
+def _oracle_slice_counter(sl, k):
+    from oracle import corac
+    return torch.from_numpy(corac.count_dense(bytes(sl), k).view(np.int32).copy())
+
+
+def _split_worker(rank, world, port, path, k, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "kmer-ml_amd"), os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        row = kmatrix.count_genome_split(path, k, count_fn=_oracle_slice_counter)
+        np.save(os.path.join(outdir, f"split{rank}.npy"), row.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,n", [(2, 6, 5000), (3, 12, 4099), (3, 4, 20)])
+def test_count_genome_split_gloo(tmp_path, oracle_lib, world, k, n):
+    """One genome split across ranks with a (k - 1)-byte halo + all-reduce(SUM): every rank's
+    row equals the whole genome counted at once (records, lowercase, N runs, a record shorter
+    than k, a genome too short for some ranks to own a window)."""
+    from oracle import corac
+    from oracle import fasta as ofasta
+    from oracle import synth as osynth
+    seq = osynth.synth_bases(n, osynth.genome_seed(7)).tobytes()
+    mid = len(seq) // 2
+    recs = [("r1", seq[:mid].lower() + b"NNNN" + seq[mid:mid + 10]), ("r2", b"ACG"), ("r3", seq[mid:])]
+    path = tmp_path / "g.fa"
+    osynth.write_fasta(path, recs)
+    mp.spawn(_split_worker, args=(world, _free_port(), str(path), k, str(tmp_path)), nprocs=world, join=True)
+    kept = [s for _, _, s in ofasta.parse_fasta(str(path)) if len(s) >= k]
+    want = corac.count_dense("".join(s + "\n" for s in kept).encode(), k)
+    for r in range(world):
+        got = np.load(tmp_path / f"split{r}.npy").view(np.uint32)
+        assert np.array_equal(got, want)
+
+
+def test_split_bounds_count_every_window_once():
+    for n in range(0, 300, 7):
+        for W in (1, 2, 3, 8):
+            for k in (1, 5, 12):
+                seen = np.zeros(max(n - k + 1, 0), np.int64)
+                for r in range(W):
+                    a, b, e = kmatrix.split_bounds(n, W, r, k)
+                    assert a % 16 == 0 and a <= b <= n and e <= n
+                    for s in range(a, b):
+                        if s + k <= e:
+                            seen[s] += 1
+                        else:
+                            assert s + k > n
+                assert np.all(seen == 1)
