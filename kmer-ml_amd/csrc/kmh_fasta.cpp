@@ -12,8 +12,12 @@
 //
 // kmh_format_lines replaces the writer loop of _save_kmers_to_file (generate.py:86-91).
 #include <errno.h>
+#include <stdlib.h>
+#include <sys/mman.h>
+#include <fcntl.h>
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <memory>
 #include <new>
@@ -21,6 +25,7 @@
 #include <vector>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <thread>
 #include "kmh_internal.h"
@@ -29,8 +34,12 @@ struct kmh_fasta {
     struct Rec {
         uint64_t id_off, id_len, seq_off, seq_len, char_len;
     };
+    struct Free {
+        void operator()(uint8_t* q) const { free(q); }
+    };
     std::string ids;
-    std::vector<uint8_t> seqs;
+    std::unique_ptr<uint8_t[], Free> seqs;   // every record's bytes, back to back
+    uint64_t nseq = 0;
     std::vector<Rec> recs;
 };
 
@@ -75,6 +84,150 @@ size_t rstrip_len(const uint8_t* p, size_t n) {
     return n;
 }
 
+
+// n bytes (at least 1) for a whole file: 2 MiB aligned with transparent huge pages requested,
+// so that first-touching a genome-sized buffer takes a few hundred page faults, not ~25 000
+// per 100 MB.  Throws std::bad_alloc.
+uint8_t* alloc_bytes(size_t n) {
+    constexpr size_t kHuge = 2u << 20;
+    void* q = nullptr;
+    const size_t sz = (std::max<size_t>(n, 1) + kHuge - 1) / kHuge * kHuge;
+    if (posix_memalign(&q, kHuge, sz) != 0 || !q) throw std::bad_alloc();
+    madvise(q, sz, MADV_HUGEPAGE);   // advisory: ignored where THP is off
+    return static_cast<uint8_t*>(q);
+}
+
+// One piece of a FASTA buffer, parsed in place: its sequence bytes (lines before its first
+// header included -- whether they belong to a record is decided when the pieces are stitched)
+// are compacted to the front of the piece's own byte range, which they never outgrow, so
+// parsing allocates nothing.  Each header keeps the output offset where its record's bases
+// start and the continuation-byte count before it.
+struct Piece {
+    struct Hdr {
+        uint64_t at, cont_before;
+        std::string id;
+    };
+    uint64_t len = 0, cont = 0;
+    std::vector<Hdr> hdrs;
+};
+
+uint64_t count_continuation(const uint8_t* p, size_t n);
+
+// The lines of p[a, b): a is a line start, b a line start or the end of the buffer.
+void parse_lines(uint8_t* p, size_t a, size_t b, Piece& out) {
+    size_t i = a, w = a;   // read and write positions, w <= i
+    while (i < b) {
+        // line end: the first '\n' or '\r' (memchr: vectorised scans of ~80-byte lines)
+        const void* nl = memchr(p + i, '\n', b - i);
+        size_t j = nl ? (size_t)(static_cast<const uint8_t*>(nl) - p) : b;
+        if (const void* cr = memchr(p + i, '\r', j - i)) j = (size_t)(static_cast<const uint8_t*>(cr) - p);
+        const uint8_t* line = p + i;
+        const size_t len = j - i;
+        // advance past the line terminator (\r\n counts once)
+        if (j < b && p[j] == '\r' && j + 1 < b && p[j + 1] == '\n') i = j + 2;
+        else i = j + 1;
+        if (len > 0 && line[0] == '>') {
+            const size_t tl = rstrip_len(line + 1, len - 1);
+            const uint8_t* t = line + 1;
+            size_t c = 0;
+            for (size_t x; c < tl && (x = leading_space(t + c, tl - c)) != 0;) c += x;
+            size_t d = c;
+            while (d < tl && leading_space(t + d, tl - d) == 0) ++d;
+            out.hdrs.push_back(Piece::Hdr{w - a, out.cont, std::string(reinterpret_cast<const char*>(t + c), d - c)});
+            continue;
+        }
+        const size_t sl = rstrip_len(line, len);
+        const size_t w0 = w;
+        if (!memchr(line, ' ', sl)) {
+            memmove(p + w, line, sl);
+            w += sl;
+        } else {
+            for (size_t q = 0; q < sl; ++q)
+                if (line[q] != ' ') p[w++] = line[q];
+        }
+        out.cont += count_continuation(p + w0, w - w0);
+    }
+    out.len = w - a;
+}
+
+// Run f(t) for t in [0, n) on up to `threads` threads (the caller's thread included).
+template <typename F>
+void run_pool(size_t n, unsigned threads, F&& f) {
+    if (n == 0) return;
+    std::atomic<size_t> next{0};
+    std::atomic<bool> oom{false};
+    auto work = [&]() {
+        try {
+            for (size_t t; (t = next.fetch_add(1)) < n;) f(t);
+        } catch (const std::bad_alloc&) {
+            oom = true;
+        }
+    };
+    std::vector<std::thread> pool;
+    const unsigned nt = (unsigned)std::min<size_t>(n, std::max(1u, threads));
+    for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    if (oom) throw std::bad_alloc();
+}
+
+// UTF-8 continuation bytes (10xxxxxx) of p[0, n): a record's character count, the length
+// Python's len(str) reports for generate.py:44's short-record rule, is bytes minus these.
+uint64_t count_continuation(const uint8_t* p, size_t n) {
+    uint64_t c = 0;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        c += (uint64_t)__builtin_popcountll(w & ~(w << 1) & 0x8080808080808080ull);
+    }
+    for (; i < n; ++i) c += (p[i] & 0xC0u) == 0x80u;
+    return c;
+}
+
+// Records from the pieces in order: a piece's bytes before its first header continue the
+// record open at its start (text before the file's first header belongs to none).  The
+// pieces' outputs are moved down over the gaps (header lines, line ends) left between them,
+// in order, inside the same buffer, which then holds every record back to back.
+void stitch(std::vector<Piece>& pieces, const std::vector<size_t>& cut, uint8_t* buf, kmh_fasta& f) {
+    uint64_t pos = 0, cont = 0;   // output end; continuation bytes of the open record
+    bool in_record = false;
+    auto move = [&](uint64_t from, uint64_t len) {
+        if (from != pos && len) memmove(buf + pos, buf + from, len);
+        pos += len;
+    };
+    auto close = [&]() {
+        kmh_fasta::Rec& r = f.recs.back();
+        r.seq_len = pos - r.seq_off;
+        r.char_len = r.seq_len - cont;
+    };
+    for (size_t t = 0; t < pieces.size(); ++t) {
+        const Piece& pc = pieces[t];
+        const uint64_t base = cut[t];
+        const uint64_t first = pc.hdrs.empty() ? pc.len : pc.hdrs[0].at;
+        if (in_record) {
+            move(base, first);
+            cont += pc.hdrs.empty() ? pc.cont : pc.hdrs[0].cont_before;
+        }
+        for (size_t h = 0; h < pc.hdrs.size(); ++h) {
+            if (in_record) close();
+            in_record = true;
+            kmh_fasta::Rec r{};
+            r.id_off = f.ids.size();
+            r.id_len = pc.hdrs[h].id.size();
+            f.ids += pc.hdrs[h].id;
+            r.seq_off = pos;
+            f.recs.push_back(r);
+            const bool last = h + 1 == pc.hdrs.size();
+            const uint64_t end = last ? pc.len : pc.hdrs[h + 1].at;
+            move(base + pc.hdrs[h].at, end - pc.hdrs[h].at);
+            cont = (last ? pc.cont : pc.hdrs[h + 1].cont_before) - pc.hdrs[h].cont_before;
+        }
+    }
+    if (in_record) close();
+    f.nseq = pos;
+}
+
 }  // namespace
 
 namespace {
@@ -113,16 +266,48 @@ int kmh_fasta_read(const char* path, kmh_fasta** out) {
         kmh::set_thread_error(std::string("cannot open ") + path + ": " + strerror(errno));
         return KMH_ERR_IO;
     }
-    std::vector<uint8_t> buf;
+    // The file is read straight into one buffer of its size, by up to 16 threads with pread
+    // (a page-cache copy); anything past that size (a file that grew, a pipe) is appended
+    // from a chunked read.
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned max_threads = std::min(16u, hw);
+    const bool prof = kmh::env_long("KMH_FASTA_PROF", 0) != 0;   // phase times on stderr
+    auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = prof ? now() : 0.0;
+    std::unique_ptr<uint8_t[], kmh_fasta::Free> whole;
+    std::vector<uint8_t> more;
+    size_t n = 0;
     try {
+        long sz = -1;
         if (fseek(fp, 0, SEEK_END) == 0) {
-            const long sz = ftell(fp);
-            if (sz > 0) buf.reserve((size_t)sz);
+            sz = ftell(fp);
             fseek(fp, 0, SEEK_SET);
+        }
+        if (sz > 0) {
+            whole.reset(alloc_bytes((size_t)sz));
+            const int fd = fileno(fp);
+            const size_t blk = std::max<size_t>(1u << 22, ((size_t)sz + max_threads - 1) / max_threads);
+            const size_t nblk = ((size_t)sz + blk - 1) / blk;
+            std::vector<size_t> got(nblk, 0);
+            run_pool(nblk, max_threads, [&](size_t b) {
+                const size_t a0 = b * blk, e = std::min((size_t)sz, a0 + blk);
+                size_t q = a0;
+                while (q < e) {
+                    const ssize_t r = pread(fd, whole.get() + q, e - q, (off_t)q);
+                    if (r <= 0) break;
+                    q += (size_t)r;
+                }
+                got[b] = q - a0;
+            });
+            bool full = true;
+            for (size_t b = 0; b < nblk; ++b) full = full && got[b] == std::min((size_t)sz, (b + 1) * blk) - b * blk;
+            n = full ? (size_t)sz : 0;   // a short read: read the whole file sequentially below
+            if (fseek(fp, (long)n, SEEK_SET) != 0) n = 0;
         }
         uint8_t chunk[1 << 16];
         size_t got;
-        while ((got = fread(chunk, 1, sizeof chunk, fp)) > 0) buf.insert(buf.end(), chunk, chunk + got);
+        while ((got = fread(chunk, 1, sizeof chunk, fp)) > 0) more.insert(more.end(), chunk, chunk + got);
+        if (!more.empty() && n) more.insert(more.begin(), whole.get(), whole.get() + n);
     } catch (const std::bad_alloc&) {
         fclose(fp);
         kmh::set_thread_error("out of host memory reading FASTA");
@@ -134,61 +319,44 @@ int kmh_fasta_read(const char* path, kmh_fasta** out) {
         kmh::set_thread_error(std::string("read error on ") + path);
         return KMH_ERR_IO;
     }
+    if (!more.empty()) {   // the parse works in place: the bytes go to one owned buffer
+        n = more.size();
+        whole.reset(alloc_bytes(n));
+        memcpy(whole.get(), more.data(), n);
+        more = std::vector<uint8_t>();
+    }
+    if (!whole) whole.reset(alloc_bytes(1));   // an empty file: records point into a valid buffer
+    uint8_t* p = whole.get();
 
     std::unique_ptr<kmh_fasta> f(new (std::nothrow) kmh_fasta);
     if (!f) return KMH_ERR_NOMEM;
     try {
-        f->seqs.reserve(buf.size());
-        const uint8_t* p = buf.data();
-        const size_t n = buf.size();
-        size_t i = 0;
-        bool in_record = false;
-        kmh_fasta::Rec cur{};
-        auto close_record = [&]() {
-            cur.seq_len = f->seqs.size() - cur.seq_off;
-            // characters = bytes that are not UTF-8 continuation bytes (a vectorised count)
-            const uint8_t* sp = f->seqs.data() + cur.seq_off;
-            uint64_t cont = 0;
-            for (uint64_t q = 0, e = cur.seq_len; q < e; ++q) cont += (sp[q] & 0xC0u) == 0x80u;
-            cur.char_len = cur.seq_len - cont;
-            f->recs.push_back(cur);
-        };
-        while (i < n) {
-            // line end: the first '\n' or '\r' (memchr: vectorised scans of ~80-byte lines)
-            const void* nl = memchr(p + i, '\n', n - i);
-            size_t j = nl ? (size_t)(static_cast<const uint8_t*>(nl) - p) : n;
-            if (const void* cr = memchr(p + i, '\r', j - i)) j = (size_t)(static_cast<const uint8_t*>(cr) - p);
-            const uint8_t* line = p + i;
-            const size_t len = j - i;
-            // advance past the line terminator (\r\n counts once)
-            if (j < n && p[j] == '\r' && j + 1 < n && p[j + 1] == '\n') i = j + 2;
-            else i = j + 1;
-            if (len > 0 && line[0] == '>') {
-                if (in_record) close_record();
-                in_record = true;
-                const size_t tl = rstrip_len(line + 1, len - 1);
-                const uint8_t* t = line + 1;
-                size_t a = 0;
-                for (size_t w; a < tl && (w = leading_space(t + a, tl - a)) != 0;) a += w;
-                size_t b = a;
-                while (b < tl && leading_space(t + b, tl - b) == 0) ++b;
-                cur = kmh_fasta::Rec{};
-                cur.id_off = f->ids.size();
-                cur.id_len = b - a;
-                f->ids.append(reinterpret_cast<const char*>(t + a), b - a);
-                cur.seq_off = f->seqs.size();
-                continue;
+        // Pieces of max(4 MiB, n / threads) bytes (KMH_FASTA_CHUNK overrides: tests use tiny pieces), each
+        // ending just after a '\n' -- always a line end, never inside "\r\n" -- parsed on up
+        // to 16 threads, then stitched in order.
+        const long env_chunk = kmh::env_long("KMH_FASTA_CHUNK", 0);
+        const size_t cs = env_chunk > 0 ? (size_t)env_chunk
+                                        : std::max<size_t>(4u << 20, (n + max_threads - 1) / max_threads);
+        std::vector<size_t> cut{0};
+        while (cut.back() < n) {
+            size_t at = cut.back() + cs;
+            if (at >= n) {
+                cut.push_back(n);
+                break;
             }
-            if (!in_record) continue;  // text before the first record
-            const size_t sl = rstrip_len(line, len);
-            if (!memchr(line, ' ', sl)) {
-                f->seqs.insert(f->seqs.end(), line, line + sl);
-            } else {
-                for (size_t q = 0; q < sl; ++q)
-                    if (line[q] != ' ') f->seqs.push_back(line[q]);
-            }
+            const void* nl = memchr(p + at, '\n', n - at);
+            cut.push_back(nl ? (size_t)(static_cast<const uint8_t*>(nl) - p) + 1 : n);
         }
-        if (in_record) close_record();
+        const size_t np = cut.size() - 1;
+        std::vector<Piece> pieces(np);
+        const double t1 = prof ? now() : 0.0;
+        run_pool(np, max_threads, [&](size_t t) { parse_lines(p, cut[t], cut[t + 1], pieces[t]); });
+        const double t2 = prof ? now() : 0.0;
+        stitch(pieces, cut, p, *f);
+        f->seqs = std::move(whole);
+        if (prof)
+            fprintf(stderr, "kmh_fasta_read: read %.4f s, parse %.4f s (%zu pieces), stitch %.4f s\n", t1 - t0,
+                    t2 - t1, np, now() - t2);
     } catch (const std::bad_alloc&) {
         kmh::set_thread_error("out of host memory parsing FASTA");
         return KMH_ERR_NOMEM;
@@ -208,7 +376,7 @@ int kmh_fasta_record(const kmh_fasta* f, uint64_t i, const char** id, uint64_t* 
     const kmh_fasta::Rec& r = f->recs[i];
     if (id) *id = f->ids.data() + r.id_off;
     if (id_len) *id_len = r.id_len;
-    if (seq) *seq = f->seqs.data() + r.seq_off;
+    if (seq) *seq = f->seqs.get() + r.seq_off;
     if (seq_len) *seq_len = r.seq_len;
     if (char_len) *char_len = r.char_len;
     return KMH_OK;
@@ -235,7 +403,7 @@ int kmh_fasta_pack(const kmh_fasta* f, uint64_t min_len, uint8_t* out, uint64_t 
     uint8_t* o = out;
     for (const auto& r : f->recs) {
         if (r.char_len < min_len) continue;
-        memcpy(o, f->seqs.data() + r.seq_off, r.seq_len);
+        memcpy(o, f->seqs.get() + r.seq_off, r.seq_len);
         o += r.seq_len;
         *o++ = '\n';
     }

@@ -1,5 +1,6 @@
 """CPU: the C-ABI library loads, exports every declared symbol, and its host-side pieces
 (FASTA ingest, text formatter, error reporting) match the oracle.  No GPU needed."""
+import contextlib
 import os
 import re
 
@@ -53,12 +54,32 @@ def _native_records(path):
     return out
 
 
-def test_fasta_parser_matches_oracle_on_golden_inputs(golden_dir):
+@contextlib.contextmanager
+def _fasta_chunk(nbytes):
+    """Parse with pieces of `nbytes` (KMH_FASTA_CHUNK): tiny pieces put piece boundaries at
+    nearly every line of a small input, so the threaded parse and the stitching are tested."""
+    old = os.environ.get("KMH_FASTA_CHUNK")
+    if nbytes is None:
+        os.environ.pop("KMH_FASTA_CHUNK", None)
+    else:
+        os.environ["KMH_FASTA_CHUNK"] = str(nbytes)
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("KMH_FASTA_CHUNK", None)
+        else:
+            os.environ["KMH_FASTA_CHUNK"] = old
+
+
+@pytest.mark.parametrize("chunk", [None, 1, 7, 64])
+def test_fasta_parser_matches_oracle_on_golden_inputs(golden_dir, chunk):
     inputs = os.path.join(golden_dir, "inputs")
     for name in sorted(os.listdir(inputs)):
         path = os.path.join(inputs, name)
         ref = ofasta.parse_fasta(path)
-        got = _native_records(path)
+        with _fasta_chunk(chunk):
+            got = _native_records(path)
         assert [r[0] for r in got] == [r[0] for r in ref], name
         assert [r[1].decode() for r in got] == [r[2] for r in ref], name
         assert [r[2] for r in got] == [len(r[2]) for r in ref], name
@@ -72,13 +93,14 @@ def test_fasta_missing_file_raises_oserror(tmp_path):
 _alphabet = st.sampled_from(list("ACGTacgtNnRY \t\r\n>;-*xé") + [" ", " ", "　"])
 
 
-@settings(max_examples=200, deadline=None)
-@given(st.lists(_alphabet, max_size=300).map("".join))
-def test_fasta_parser_property(tmp_path_factory, text):
+@settings(max_examples=300, deadline=None)
+@given(st.lists(_alphabet, max_size=300).map("".join), st.sampled_from([None, 1, 5, 16]))
+def test_fasta_parser_property(tmp_path_factory, text, chunk):
     path = tmp_path_factory.mktemp("fa") / "x.fa"
     path.write_bytes(text.encode("utf-8"))
     ref = ofasta.parse_fasta(path)
-    got = _native_records(path)
+    with _fasta_chunk(chunk):
+        got = _native_records(path)
     assert [(r[0], r[2]) for r in ref] == [(g[0], g[1].decode("utf-8")) for g in got]
     assert [len(r[2]) for r in ref] == [g[2] for g in got]
 
