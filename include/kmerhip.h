@@ -108,6 +108,10 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
 uint64_t kmh_kmers_size(const kmh_kmers* r);
 /* Copy the result out; any pointer may be NULL.  codes/counts/first: size() entries. */
 int kmh_kmers_export(const kmh_kmers* r, uint64_t* codes, uint32_t* counts, uint64_t* first);
+/* Borrow the result arrays without a copy (valid until kmh_kmers_free); any pointer may be
+ * NULL.  The Python mirror wraps them as numpy views that keep the result alive. */
+int kmh_kmers_data(const kmh_kmers* r, const uint64_t** codes, const uint32_t** counts,
+                   const uint64_t** first);
 void kmh_kmers_free(kmh_kmers* r);
 
 /* Dense 4^k count vector of one host sequence (1 <= k <= 12), counts[4^k]

@@ -368,6 +368,15 @@ int kmh_kmers_export(const kmh_kmers* r, uint64_t* codes, uint32_t* counts, uint
     return KMH_OK;
 }
 
+int kmh_kmers_data(const kmh_kmers* r, const uint64_t** codes, const uint32_t** counts,
+                   const uint64_t** first) {
+    if (!r) return KMH_ERR_INVALID;
+    if (codes) *codes = r->codes.data();
+    if (counts) *counts = r->counts.data();
+    if (first) *first = r->first.data();
+    return KMH_OK;
+}
+
 void kmh_kmers_free(kmh_kmers* r) { delete r; }
 
 }  // extern "C"

@@ -221,14 +221,23 @@ int dense_order(Ctx* ctx, const uint32_t* d_counts, const uint32_t* d_first, siz
     KMH_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(tmp, t, keys, keys2, sel, vals2, (int)m, 0, bits, s));
     hipLaunchKernelGGL(k_gather_counts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, vals2, d_counts, m, cnt2);
     KMH_HIP(ctx, hipGetLastError());
-    std::vector<uint32_t> c32(m), f32(m);
+    // The u32 codes and first starts land in the upper half of their u64 arrays and are
+    // widened in place, front to back (element i's 8 bytes end at or before the 4-byte
+    // source of element i + 1), so no u32 staging arrays are allocated.
+    codes.resize(m);
+    first.resize(m);
     counts.resize(m);
-    KMH_HIP(ctx, hipMemcpyAsync(c32.data(), vals2, m * 4, hipMemcpyDeviceToHost, s));
-    KMH_HIP(ctx, hipMemcpyAsync(f32.data(), keys2, m * 4, hipMemcpyDeviceToHost, s));
+    uint32_t* c32 = reinterpret_cast<uint32_t*>(codes.data()) + m;
+    uint32_t* f32 = reinterpret_cast<uint32_t*>(first.data()) + m;
+    KMH_HIP(ctx, hipMemcpyAsync(c32, vals2, m * 4, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipMemcpyAsync(f32, keys2, m * 4, hipMemcpyDeviceToHost, s));
     KMH_HIP(ctx, hipMemcpyAsync(counts.data(), cnt2, m * 4, hipMemcpyDeviceToHost, s));
     KMH_HIP(ctx, hipStreamSynchronize(s));
-    codes.assign(c32.begin(), c32.end());
-    first.assign(f32.begin(), f32.end());
+    for (uint64_t i = 0; i < m; ++i) {
+        const uint32_t c = c32[i], f = f32[i];
+        codes[i] = c;
+        first[i] = f;
+    }
     return KMH_OK;
 }
 

@@ -43,6 +43,7 @@ SIGNATURES = [
     ("kmh_count_host", _c.c_int, [_vp, _vp, _u64, _c.c_int, _c.c_int, _c.POINTER(_vp)]),
     ("kmh_kmers_size", _u64, [_vp]),
     ("kmh_kmers_export", _c.c_int, [_vp, _vp, _vp, _vp]),
+    ("kmh_kmers_data", _c.c_int, [_vp, _vp, _vp, _vp]),
     ("kmh_kmers_free", None, [_vp]),
     ("kmh_count_dense_host", _c.c_int, [_vp, _vp, _u64, _c.c_int, _vp]),
     ("kmh_count_dense_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp]),
@@ -147,15 +148,15 @@ class Context:
         r = ctypes.c_void_p()
         _check(lib().kmh_count_host(self._h, _ptr(buf), buf.size, int(k), int(bool(canonical)),
                                     ctypes.byref(r)), self._h)
-        try:
-            n = lib().kmh_kmers_size(r)
-            codes = np.empty(n, np.uint64)
-            counts = np.empty(n, np.uint32)
-            first = np.empty(n, np.uint64)
-            _check(lib().kmh_kmers_export(r, _ptr(codes), _ptr(counts), _ptr(first)))
-        finally:
-            lib().kmh_kmers_free(r)
-        return codes, counts, first
+        # numpy views of the result's own arrays (no copy); they keep it alive
+        owner = _Kmers(r)
+        n = lib().kmh_kmers_size(r)
+        if n == 0:
+            return np.empty(0, np.uint64), np.empty(0, np.uint32), np.empty(0, np.uint64)
+        pc, pn, pf = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _check(lib().kmh_kmers_data(r, ctypes.byref(pc), ctypes.byref(pn), ctypes.byref(pf)))
+        return (owner.view(pc, n, ctypes.c_uint64), owner.view(pn, n, ctypes.c_uint32),
+                owner.view(pf, n, ctypes.c_uint64))
 
     def count_dense(self, seq, k):
         buf = _as_u8(seq)
@@ -247,6 +248,24 @@ def _as_u8(seq):
     return np.frombuffer(bytes(seq), dtype=np.uint8)
 
 
+class _Kmers:
+    """Owns a kmh_kmers result; numpy views of its arrays keep it alive through their base
+    (a ctypes array over the C memory that holds a reference to this object)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def view(self, ptr, n, ctype):
+        buf = (ctype * n).from_address(ptr.value)
+        buf._owner = self
+        return np.frombuffer(buf, dtype=np.dtype(ctype))
+
+    def __del__(self):
+        if self._h:
+            lib().kmh_kmers_free(self._h)
+            self._h = None
+
+
 class FastaFile:
     """Records of a FASTA file parsed by kmh_fasta_read (generate.py:39-41 semantics)."""
 
@@ -302,15 +321,21 @@ def write_file(path, data, gzip_level=-1, threads=0):
     _check(lib().kmh_write_file(os.fsencode(str(path)), _ptr(buf), len(data), int(gzip_level), int(threads)))
 
 
-def format_lines(k, codes, counts):
-    """k{k}.txt bytes for (codes, counts) -- generate.py:86-91 text."""
+def format_lines_array(k, codes, counts):
+    """k{k}.txt text for (codes, counts) -- generate.py:86-91 -- as a uint8 array (written
+    in place: no zero-filled staging buffer, no copy into a bytes object)."""
     codes = np.ascontiguousarray(codes, dtype=np.uint64)
     counts = np.ascontiguousarray(counts, dtype=np.uint64)
     n = codes.size
     need = _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, None, 0))
-    out = ctypes.create_string_buffer(max(need, 1))
-    _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, out, need))
-    return out.raw[:need]
+    out = np.empty(max(need, 1), np.uint8)
+    _check(lib().kmh_format_lines(int(k), _ptr(codes), _ptr(counts), n, _ptr(out), need))
+    return out[:need]
+
+
+def format_lines(k, codes, counts):
+    """k{k}.txt bytes for (codes, counts) -- generate.py:86-91 text."""
+    return format_lines_array(k, codes, counts).tobytes()
 
 
 def format_lines_seq(k, seq, first, counts):

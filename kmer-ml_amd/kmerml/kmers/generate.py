@@ -77,7 +77,7 @@ class KmerExtractor:
         for k in k_order:
             codes, counts, first = results.get(k, (np.empty(0, np.uint64), np.empty(0, np.uint32),
                                                    np.empty(0, np.uint64)))
-            counts = counts.astype(np.uint64) * np.uint64(multiplicity[k])
+            counts = np.multiply(counts, np.uint64(multiplicity[k]), dtype=np.uint64)
             if k > 32:   # a code holds 32 bases: the line digits come from the sequence
                 self._write_bytes(self._kmer_path(organism_id, k),
                                   _native.format_lines_seq(k, packed, first, counts))
@@ -94,7 +94,7 @@ class KmerExtractor:
         _native.write_file(path, data, gzip_level=9 if self.compress else -1)
 
     def _write_kmer_file(self, organism_id, k, codes, counts):
-        self._write_bytes(self._kmer_path(organism_id, k), _native.format_lines(k, codes, counts))
+        self._write_bytes(self._kmer_path(organism_id, k), _native.format_lines_array(k, codes, counts))
 
     # generate.py:68-91 -- kept for callers that hand in a {kmer: count} dict.
     def _save_kmers_to_file(self, kmers, organism_id, k):
