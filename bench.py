@@ -60,6 +60,8 @@ def parse():
                         "the u32 rows after each count")
     p.add_argument("--cpu-sample", type=int, default=16_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
+    p.add_argument("--kernel-events", choices=["roofline", "all"], default="roofline",
+                   help="HIP event pairs around the kernels the roofline names only (default), or all")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="experiments: no per-kernel HIP events in the timed region (roofline = null)")
     p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
@@ -299,6 +301,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if a.kernel_events == "roofline":   # an event pair costs a few us of stream time per launch
+        os.environ["KMH_TIMING_ONLY"] = "k_partition,k_bucket_count,k_direct"
     ctx.timing(not a.no_kernel_events)
     t0 = time.perf_counter()
     for i in range(a.steps):

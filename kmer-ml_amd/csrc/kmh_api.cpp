@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <new>
@@ -85,13 +86,18 @@ static hipEvent_t take_event(Ctx* ctx) {
 
 void time_begin(Ctx* ctx, hipStream_t s, const char* name) {
     if (!ctx->timing) return;
+    // KMH_TIMING_ONLY=name,name: event pairs only around those kernels (each pair costs a few
+    // microseconds of stream time; the bench times only the kernels its roofline names)
+    ctx->timing_skip = !ctx->timing_only.empty() &&
+                       ctx->timing_only.find("," + std::string(name) + ",") == std::string::npos;
+    if (ctx->timing_skip) return;
     TimedLaunch t{name, take_event(ctx), take_event(ctx)};
     if (t.start) (void)hipEventRecord(t.start, s);
     ctx->launches.push_back(t);
 }
 
 void time_end(Ctx* ctx, hipStream_t s) {
-    if (!ctx->timing || ctx->launches.empty()) return;
+    if (!ctx->timing || ctx->timing_skip || ctx->launches.empty()) return;
     TimedLaunch& t = ctx->launches.back();
     if (t.stop) (void)hipEventRecord(t.stop, s);
 }
@@ -165,6 +171,9 @@ const char* kmh_last_error(const kmh_ctx* ctx) {
 int kmh_timing_enable(kmh_ctx* ctx, int enable) {
     if (!ctx) return KMH_ERR_INVALID;
     ctx->timing = enable != 0;
+    ctx->timing_skip = false;
+    const char* only = std::getenv("KMH_TIMING_ONLY");
+    ctx->timing_only = (only && *only) ? "," + std::string(only) + "," : std::string();
     for (auto& t : ctx->launches) {
         if (t.start) ctx->event_pool.push_back(t.start);
         if (t.stop) ctx->event_pool.push_back(t.stop);

@@ -48,6 +48,8 @@ struct Ctx {
     hipEvent_t pinned_ready = nullptr;
     // per-kernel timing
     bool timing = false;
+    bool timing_skip = false;        // the launch in flight is not timed (KMH_TIMING_ONLY)
+    std::string timing_only;         // ",name,name," -- empty: time every launch
     std::vector<TimedLaunch> launches;
     std::vector<hipEvent_t> event_pool;
     std::vector<std::string> report_names;
