@@ -326,7 +326,11 @@ def main():
     last = locals_[(a.steps - 1) % len(locals_)]
     if mode in ("u4", "u8"):
         full = fulls[(a.steps - 1) % 2]
-    rows = full[:G] if (assemble and G % world == 0) else last[:g_local]
+    if assemble:   # every rank's block of the assembled matrix (blocks padded to B rows)
+        idx = [q * B + i for q in range(world) for i in range((G * (q + 1)) // world - (G * q) // world)]
+        rows = full[torch.tensor(idx, dtype=torch.long, device=full.device)]
+    else:
+        rows = last[:g_local]
     ok = bool(torch.all(rows.sum(1, dtype=torch.int64) == max(L - k + 1, 0)).item())
     if mode == "u32":   # this rank's block of the assembled matrix is bit-identical to its own count
         ok = ok and bool(torch.equal(full[rank * B:rank * B + g_local], last[:g_local]))
