@@ -209,3 +209,25 @@ def test_format_lines_many_blocks_and_partial_buffer():
     assert total == len(text)
     cut = text[:cap].rfind(b"\n") + 1
     assert buf.raw[:cut] == text[:cut]
+
+
+def test_fasta_parser_multi_piece_natural(tmp_path):
+    """A 12.16 Mbp, 17-record file (the config-1 stand-in, 80-column lines, CRLF on every other
+    record) parsed with the default piece size (4 MiB, so pieces cut records mid-sequence):
+    same records, bytes and character counts as the restated parser."""
+    from oracle import synth as osynth
+    recs = osynth.yeast_standin_records()
+    path = tmp_path / "y.fa"
+    osynth.write_fasta(path, recs)
+    raw = path.read_bytes()
+    # CRLF line ends in the odd records: the piece cuts (after a '\n') must never split "\r\n"
+    parts = raw.split(b">")
+    raw = b">".join(p.replace(b"\n", b"\r\n") if i % 2 else p for i, p in enumerate(parts))
+    path.write_bytes(raw)
+    ref = ofasta.parse_fasta(path)
+    with _fasta_chunk(None):
+        got = _native_records(path)
+    assert [g[0] for g in got] == [r[0] for r in ref]
+    assert all(g[1] == r[2].encode() for g, r in zip(got, ref))
+    assert [g[2] for g in got] == [len(r[2]) for r in ref]
+    assert len(raw) > 2 * (4 << 20)   # three pieces at the default size
