@@ -622,6 +622,20 @@ def test_count_genome_split(tmp_path, oracle_lib, backend, nproc):
         assert np.array_equal(got, want)
 
 
+def test_count_result_views_outlive_other_views(ctx):
+    """ctx.count returns numpy views of the C result (kmh_kmers_data, no copy): one view stays
+    valid after the others are dropped, the garbage collector runs and host memory is reused."""
+    import gc
+    seq = osynth.synth_bases(2_000_000, osynth.genome_seed(3)).tobytes()
+    codes, counts, first = ctx.count(seq, 12)
+    n = codes.size
+    del codes, first
+    gc.collect()
+    junk = [np.ones(1 << 20, np.uint64) for _ in range(32)]
+    assert counts.size == n and int(counts.sum(dtype=np.uint64)) == len(seq) - 12 + 1
+    del junk
+
+
 def test_bench_pipelined_u8_assembly_rccl():
     """bench.py's pipelined u8 all-gather path (the N > 1 default) through RCCL, one rank."""
     r = _torchrun(["bench.py", "--assemble", "u8", "--genomes", "3", "--genome-len", "3000000",
