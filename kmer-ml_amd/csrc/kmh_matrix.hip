@@ -117,6 +117,94 @@ __global__ __launch_bounds__(256) void k_encode_u4(const uint32_t* __restrict__ 
     }
 }
 
+// Wave-coalesced u4 encode: a wave takes 512 consecutive 4-count groups (uint4) per step; lane
+// l takes groups base + 64u + l, u = 0..7, so every load instruction reads 1 KiB contiguous
+// and every store writes 128 B contiguous (group g -> the u16 at index g: the same nibble
+// layout as k_encode_u4).  Escapes are counted per lane, scanned across the wave and appended
+// behind one atomic per wave (a single global counter per lane-escape serialises at L2).
+__global__ __launch_bounds__(256) void k_encode_u4w(const uint32_t* __restrict__ rows, uint64_t n4,
+                                                    uint16_t* __restrict__ out,
+                                                    uint32_t* __restrict__ esc, uint32_t cap,
+                                                    uint32_t* __restrict__ esc_n) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint4* src = reinterpret_cast<const uint4*>(rows);
+    for (uint64_t base = w0 * 512u; base < n4; base += nw * 512u) {
+        uint4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+            v[u] = src[e < n4 ? e : n4 - 1];   // unconditional load (a guarded one drains vmcnt)
+        }
+        uint32_t nesc = 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+            const uint4 a = v[u];
+            if (e < n4) {
+                nesc += (uint32_t)(a.x >= 15u) + (uint32_t)(a.y >= 15u) + (uint32_t)(a.z >= 15u) + (uint32_t)(a.w >= 15u);
+                out[e] = (uint16_t)(sat4(a.x) | (sat4(a.y) << 4) | (sat4(a.z) << 8) | (sat4(a.w) << 12));
+            }
+        }
+        if (__ballot(nesc != 0u)) {   // wave-uniform; rare for uniform genomes
+            uint32_t incl = nesc;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(incl, d);
+                if (lane >= d) incl += t;
+            }
+            uint32_t at0 = 0u;
+            if (lane == 63) at0 = atomicAdd(esc_n, incl);
+            uint32_t at = (uint32_t)__shfl((int)at0, 63) + incl - nesc;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+                const uint32_t c[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (e < n4 && c[j] >= 15u) {
+                        if (at < cap) {
+                            esc[2 * (uint64_t)at] = (uint32_t)(4 * e + (uint64_t)j);
+                            esc[2 * (uint64_t)at + 1] = c[j];
+                        }
+                        ++at;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Wave-coalesced u4 decode: group g (a u16 of four nibbles) -> uint4 g of the rows; lanes take
+// groups base + 64u + l, so loads read 128 B and non-temporal stores write 1 KiB contiguous per
+// instruction.
+__global__ __launch_bounds__(256) void k_decode_u4w(const uint16_t* __restrict__ in, uint64_t n4,
+                                                    uint32_t* __restrict__ rows) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    uint4* dst = reinterpret_cast<uint4*>(rows);
+    for (uint64_t base = w0 * 512u; base < n4; base += nw * 512u) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+            x[u] = in[e < n4 ? e : n4 - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+            if (e < n4) store_nt(&dst[e], make_uint4(x[u] & 15u, (x[u] >> 4) & 15u, (x[u] >> 8) & 15u, x[u] >> 12));
+        }
+    }
+}
+
+unsigned grid_waves(uint64_t n4) {   // 256-thread blocks, one 512-group step per wave at least
+    const uint64_t b = (n4 + 2047) / 2048;
+    return (unsigned)(b < 4096 ? (b ? b : 1) : 4096);
+}
+
 __global__ __launch_bounds__(256) void k_decode_u4(const uint8_t* __restrict__ in, uint64_t n32,
                                                    uint32_t* __restrict__ rows) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n32;
@@ -201,7 +289,11 @@ int rows_encode_u4(Ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t col
     const uint64_t n32 = rows * cols / 32;
     if (n32 == 0) return KMH_OK;
     time_begin(ctx, s, "k_encode_u4");
-    hipLaunchKernelGGL(k_encode_u4, dim3(grid_for(n32)), dim3(256), 0, s, d_rows, n32, d_u4, d_esc, cap, d_esc_n);
+    if (env_long("KMH_U4_OLD", 0))   // the per-thread-contiguous kernel (A/B only)
+        hipLaunchKernelGGL(k_encode_u4, dim3(grid_for(n32)), dim3(256), 0, s, d_rows, n32, d_u4, d_esc, cap, d_esc_n);
+    else
+        hipLaunchKernelGGL(k_encode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s, d_rows, 8 * n32,
+                           reinterpret_cast<uint16_t*>(d_u4), d_esc, cap, d_esc_n);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     return KMH_OK;
@@ -215,7 +307,11 @@ int rows_decode_u4(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, 
     const uint64_t n32 = rows * cols / 32;
     if (n32 == 0) return KMH_OK;
     time_begin(ctx, s, "k_decode_u4");
-    hipLaunchKernelGGL(k_decode_u4, dim3(grid_for(n32)), dim3(256), 0, s, d_u4, n32, d_rows);
+    if (env_long("KMH_U4_OLD", 0))
+        hipLaunchKernelGGL(k_decode_u4, dim3(grid_for(n32)), dim3(256), 0, s, d_u4, n32, d_rows);
+    else
+        hipLaunchKernelGGL(k_decode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s,
+                           reinterpret_cast<const uint16_t*>(d_u4), 8 * n32, d_rows);  // 8 four-count groups per 32 counts
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (cap > 0) {
