@@ -126,7 +126,34 @@ __global__ __launch_bounds__(256) void k_encode_u4w(const uint32_t* __restrict__
                                                     uint16_t* __restrict__ out,
                                                     uint32_t* __restrict__ esc, uint32_t cap,
                                                     uint32_t* __restrict__ esc_n) {
-    const int lane = threadIdx.x & 63;
+    // Per-wave escape staging in LDS: a wave appends its (index, value) pairs here and moves
+    // them to the global list behind ONE atomic per kStage entries (uniform genomes: ~3
+    // escapes per 512-group step, so ~one global atomic per 170 steps instead of one per
+    // step -- a single counter that every wave hits serialises at one L2 channel).
+    constexpr uint32_t kStage = 512;
+    __shared__ uint32_t stage[4][2 * kStage];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* st = stage[wave];
+    uint32_t held = 0u;   // wave-uniform
+    auto sync_wave = []() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto flush = [&]() {
+        sync_wave();
+        uint32_t at0 = 0u;
+        if (lane == 0) at0 = atomicAdd(esc_n, held);
+        at0 = (uint32_t)__shfl((int)at0, 0);
+        for (uint32_t i = (uint32_t)lane; i < held; i += 64u) {
+            if (at0 + i < cap) {
+                esc[2 * (uint64_t)(at0 + i)] = st[2 * i];
+                esc[2 * (uint64_t)(at0 + i) + 1] = st[2 * i + 1];
+            }
+        }
+        sync_wave();
+        held = 0u;
+    };
     const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint4* src = reinterpret_cast<const uint4*>(rows);
@@ -154,9 +181,17 @@ __global__ __launch_bounds__(256) void k_encode_u4w(const uint32_t* __restrict__
                 const uint32_t t = __shfl_up(incl, d);
                 if (lane >= d) incl += t;
             }
-            uint32_t at0 = 0u;
-            if (lane == 63) at0 = atomicAdd(esc_n, incl);
-            uint32_t at = (uint32_t)__shfl((int)at0, 63) + incl - nesc;
+            const uint32_t tot = (uint32_t)__shfl((int)incl, 63);
+            if (held + tot > kStage) flush();
+            const bool direct = tot > kStage;   // a step of mostly escapes: straight to global
+            uint32_t at;
+            if (direct) {
+                uint32_t at0 = 0u;
+                if (lane == 63) at0 = atomicAdd(esc_n, incl);
+                at = (uint32_t)__shfl((int)at0, 63) + incl - nesc;
+            } else {
+                at = held + incl - nesc;
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
@@ -164,16 +199,24 @@ __global__ __launch_bounds__(256) void k_encode_u4w(const uint32_t* __restrict__
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     if (e < n4 && c[j] >= 15u) {
-                        if (at < cap) {
-                            esc[2 * (uint64_t)at] = (uint32_t)(4 * e + (uint64_t)j);
-                            esc[2 * (uint64_t)at + 1] = c[j];
+                        const uint32_t idx = (uint32_t)(4 * e + (uint64_t)j);
+                        if (direct) {
+                            if (at < cap) {
+                                esc[2 * (uint64_t)at] = idx;
+                                esc[2 * (uint64_t)at + 1] = c[j];
+                            }
+                        } else {
+                            st[2 * at] = idx;
+                            st[2 * at + 1] = c[j];
                         }
                         ++at;
                     }
                 }
             }
+            if (!direct) held += tot;
         }
     }
+    if (held) flush();
 }
 
 // Wave-coalesced u4 decode: group g (a u16 of four nibbles) -> uint4 g of the rows; lanes take
