@@ -4,6 +4,8 @@
 // and the blocks travel over xGMI.  Rows are sent as saturating u8 (values >= 255 stored as
 // 255) plus an exact escape list (row, column, value) of every value >= 255, and widened
 // back to u32 after the all-gather: 4x fewer bytes on the links for the same matrix.
+#include <algorithm>
+
 #include "kmh_device.h"
 
 namespace kmh {
@@ -77,6 +79,30 @@ __global__ __launch_bounds__(256) void k_apply_escapes(const uint32_t* __restric
 // ---- u4: two counts per byte (element 2i in the low nibble of byte i), values >= 15 stored
 // as 15 with an exact (index, value) escape.  Uniform 100 Mbp genomes at k = 12 average ~6
 // per bin, so ~0.14 % of the cells escape; 8x fewer bytes than u32 rows on the links.
+// Wave-coalesced u8 decode: group g (a u32 of four counts) -> uint4 g of the rows; lanes take
+// groups base + 64u + l, so every instruction covers contiguous bytes (256 B loads, 1 KiB
+// non-temporal stores).
+__global__ __launch_bounds__(256) void k_decode_u8w(const uint32_t* __restrict__ in, uint64_t n4,
+                                                    uint32_t* __restrict__ rows) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    uint4* dst = reinterpret_cast<uint4*>(rows);
+    for (uint64_t base = w0 * 512u; base < n4; base += nw * 512u) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+            x[u] = in[e < n4 ? e : n4 - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t e = base + 64u * (uint64_t)u + (uint64_t)lane;
+            if (e < n4) store_nt(&dst[e], make_uint4(x[u] & 0xFFu, (x[u] >> 8) & 0xFFu, (x[u] >> 16) & 0xFFu, x[u] >> 24));
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t sat4(uint32_t x) { return x < 15u ? x : 15u; }
 
 // 32 elements per thread per step: eight 16-byte loads, one 16-byte store.
@@ -307,7 +333,11 @@ int rows_decode_u8(Ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
     const uint64_t n16 = rows * cols / 16;
     if (n16) {
         time_begin(ctx, s, "k_decode_u8");
-        hipLaunchKernelGGL(k_decode_u8, dim3(grid_for(n16)), dim3(256), 0, s, d_u8, n16, d_rows);
+        if (env_long("KMH_U4_OLD", 0))   // the per-thread-contiguous kernel (A/B only)
+            hipLaunchKernelGGL(k_decode_u8, dim3(grid_for(n16)), dim3(256), 0, s, d_u8, n16, d_rows);
+        else
+            hipLaunchKernelGGL(k_decode_u8w, dim3((unsigned)std::min<uint64_t>(4096, (4 * n16 + 2047) / 2048)), dim3(256), 0, s,
+                               reinterpret_cast<const uint32_t*>(d_u8), 4 * n16, d_rows);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
     }

@@ -1,4 +1,4 @@
-"""u4 + escape row encode / decode throughput (the multi-GPU assembly kernels):
+"""u4 / u8 + escape row encode / decode throughput (the multi-GPU assembly kernels):
 8 count rows of synthetic 100 Mbp genomes at k = 12 (a rank's block at N = 8), round trip
 checked, HIP events on the launch stream; KMH_U4_OLD=1 selects the per-thread-contiguous
 kernels for the A/B.
@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from kmerml import _native  # noqa: E402
-from kmerml.kmers.matrix import slot_layout_u4  # noqa: E402
+from kmerml.kmers.matrix import slot_layout, slot_layout_u4  # noqa: E402
 
 SEED_BASE = 0x6B6D65724D4C0000
 
@@ -63,6 +63,29 @@ def main():
                           "round_trip_exact": ok, "encode_ms": me, "decode_ms": md,
                           "encode_GBs": cells * 4.5 / me / 1e6, "decode_GBs": cells * 4.5 / md / 1e6}), flush=True)
         back.zero_()
+        # u8 + escapes (the fallback wire format)
+        cap8, P8 = slot_layout(B, cols)
+        slot8 = torch.zeros(P8, dtype=torch.uint8, device=dev)
+        te, td = [], []
+        for it in range(8):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record()
+            ctx.rows_encode_u8(rows.data_ptr(), B, cols, slot8.data_ptr(), slot8[cells + 16:].data_ptr(), cap8,
+                               slot8[cells:].data_ptr(), s)
+            e1.record()
+            ctx.rows_decode_u8(slot8.data_ptr(), B, cols, slot8[cells + 16:].data_ptr(), cap8, slot8[cells:].data_ptr(),
+                               1, B, back.data_ptr(), s)
+            e2.record()
+            torch.cuda.synchronize()
+            if it >= 2:
+                te.append(e0.elapsed_time(e1))
+                td.append(e1.elapsed_time(e2))
+        me, md = float(np.median(te)), float(np.median(td))
+        print(json.dumps({"variant": variant, "wire": "u8", "round_trip_exact": bool(torch.equal(rows, back)),
+                          "encode_ms": me, "decode_ms": md, "encode_GBs": cells * 5 / me / 1e6,
+                          "decode_GBs": cells * 5 / md / 1e6}), flush=True)
+        back.zero_()
+        del slot8
 
 
 if __name__ == "__main__":
