@@ -57,3 +57,10 @@ $(MALLBENCH): tests/native/mall_bench.hip
 	@mkdir -p $(OUTDIR)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 .PHONY: mallbench
+
+FABBENCH := $(OUTDIR)/fabric_bench
+fabbench: $(FABBENCH)
+$(FABBENCH): tests/native/fabric_bench.hip
+	@mkdir -p $(OUTDIR)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+.PHONY: fabbench

@@ -16,8 +16,8 @@ namespace kmh {
 constexpr int kTileThreads = 1024;                     // threads of a tile workgroup
 constexpr int kTileBpt = 32;                           // window starts per thread
 constexpr int kTile = kTileThreads * kTileBpt;         // 32768 window starts per tile
-constexpr int kSubBits = 15;                           // bins owned by one count workgroup
-constexpr int kSubBins = 1 << kSubBits;                // 32768 u32 = 128 KiB of LDS
+constexpr int kSubBits = 15;                           // k_direct: LDS slice of 32768 u32 bins
+constexpr int kSubBins = 1 << kSubBits;                // = 128 KiB of LDS
 constexpr int kCountThreads = 1024;                    // threads of a bucket-count workgroup
 constexpr int kDirectMaxK = 7;                         // k <= 7: whole table in LDS
 

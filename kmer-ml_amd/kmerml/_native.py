@@ -9,7 +9,8 @@ import threading
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkmerhip.so")
+# KMH_LIB_PATH: A/B profiling of another build of the same ABI (profiles/); default: the in-tree build
+LIB_PATH = os.environ.get("KMH_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkmerhip.so")
 
 KMH_OK = 0
 KMH_ERR_INVALID = -1

@@ -22,10 +22,10 @@ __global__ __launch_bounds__(T) void k_lds(uint32_t* out, uint32_t seed) {
         for (int j = 0; j < 16; ++j) {
             uint32_t a;
             if (MODE == 2) a = (threadIdx.x + (uint32_t)(it * 16 + j) * T) & (BINS - 1);           // conflict-free
-            else if (MODE == 4) a = (((r[j] + it * 7919u) >> 5) << 5 | (lane & 31)) & (BINS - 1);  // one bank per lane
+            else if (MODE == 4 || MODE == 11) a = (((r[j] + it * 7919u) >> 5) << 5 | (lane & 31)) & (BINS - 1);  // one bank per lane
             else a = (r[j] + it * 7919u) & (BINS - 1);                                             // random
             if (MODE == 0 || MODE == 2 || MODE == 4) atomicAdd(&tbl[a], 1u);
-            else if (MODE == 1) acc += atomicAdd(&tbl[a], 1u);
+            else if (MODE == 1 || MODE == 11) acc += atomicAdd(&tbl[a], 1u);
             else if (MODE == 3) reinterpret_cast<uint16_t*>(tbl)[a * 2 + (j & 1)] = (uint16_t)it;
             else if (MODE == 5) acc += tbl[a];
             else if (MODE == 6) acc += atomicCAS(&tbl[a], 0u, r[j]);                     // cas b32, mostly fails
@@ -88,5 +88,6 @@ int main() {
     run<8>("ds_cmpst_rtn_b64", nb);
     run<9>("ds_add_u64", nb);
     run<10>("ds_read_b64 random", nb);
+    run<11>("ds_add_rtn bank-per-lane", nb);
     return 0;
 }

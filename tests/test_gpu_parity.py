@@ -89,19 +89,30 @@ def test_dense_low_complexity(ctx, dev, oracle_lib, k):
         assert np.array_equal(rows[g], oracle_lib.count_dense(seq, k)), (k, g)
 
 
-@pytest.mark.parametrize("part", ["0", "1"])
+@pytest.mark.parametrize("k", [10, 12])
+def test_dense_u16_wraps(ctx, dev, oracle_lib, k):
+    """Counts past 65535 in both halves of one packed u16 word of the count table: bins 0
+    (A...A) and 1 (A...AC) each exceed 2^16, so their wraps, the carry of the low half into
+    the high half and the carry out of the word are all corrected; also a bin > 2^17."""
+    genomes = [np.frombuffer(b"A" * 200_000 + b"A" * (k - 1) + b"C" + (b"A" * (k - 1) + b"C") * 70_000, np.uint8).copy(),
+               np.frombuffer(b"A" * 140_000 + b"G" + b"T" * 70_000 + b"N" + b"A" * 66_000, np.uint8).copy()]
+    rows, _, _ = _dense_rows(ctx, dev, genomes, k)
+    for g, seq in enumerate(genomes):
+        want = oracle_lib.count_dense(seq, k)
+        assert want[0] > 65536 and np.array_equal(rows[g], want), (k, g)
+    assert oracle_lib.count_dense(genomes[0], k)[1] > 65536
+
+
 @pytest.mark.parametrize("k", [10, 11, 12])
-def test_dense_partition_many_genomes(ctx, dev, oracle_lib, monkeypatch, part, k):
-    """Both partition kernels (KMH_PART=0: one tile per workgroup, the default; 1: the
-    persistent k_partition_rep experiment) on 120 ragged genomes -- empty ones, one spanning ~60 tiles -- so that
-    a persistent workgroup's run of tiles crosses genome boundaries; then again with one
-    genome per launch (KMH_SUF_BUDGET_MB=1)."""
-    monkeypatch.setenv("KMH_PART", part)
+def test_dense_partition_many_genomes(ctx, dev, oracle_lib, monkeypatch, k):
+    """The partition / count kernels on 120 ragged genomes -- empty ones, one spanning ~120
+    tiles, one of exactly one tile of windows -- in one batch; then again with one genome per
+    batch (KMH_SUF_BUDGET_MB=1)."""
     rng = np.random.default_rng(7000 + k)
     lens = rng.integers(0, 90_000, 120)
     lens[::29] = 0
     lens[7] = 2_000_003
-    lens[8] = 32_768 + k - 1          # exactly one full tile of windows
+    lens[8] = 16_384 + k - 1          # exactly one full tile of windows
     genomes = [_rand_seq(rng, int(n)) for n in lens]
     want = [oracle_lib.count_dense(seq, k) for seq in genomes]
     rows, _, _ = _dense_rows(ctx, dev, genomes, k)
@@ -113,13 +124,10 @@ def test_dense_partition_many_genomes(ctx, dev, oracle_lib, monkeypatch, part, k
         assert np.array_equal(rows[g], want[g]), (k, g, "batched")
 
 
-@pytest.mark.parametrize("part", ["0", "1"])
 @pytest.mark.parametrize("k", [11, 12])
-def test_dense_partition_long_runs_large_offsets(ctx, dev, oracle_lib, monkeypatch, part, k):
-    """Every persistent partition workgroup walks several tiles that cross genome
-    boundaries, and the genomes lie past byte 2^31 of the buffer (a 2.2 GB genome of 'N'
-    -- tiles but no valid window -- comes first): 40 ragged genomes, ~40 Mbp."""
-    monkeypatch.setenv("KMH_PART", part)
+def test_dense_partition_long_runs_large_offsets(ctx, dev, oracle_lib, k):
+    """The genomes lie past byte 2^31 of the buffer (a 2.2 GB genome of 'N' -- tiles but no
+    valid window -- comes first): 40 ragged genomes, ~40 Mbp."""
     rng = np.random.default_rng(900 + k)
     lens = rng.integers(0, 2_000_000, 40)
     lens[3] = 0
