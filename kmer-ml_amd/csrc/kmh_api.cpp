@@ -157,9 +157,6 @@ void kmh_ctx_destroy(kmh_ctx* ctx) {
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
-    for (auto e : ctx->pipe_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -383,7 +383,7 @@ struct FixLog {
     uint32_t cap;
 };
 
-__device__ __noinline__ void log_wrap(const FixLog& L, uint64_t row0, uint32_t v, uint32_t old) {
+__device__ __forceinline__ void log_wrap(const FixLog& L, uint64_t row0, uint32_t v, uint32_t old) {
     auto put = [&](uint64_t idx, uint32_t minus_one) {
         const uint32_t at = atomicAdd(L.cursor, 1u);
         if (at < L.cap) L.entries[at] = (idx << 1) | minus_one;
@@ -396,29 +396,32 @@ __device__ __noinline__ void log_wrap(const FixLog& L, uint64_t row0, uint32_t v
 }
 
 // The first nv entries of one 16-byte chunk (8 suffixes) into the table; the other slots add 0
-// (branch-free).  The eight returning adds go out back to back; a wrap shows as bit 16 of
-// (old half + added) and is checked once per chunk.
+// (branch-free).  The eight returning adds go out back to back; a wrap (an added-to half that
+// held 0xFFFF) is looked for once per chunk through the maximum of the returned halves (an
+// add-0 slot at 0xFFFF is a false alarm that the rare path sorts out).
 __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv, const FixLog& L,
                                             uint64_t row0) {
     const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
-    uint32_t old[8];
-    uint32_t acc = 0u;
+    uint32_t old[8], off[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint32_t v = (wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        const uint32_t w = wd[i >> 1];
+        // entry v = the low / high half of w: word (v >> 1) * 4 bytes, half (v & 1) * 16 bits
+        const uint32_t addr = (i & 1) ? (w >> 15) & 0x1FFFCu : (w << 1) & 0x1FFFCu;
+        off[i] = (i & 1) ? (w >> 12) & 16u : (w << 4) & 16u;
         const uint32_t add = (uint32_t)i < nv ? 1u : 0u;
-        old[i] = atomicAdd(&tbl[v >> 1], add << ((v & 1u) << 4));
+        old[i] = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tbl) + addr),
+                                        add << off[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    uint32_t mx = 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t v = (wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        acc |= __builtin_amdgcn_ubfe(old[i], (v & 1u) << 4, 16) + ((uint32_t)i < nv ? 1u : 0u);
-    }
-    if (__builtin_expect((acc >> 16) != 0u, 0)) {
+    for (int i = 0; i < 8; i += 2)
+        mx = max(mx, max(__builtin_amdgcn_ubfe(old[i], off[i], 16), __builtin_amdgcn_ubfe(old[i + 1], off[i + 1], 16)));
+    if (__builtin_expect(mx == 0xFFFFu, 0)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t v = (wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-            if ((uint32_t)i < nv && __builtin_amdgcn_ubfe(old[i], (v & 1u) << 4, 16) == 0xFFFFu)
+            if ((uint32_t)i < nv && __builtin_amdgcn_ubfe(old[i], off[i], 16) == 0xFFFFu)
                 log_wrap(L, row0, v, old[i]);
         }
     }
@@ -487,13 +490,8 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     for (; tw < tb; tw += (uint64_t)NW * BT) {
         const uint32_t c0 = lo_n & 0xFFFu, nc = (hi_n & 0xFFFu) - c0;
         const uint32_t nlast = 8u - (lo_n >> 12);
-        uint32_t incl = nc;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
-        }
-        const uint32_t total = __shfl(incl, 63);
+        const uint32_t incl = scan64(nc);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint64_t cbat = tw * (uint64_t)CPT;                  // the batch's first chunk
         const uint32_t crel = (uint32_t)lane * CPT + c0;           // this segment's, relative
         if (total <= (uint32_t)QMAX) {
@@ -630,12 +628,13 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
     constexpr int NBK = num_buckets<K>();
     constexpr int U = 6;                  // chunk loads in flight per lane (queue = 64 U)
     const size_t row = (size_t)1 << (2 * K);
-    // Genomes per batch: the suffix buffer of one batch stays within the budget (4 GiB: 18
-    // genomes of 100 Mbp at k = 12).  Measured (profiles/ab_r02.sh): 1, 2 and 4 GiB budgets
-    // give 10.1, 10.3 and 9.4 ms per config-3 step -- launch tails and boundaries cost more
-    // than the larger write footprint.  KMH_SUF_BUDGET_MB changes only the batching (tests
+    // Genomes per batch: the suffix buffer of one batch stays within the budget (8 GiB: 36
+    // genomes of 100 Mbp at k = 12).  Measured (profiles/ab2_r02.sh, config 3): 2 / 4 / 8 GiB
+    // budgets 10.1 / 9.3 / 9.2 ms per step; the partition of batch i + 1 on a side stream beside
+    // the count of batch i was no faster (10.3 / 10.3 / 9.3 ms): both kernels move ~5 TB/s of
+    // mixed HBM traffic.  KMH_SUF_BUDGET_MB changes only the batching, never the counts (tests
     // force one genome per batch with it).
-    const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 4096) << 20;
+    const size_t budget = env_mb("KMH_SUF_BUDGET_MB", 8192) << 20;
     const size_t tile_bytes = (size_t)tile_cap<K>() * sizeof(uint16_t);
     auto batch_end = [&](int g) {
         int h = g;

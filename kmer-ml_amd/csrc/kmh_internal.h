@@ -37,8 +37,6 @@ struct Ctx {
     int device = 0;
     int num_cu = 256;                  // compute units of the device (persistent grids)
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;        // partition stream of the two-stream pipeline
-    hipEvent_t pipe_ev[5] = {};        // input-ready, partition-done x2, count-done x2
     std::string err;
     // device workspace
     DevBuf seq, suf, toff, meta, out, out2, fix, sparse[8], order;
