@@ -236,7 +236,7 @@ def main():
         locals_ = [f[rank * B:(rank + 1) * B] for f in fulls]
         send = [torch.zeros(P, dtype=torch.uint8, device=dev) for _ in range(2)]
         recv = [torch.empty(world * P, dtype=torch.uint8, device=dev) for _ in range(2)]
-        esc_max = torch.zeros(world, dtype=torch.int32, device=dev)
+        esc_max = torch.zeros(world, dtype=torch.int64, device=dev)
         side = torch.cuda.Stream(dev)
         dec_done = [None, None]
         pending = []
@@ -261,7 +261,7 @@ def main():
                     else:
                         ctx.rows_decode_u8(slot, B, bins, slot + payload + 16, cap, slot + payload,
                                            1, B, dst[q * B:].data_ptr(), side.cuda_stream)
-                n = r.view(world, P)[:, payload:payload + 4].view(torch.int32)[:, 0]
+                n = r.view(world, P)[:, payload:payload + 4].contiguous().view(torch.int32)[:, 0].to(torch.int64) & 0xFFFFFFFF
                 torch.maximum(esc_max, n, out=esc_max)
                 ev = torch.cuda.Event()
                 ev.record(side)

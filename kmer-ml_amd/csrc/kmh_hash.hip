@@ -447,7 +447,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
     const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
     uint32_t* __restrict__ counts, unsigned long long* __restrict__ nk,
-    const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed, int abl,
+    const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed,
     unsigned long long* __restrict__ prof) {
     // Slot = key << 32 | count; a slot is empty iff its count is 0, so every 32-bit residue
     // (k = 21 uses all 32 bits) is a valid key.  Emission scans the table: for each of the
@@ -527,8 +527,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     // their lengths, and takes an equal share of the group's entries (concatenated in
     // split-item order): entry e lies in the last segment whose exclusive start is <= e.
     // Equal shares matter: the workgroup waits at the barrier for its slowest wave.
-    uint32_t sink = 0u;
-    for (uint32_t g = it.s0; g < it.s1 && !(abl & 4); g += 64u) {
+    for (uint32_t g = it.s0; g < it.s1; g += 64u) {
         const uint32_t ns = min(64u, it.s1 - g);
         const uint32_t j = g + (uint32_t)lane;
         uint32_t lo = 0u, len = 0u;
@@ -575,23 +574,17 @@ __global__ __launch_bounds__(NT) void k_sp_count(
                 r[u] = ok ? v : 0u;
                 cnt += ok ? 1 : 0;   // valid entries of a lane are a prefix of r
             }
-            if (abl & 1) {
+            // two calls of 8 keys (a lane's valid keys are a prefix of r)
+            uint32_t a8[8], b8[8];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) sink ^= u < cnt ? r[u] : 0u;
-            } else {
-                // two calls of 8 keys (a lane's valid keys are a prefix of r)
-                uint32_t a8[8], b8[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    a8[u] = r[u];
-                    b8[u] = r[u + 8];
-                }
-                insert_keys(a8, cnt < 8 ? cnt : 8);
-                if (__ballot(cnt > 8)) insert_keys(b8, cnt > 8 ? cnt - 8 : 0);
+            for (int u = 0; u < 8; ++u) {
+                a8[u] = r[u];
+                b8[u] = r[u + 8];
             }
+            insert_keys(a8, cnt < 8 ? cnt : 8);
+            if (__ballot(cnt > 8)) insert_keys(b8, cnt > 8 ? cnt - 8 : 0);
         }
     }
-    if (abl & 1) asm volatile("" ::"v"(sink));
     lds_barrier();
     const unsigned long long c1 = prof ? clock64() : 0ull;
 
@@ -624,12 +617,11 @@ __global__ __launch_bounds__(NT) void k_sp_count(
             const uint32_t at = atomicAdd(&failed[0], 1u);
             failed[1 + at] = item;
         } else {
-            obase = (abl & 8) ? (unsigned long long)(item & 255u) * 4096ull   // timing only
-                              : atomicAdd(&nk[it.g], (unsigned long long)used);
+            obase = atomicAdd(&nk[it.g], (unsigned long long)used);
         }
     }
     lds_barrier();
-    if (!bad && !(abl & 2)) {
+    if (!bad) {
         const uint64_t at = out_off[it.g] + obase + before;
         const uint64_t hib = (uint64_t)it.b << R;
         uint32_t run = 0u;
@@ -803,9 +795,14 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
 
     const size_t tile_bytes = (size_t)kSpTile * sizeof(uint32_t);
     const size_t budget = env_mb("KMH_SP_BUDGET_MB", 16384) << 20;
-    // LDS hash table of the count kernel: 2^table_bits slots (KMH_SP_TABLE_BITS 12..14);
-    // smaller tables let several count workgroups share a CU and overlap their latencies.
+    // LDS hash table of the count kernel: 2^14 slots.  Experiment builds (-DKMH_EXPERIMENTS)
+    // also take KMH_SP_TABLE_BITS 12..13: smaller tables, several count workgroups per CU
+    // (measured slower).
+#ifdef KMH_EXPERIMENTS
     const int table_bits = (int)std::min<long>(14, std::max<long>(12, env_long("KMH_SP_TABLE_BITS", 14)));
+#else
+    const int table_bits = 14;
+#endif
     const unsigned wg_per_cu = 1u << (14 - table_bits);   // LDS-limited residency
     const uint32_t target = (uint32_t)std::max<long>(1, env_long("KMH_SP_TARGET", 1l << (table_bits - 1)));
     const uint32_t split_target = (uint32_t)std::max<long>(1, std::min<long>(env_long("KMH_SP_SPLIT", 12288), kCaps));
@@ -835,9 +832,13 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     uint32_t* ent = static_cast<uint32_t*>(ctx->sparse[2].ptr);
     uint16_t* toff = static_cast<uint16_t*>(ctx->sparse[3].ptr);
 
-    // KMH_SP_PROF=1 or 2 prints the host phases of every batch (2: without the kernel's own
-    // cycle counters, which slow it down; experiments)
+    // Experiment builds: KMH_SP_PROF=1 or 2 prints the host phases of every batch (2: without
+    // the kernel's own cycle counters, which slow it down)
+#ifdef KMH_EXPERIMENTS
     const bool hprof = env_long("KMH_SP_PROF", 0) != 0;
+#else
+    const bool hprof = false;
+#endif
     auto now_ms = [] {
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     };
@@ -906,9 +907,13 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         KMH_HIP(ctx, hipGetLastError());
         time_begin(ctx, s, "k_sp_count");
         const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * wg_per_cu);
-        // KMH_SP_PROF=1: per-phase cycle counters of k_sp_count on stderr (experiments)
+        // KMH_SP_PROF=1 (experiment builds): per-phase cycle counters of k_sp_count on stderr
         unsigned long long* d_prof = nullptr;
+#ifdef KMH_EXPERIMENTS
         const bool prof = env_long("KMH_SP_PROF", 0) == 1;
+#else
+        const bool prof = false;
+#endif
         if (prof) {
             rc = ensure(ctx, ctx->sparse[7], 256);
             if (rc) return rc;
@@ -918,11 +923,13 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
 #define KMH_SP_COUNT(SB, NT)                                                                         \
     hipLaunchKernelGGL((k_sp_count<SB, NT>), dim3(cgrid), dim3(NT), 0, s, d_split, d_toff2, d_citems,   \
                        (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts,                               \
-                       reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed,                  \
-                       (int)env_long("KMH_SP_ABL", 0), d_prof)
-        if (table_bits == 14) KMH_SP_COUNT(14, 1024);
-        else if (table_bits == 13) KMH_SP_COUNT(13, 1024);
-        else KMH_SP_COUNT(12, 512);
+                       reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed, d_prof)
+#ifdef KMH_EXPERIMENTS
+        if (table_bits == 13) KMH_SP_COUNT(13, 1024);
+        else if (table_bits == 12) KMH_SP_COUNT(12, 512);
+        else
+#endif
+            KMH_SP_COUNT(14, 1024);
 #undef KMH_SP_COUNT
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());

@@ -47,19 +47,6 @@ __global__ __launch_bounds__(256) void k_encode_u8(const uint32_t* __restrict__ 
     }
 }
 
-__global__ __launch_bounds__(256) void k_decode_u8(const uint8_t* __restrict__ in, uint64_t n16,
-                                                   uint32_t* __restrict__ rows) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 v = reinterpret_cast<const uint4*>(in)[i];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint4* dst = reinterpret_cast<uint4*>(rows) + 4 * i;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            dst[q] = make_uint4(w[q] & 0xFFu, (w[q] >> 8) & 0xFFu, (w[q] >> 16) & 0xFFu, w[q] >> 24);
-    }
-}
-
 __global__ __launch_bounds__(256) void k_apply_escapes(const uint32_t* __restrict__ esc,
                                                        uint32_t cap,
                                                        const uint32_t* __restrict__ esc_n,
@@ -105,48 +92,10 @@ __global__ __launch_bounds__(256) void k_decode_u8w(const uint32_t* __restrict__
 
 __device__ __forceinline__ uint32_t sat4(uint32_t x) { return x < 15u ? x : 15u; }
 
-// 32 elements per thread per step: eight 16-byte loads, one 16-byte store.
-__global__ __launch_bounds__(256) void k_encode_u4(const uint32_t* __restrict__ rows, uint64_t n32,
-                                                   uint8_t* __restrict__ out,
-                                                   uint32_t* __restrict__ esc, uint32_t cap,
-                                                   uint32_t* __restrict__ esc_n) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n32;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4* src = reinterpret_cast<const uint4*>(rows) + 8 * i;
-        uint4 v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = src[q];
-        uint32_t packed[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const uint4 a = v[2 * h], b = v[2 * h + 1];
-            packed[h] = sat4(a.x) | (sat4(a.y) << 4) | (sat4(a.z) << 8) | (sat4(a.w) << 12) |
-                        (sat4(b.x) << 16) | (sat4(b.y) << 20) | (sat4(b.z) << 24) | (sat4(b.w) << 28);
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint32_t e[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-            if (max(max(e[0], e[1]), max(e[2], e[3])) >= 15u) {   // ~2 % of the 4-groups
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (e[j] >= 15u) {
-                        const uint32_t at = atomicAdd(esc_n, 1u);
-                        if (at < cap) {
-                            esc[2 * (uint64_t)at] = (uint32_t)(32 * i + 4 * q + j);
-                            esc[2 * (uint64_t)at + 1] = e[j];
-                        }
-                    }
-                }
-            }
-        }
-        store_nt(reinterpret_cast<uint4*>(out) + i, make_uint4(packed[0], packed[1], packed[2], packed[3]));
-    }
-}
-
 // Wave-coalesced u4 encode: a wave takes 512 consecutive 4-count groups (uint4) per step; lane
 // l takes groups base + 64u + l, u = 0..7, so every load instruction reads 1 KiB contiguous
 // and every store writes 128 B contiguous (group g -> the u16 at index g: the same nibble
-// layout as k_encode_u4).  Escapes are counted per lane, scanned across the wave and appended
+// layout: element 2i in the low nibble of byte i).  Escapes are counted per lane, scanned across the wave and appended
 // behind one atomic per wave (a single global counter per lane-escape serialises at L2).
 __global__ __launch_bounds__(256) void k_encode_u4w(const uint32_t* __restrict__ rows, uint64_t n4,
                                                     uint16_t* __restrict__ out,
@@ -274,22 +223,6 @@ unsigned grid_waves(uint64_t n4) {   // 256-thread blocks, one 512-group step pe
     return (unsigned)(b < 4096 ? (b ? b : 1) : 4096);
 }
 
-__global__ __launch_bounds__(256) void k_decode_u4(const uint8_t* __restrict__ in, uint64_t n32,
-                                                   uint32_t* __restrict__ rows) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n32;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 v = reinterpret_cast<const uint4*>(in)[i];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint4* dst = reinterpret_cast<uint4*>(rows) + 8 * i;
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const uint32_t x = w[h];
-            store_nt(dst + 2 * h, make_uint4(x & 15u, (x >> 4) & 15u, (x >> 8) & 15u, (x >> 12) & 15u));
-            store_nt(dst + 2 * h + 1, make_uint4((x >> 16) & 15u, (x >> 20) & 15u, (x >> 24) & 15u, x >> 28));
-        }
-    }
-}
-
 __global__ __launch_bounds__(256) void k_apply_escapes_u4(const uint32_t* __restrict__ esc,
                                                           uint32_t cap,
                                                           const uint32_t* __restrict__ esc_n,
@@ -333,11 +266,8 @@ int rows_decode_u8(Ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
     const uint64_t n16 = rows * cols / 16;
     if (n16) {
         time_begin(ctx, s, "k_decode_u8");
-        if (env_long("KMH_U4_OLD", 0))   // the per-thread-contiguous kernel (A/B only)
-            hipLaunchKernelGGL(k_decode_u8, dim3(grid_for(n16)), dim3(256), 0, s, d_u8, n16, d_rows);
-        else
-            hipLaunchKernelGGL(k_decode_u8w, dim3((unsigned)std::min<uint64_t>(4096, (4 * n16 + 2047) / 2048)), dim3(256), 0, s,
-                               reinterpret_cast<const uint32_t*>(d_u8), 4 * n16, d_rows);
+        hipLaunchKernelGGL(k_decode_u8w, dim3((unsigned)std::min<uint64_t>(4096, (4 * n16 + 2047) / 2048)), dim3(256), 0, s,
+                           reinterpret_cast<const uint32_t*>(d_u8), 4 * n16, d_rows);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
     }
@@ -362,10 +292,7 @@ int rows_encode_u4(Ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t col
     const uint64_t n32 = rows * cols / 32;
     if (n32 == 0) return KMH_OK;
     time_begin(ctx, s, "k_encode_u4");
-    if (env_long("KMH_U4_OLD", 0))   // the per-thread-contiguous kernel (A/B only)
-        hipLaunchKernelGGL(k_encode_u4, dim3(grid_for(n32)), dim3(256), 0, s, d_rows, n32, d_u4, d_esc, cap, d_esc_n);
-    else
-        hipLaunchKernelGGL(k_encode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s, d_rows, 8 * n32,
+    hipLaunchKernelGGL(k_encode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s, d_rows, 8 * n32,
                            reinterpret_cast<uint16_t*>(d_u4), d_esc, cap, d_esc_n);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
@@ -380,10 +307,7 @@ int rows_decode_u4(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, 
     const uint64_t n32 = rows * cols / 32;
     if (n32 == 0) return KMH_OK;
     time_begin(ctx, s, "k_decode_u4");
-    if (env_long("KMH_U4_OLD", 0))
-        hipLaunchKernelGGL(k_decode_u4, dim3(grid_for(n32)), dim3(256), 0, s, d_u4, n32, d_rows);
-    else
-        hipLaunchKernelGGL(k_decode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_decode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s,
                            reinterpret_cast<const uint16_t*>(d_u4), 8 * n32, d_rows);  // 8 four-count groups per 32 counts
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());

@@ -89,6 +89,15 @@ def slot_layout_u4(rows, cols):
     return cap, (rows * cols // 2 + 16 + cap * 8 + 255) // 256 * 256
 
 
+def escape_count(word_bytes):
+    """The u32 escape counter at the head of a slot's escape area (4 uint8 device bytes), as
+    an int64 tensor: read unsigned, so a count of 2^31 or more never looks negative and skips
+    the overflow check (the encoders count every escape, also those past cap)."""
+    import torch
+
+    return word_bytes.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+
+
 def gather_rows_u4(padded, group=None):
     """All-gather [B, cols] u32 rows (device int32 tensor) from every rank as u4 + escapes.
 
@@ -109,7 +118,7 @@ def gather_rows_u4(padded, group=None):
     send = torch.empty(P, dtype=torch.uint8, device=dev)
     ctx.rows_encode_u4(padded.data_ptr(), B, cols, send.data_ptr(), send[nib + 16:].data_ptr(),
                        cap, send[nib:].data_ptr(), s)
-    n = send[nib:nib + 4].view(torch.int32).clone()
+    n = escape_count(send[nib:nib + 4])
     dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
     if int(n.item()) > cap:
         return gather_rows_u8(padded, group)
@@ -142,7 +151,7 @@ def gather_rows_u8(padded, group=None):
     send = torch.empty(P, dtype=torch.uint8, device=dev)
     ctx.rows_encode_u8(padded.data_ptr(), B, cols, send.data_ptr(), send[u8_bytes + 16:].data_ptr(),
                        cap, send[u8_bytes:].data_ptr(), s)
-    n = send[u8_bytes:u8_bytes + 4].view(torch.int32).clone()
+    n = escape_count(send[u8_bytes:u8_bytes + 4])
     dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
     if int(n.item()) > cap:
         out = torch.empty((world * B, cols), dtype=padded.dtype, device=dev)
