@@ -10,6 +10,10 @@ OBJDIR   := $(CSRC)/build
 LIB      := $(OUTDIR)/libkmerhip.so
 OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o $(OBJDIR)/kmh_hash.o $(OBJDIR)/kmh_io.o
 HDRS     := $(CSRC)/kmh_internal.h $(CSRC)/kmh_device.h include/kmerhip.h
+SRCS     := $(wildcard $(CSRC)/*.hip $(CSRC)/*.cpp) $(HDRS)
+# Build id: hash of every product source, compiled into kmh_build_id(); bench.py prints a
+# PMC traffic figure only when profiles/pmc_traffic.json was measured on the same build id.
+BUILD_ID := $(shell cat $(SRCS) | sha256sum | cut -c1-16)
 
 all: lib oracle selftest
 
@@ -22,6 +26,10 @@ $(LIB): $(OBJS)
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(OBJDIR)/kmh_api.o: $(CSRC)/kmh_api.cpp $(SRCS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DKMH_BUILD_ID='"$(BUILD_ID)"' -x hip -c -o $@ $<
 
 $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)

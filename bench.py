@@ -64,9 +64,15 @@ def parse():
                    help="HIP event pairs around the kernels the roofline names only (default), or all")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="experiments: no per-kernel HIP events in the timed region (roofline = null)")
-    p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
+    p.add_argument("--pmc-summary", default=os.path.join(HERE, "profiles", "pmc_traffic.json"),
+                   help="rocprofv3 FETCH_SIZE / WRITE_SIZE summary (profiles/pmc_summary.py); its "
+                        "figure is printed only if it was measured on this library's build id")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="process-group backend (gloo + --single-device: multi-rank logic check on one GPU)")
+    p.add_argument("--check-dir", default=None,
+                   help="after timing, verify the assembled matrix on every rank against every rank's "
+                        "own count rows (row signatures), and have rank 0 save the assembled rows of "
+                        "genomes 0 and G-1 there as .npy (tests compare them with the oracle)")
     p.add_argument("--single-device", action="store_true",
                    help="map every rank to cuda:0 (validation only; never used for reported numbers)")
     a = p.parse_args()
@@ -119,6 +125,41 @@ def cpu_threads_baseline(k, bases_per_thread=25_000_000, threads=16):
                       f"generate.py:49-58 (oracle/kmer_oracle.c) on {threads} threads, {dt:.2f} s"}
 
 
+def _ref_loop_genome(args):
+    """One process of cpu_procs_baseline: the restated reference loop over its own genome."""
+    g, n, k = args
+    from oracle import kmers as okmers
+    from oracle import synth as osynth
+    seq = osynth.synth_bases(n, osynth.genome_seed(g)).tobytes().decode()
+    t0 = time.perf_counter()
+    table = okmers.count_sequence(seq, k)
+    dt = time.perf_counter() - t0
+    assert sum(table.values()) == n - k + 1
+    return dt
+
+
+def cpu_procs_baseline(k, bases_per_proc=4_000_000, procs=None):
+    """SURVEY.md 8(d) "ref-CPU x P": the reference's per-window Python loop (oracle/kmers.py
+    restates generate.py:49-58) with one genome per process on P host cores.  The reference
+    itself is serial (scripts/extract_kmers.py:58-61 loops over genomes), so this is the best
+    its algorithm does on this host without changing it.  P = the cores this process may use,
+    at most 16 (one GPU's share of the box).  Forked before the GPU is touched."""
+    import multiprocessing as mp
+    sys.path.insert(0, HERE)
+    if procs is None:
+        procs = max(1, min(16, len(os.sched_getaffinity(0))))
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(procs) as pool:
+        per = pool.map(_ref_loop_genome, [(g, bases_per_proc, k) for g in range(procs)])
+    dt = time.perf_counter() - t0
+    # rate over the count loops, which run concurrently (the slowest sets it); the wall time
+    # also holds pool start-up and each process generating its genome
+    return {"value": procs * bases_per_proc / max(per), "unit": "bases/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} synthetic genomes x {bases_per_proc} bases, k={k}, one genome per process: "
+                      f"the count loop of generate.py:49-58 restated in pure Python (oracle/kmers.py), "
+                      f"slowest process {max(per):.2f} s ({dt:.2f} s wall with start-up)"}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -131,14 +172,77 @@ def _cpu_model():
 
 
 def load_traffic(path, config_key):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this command."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this command.
+
+    Returns (entry, note).  An entry measured on another build of the library (its
+    "build_id" differs from kmh_build_id() of the loaded one) is stale and not returned.
+    """
+    from kmerml import _native
+
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no PMC summary"
     entry = d.get(config_key)
-    return entry if isinstance(entry, dict) else None
+    if not isinstance(entry, dict):
+        return None, f"no PMC entry {config_key}"
+    lib_id = _native.build_id()
+    if entry.get("build_id") != lib_id:
+        return None, f"stale PMC entry (build {entry.get('build_id')}, library {lib_id})"
+    return entry, f"rocprofv3 FETCH_SIZE/WRITE_SIZE passes on build {lib_id} ({entry.get('source', '')})"
+
+
+def row_signatures(rows):
+    """[n, 2] int64 per row: the sum and sum(value * (column + 1)) (int64, wrapping), one row
+    at a time (a whole-matrix int64 temporary would be 8 x its size)."""
+    n, bins = rows.shape
+    w = torch.arange(1, bins + 1, dtype=torch.int64, device=rows.device)
+    out = torch.empty((n, 2), dtype=torch.int64, device=rows.device)
+    for i in range(n):
+        r = rows[i].to(torch.int64) & 0xFFFFFFFF
+        out[i, 0] = r.sum()
+        out[i, 1] = (r * w).sum()
+    return out.cpu()
+
+
+def check_assembly(full, own, B, G, world, rank, k, check_dir):
+    """Every rank's assembled matrix against every rank's own count rows: rank q's block of
+    `full` (rows q*B ..) must have the signatures rank q computed from the rows it counted
+    (which, at N > 1, every other rank only sees after encode -> all-gather -> decode).  Rank 0
+    also saves the assembled rows of genomes 0 and G - 1 for an oracle comparison."""
+    mine = row_signatures(own)
+    if world > 1:
+        sigs = [None] * world
+        dist.all_gather_object(sigs, mine)
+    else:
+        sigs = [mine]
+    ok = True
+    for q in range(world):
+        lo, hi = (G * q) // world, (G * (q + 1)) // world
+        got = row_signatures(full[q * B:q * B + (hi - lo)])
+        ok = ok and torch.equal(got, sigs[q])
+    if rank == 0:
+        os.makedirs(check_dir, exist_ok=True)
+        last_q = world - 1
+        last_row = last_q * B + (G - 1 - (G * last_q) // world)
+        np.save(os.path.join(check_dir, "row_first.npy"), full[0].cpu().numpy().view(np.uint32))
+        np.save(os.path.join(check_dir, "row_last.npy"), full[last_row].cpu().numpy().view(np.uint32))
+    return bool(ok)
+
+
+def workload_name(G, L, k, world, single_device, backend):
+    """BASELINE.json config label -- only for the configs' own sizes on real devices; anything
+    else (smaller genomes, ranks sharing one GPU) is labelled a rehearsal."""
+    shape = f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k} dense 4^{k} count matrix"
+    if world > 1:
+        shape += f", sharded {G}/{world} per rank + {backend} all-gather"
+    real = G == 64 and L == 100_000_000 and k == 12 and not single_device
+    if single_device:
+        return f"rehearsal ({world} ranks sharing cuda:0, not a config-4 measurement): {shape}"
+    if not real:
+        return f"non-baseline size: {shape}"
+    return f"config{3 if world == 1 else 4}: {shape}"
 
 
 def main():
@@ -149,6 +253,13 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    # CPU baselines first (rank 0, N = 1 only), before the GPU is touched (the process pool
+    # forks) and so that they never overlap GPU timing.
+    cpu = cpu_mt = cpu_p = None
+    if a.workload == "dense" and rank == 0 and world == 1 and a.cpu_sample > 0:
+        cpu = cpu_baseline(a.cpu_sample, a.k)
+        cpu_p = cpu_procs_baseline(a.k)
+        cpu_mt = cpu_threads_baseline(a.k)
     dev_index = 0 if a.single_device else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -169,12 +280,6 @@ def main():
     mode = ("u4" if world > 1 else "none") if a.assemble == "auto" else a.assemble
     assemble = mode != "none"
     bins = 1 << (2 * k)
-
-    # CPU baseline first (rank 0, N = 1 only), so it never overlaps GPU timing.
-    cpu = cpu_mt = None
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu = cpu_baseline(a.cpu_sample, k)
-        cpu_mt = cpu_threads_baseline(k)
 
     ctx = _native.context(dev_index)
     stream = torch.cuda.current_stream(dev)
@@ -336,6 +441,10 @@ def main():
         ok = ok and bool(torch.equal(full[rank * B:rank * B + g_local], last[:g_local]))
     if mode in ("u4", "u8") and int(esc_max.max().item()) > cap:
         raise SystemExit(f"escape list overflow ({int(esc_max.max().item())} > {cap}): use --assemble u32")
+    assembly_checked = None
+    if a.check_dir is not None and assemble:
+        assembly_checked = check_assembly(full, last[:g_local], B, G, world, rank, k, a.check_dir)
+        ok = ok and assembly_checked
     if world > 1:
         okt = torch.tensor([int(ok)], dtype=torch.int32, device=dev if not gloo else "cpu")
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
@@ -368,10 +477,11 @@ def main():
             else:
                 algo = g_local * (L + bins * 4) / max(1, launches / a.steps)
             achieved = algo / (per_launch_ms * 1e-3) / 1e9
-            traffic = load_traffic(a.pmc_summary, f"{name}:k{k}:L{L}")
+            traffic, tnote = load_traffic(a.pmc_summary, f"{name}:k{k}:L{L}:G{g_local}")
             roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                    "traffic_source": tnote,
                     "algorithmic_bytes_per_launch": algo, "mean_launch_ms": round(per_launch_ms, 4),
                     "launches_per_step": launches / a.steps}
         count_rate = g_local * L / (count_ms * 1e-3)
@@ -379,12 +489,11 @@ def main():
             "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": (f"config{3 if world == 1 else 4}: {G} synthetic {L // 1_000_000} Mbp "
-                                    f"genomes, k={k} dense 4^{k} count matrix"
-                                    + ("" if world == 1 else f", sharded {G}/{world} per GPU + RCCL all-gather")),
+            "config": {"workload": workload_name(G, L, k, world, a.single_device, a.backend),
                        "genomes": G, "genome_len": L, "k": k,
                        "parallelism": f"genome-sharded x{world}" + (f" + {mode} allgather" if assemble else ""),
                        "assembly": mode},
+            "single_device": bool(a.single_device),
             "roofline": roof,
             "step_roofline": {"algorithmic_bytes": algo_step, "achieved_GBs": round(algo_step / (ms * 1e-3) / 1e9, 1),
                               "frac": round(algo_step / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -395,7 +504,9 @@ def main():
             "kernels": {n: {"launches": l, "total_ms": round(t, 4), "mean_ms": round(t / l, 4)}
                         for n, (l, t) in kernels.items()},
             "rows_checked": ok,
+            "assembly_checked": assembly_checked,
             "cpu_baseline": cpu,
+            "cpu_procs_baseline": cpu_p,
             "cpu_threads_baseline": cpu_mt,
         }
         if cpu:
@@ -487,10 +598,11 @@ def run_sparse(a, world, rank, dev, dev_index):
             else:
                 algo = algo_step / per_step
             achieved = algo / (per_launch_ms * 1e-3) / 1e9
-            traffic = load_traffic(a.pmc_summary, f"{name}:k{k}:L{L}")
+            traffic, tnote = load_traffic(a.pmc_summary, f"{name}:k{k}:L{L}:G{g_local}")
             roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+                    "traffic_source": tnote,
                     "algorithmic_bytes_per_launch": algo, "mean_launch_ms": round(per_launch_ms, 4),
                     "launches_per_step": per_step}
         out = {

@@ -56,6 +56,11 @@ typedef struct kmh_kmers kmh_kmers;
 /* Version string, e.g. "kmerhip 0.1.0 gfx950". */
 const char* kmh_version(void);
 
+/* Build id: the first 16 hex digits of a SHA-256 over the library's sources (set by the
+ * Makefile; "unknown" for other builds).  bench.py matches it against the build id stamped
+ * into profiles/pmc_traffic.json before it reports a PMC traffic figure. */
+const char* kmh_build_id(void);
+
 /* Create a context on HIP device `device`: selects the device, creates a stream and
  * an empty device workspace.  Replaces nothing in the reference (it has no device). */
 int kmh_ctx_create(int device, kmh_ctx** out);

@@ -112,7 +112,12 @@ static hipStream_t pick_stream(kmh_ctx*, void* stream) { return static_cast<hipS
 
 extern "C" {
 
-const char* kmh_version(void) { return "kmerhip 0.1.0 gfx950"; }
+const char* kmh_version(void) { return "kmerhip 0.2.0 gfx950"; }
+
+#ifndef KMH_BUILD_ID
+#define KMH_BUILD_ID "unknown"
+#endif
+const char* kmh_build_id(void) { return KMH_BUILD_ID; }
 
 int kmh_ctx_create(int device, kmh_ctx** out) {
     if (!out) {

@@ -29,6 +29,7 @@ _u64p = _c.POINTER(_c.c_uint64)
 # (name, restype, argtypes) for every symbol of include/kmerhip.h
 SIGNATURES = [
     ("kmh_version", _c.c_char_p, []),
+    ("kmh_build_id", _c.c_char_p, []),
     ("kmh_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_vp)]),
     ("kmh_ctx_destroy", None, [_vp]),
     ("kmh_last_error", _c.c_char_p, [_vp]),
@@ -92,6 +93,11 @@ def lib():
                     fn.argtypes = args
                 _lib = L
     return _lib
+
+
+def build_id():
+    """Source hash the loaded library was built from (kmh_build_id)."""
+    return lib().kmh_build_id().decode()
 
 
 def _check(rc, ctx=None):

@@ -14,9 +14,47 @@ generate.py:39-58 exactly (records shorter than k skipped, non-ACGT windows drop
 Nothing here falls back to the CPU; ``count_fn`` exists so the sharding and assembly
 logic can be exercised with the gloo backend in CPU-only tests.
 """
+import os
+
 import numpy as np
 
 from kmerml import _native
+
+# Wire format the last gather_rows_* call ended up using ("u4", "u8" or "u32").
+LAST_WIRE = None
+
+
+def _cap_override(name, cap):
+    """Test knob: KMH_ESC_CAP_U4 / KMH_ESC_CAP_U8 lower an escape capacity so that the exact
+    fallbacks (u4 -> u8 -> u32) can be forced on real data.  Only ever lowers the capacity:
+    a lower cap changes which wire format is used, never the assembled matrix."""
+    v = os.environ.get(name)
+    return min(cap, max(0, int(v))) if v else cap
+
+
+def _all_reduce_max(t, group):
+    import torch.distributed as dist
+
+    if t.is_cuda and dist.get_backend(group) == "gloo":   # gloo reduces host tensors
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t
+
+
+def _all_gather(out, inp, group):
+    import torch
+    import torch.distributed as dist
+
+    if inp.is_cuda and dist.get_backend(group) == "gloo":   # gloo gathers host tensors
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, inp.cpu(), group=group)
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    return out
 
 
 def shard_bounds(n_items, world, rank):
@@ -73,7 +111,7 @@ def slot_layout(rows, cols):
     [rows * cols saturating u8 counts][escape count u32 + 12 B pad][cap (row, col, value) u32
     triples]; returns (cap, slot_bytes).  cap allows one escape (count >= 255) per 1024 cells.
     """
-    cap = max(4096, rows * cols // 1024)
+    cap = _cap_override("KMH_ESC_CAP_U8", max(4096, rows * cols // 1024))
     return cap, (rows * cols + 16 + cap * 12 + 255) // 256 * 256
 
 
@@ -85,7 +123,7 @@ def slot_layout_u4(rows, cols):
     slot_bytes).  cap allows one escape (count >= 15) per 256 cells: uniform 100 Mbp genomes at
     k = 12 (Poisson, mean ~6) need ~1.4 per 1000.
     """
-    cap = max(4096, rows * cols // 256)
+    cap = _cap_override("KMH_ESC_CAP_U4", max(4096, rows * cols // 256))
     return cap, (rows * cols // 2 + 16 + cap * 8 + 255) // 256 * 256
 
 
@@ -118,12 +156,12 @@ def gather_rows_u4(padded, group=None):
     send = torch.empty(P, dtype=torch.uint8, device=dev)
     ctx.rows_encode_u4(padded.data_ptr(), B, cols, send.data_ptr(), send[nib + 16:].data_ptr(),
                        cap, send[nib:].data_ptr(), s)
-    n = escape_count(send[nib:nib + 4])
-    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    n = _all_reduce_max(escape_count(send[nib:nib + 4]), group)
     if int(n.item()) > cap:
         return gather_rows_u8(padded, group)
-    recv = torch.empty(world * P, dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(recv, send, group=group)
+    global LAST_WIRE
+    LAST_WIRE = "u4"
+    recv = _all_gather(torch.empty(world * P, dtype=torch.uint8, device=dev), send, group)
     out = torch.empty((world * B, cols), dtype=padded.dtype, device=dev)
     base = recv.data_ptr()
     for q in range(world):
@@ -151,14 +189,14 @@ def gather_rows_u8(padded, group=None):
     send = torch.empty(P, dtype=torch.uint8, device=dev)
     ctx.rows_encode_u8(padded.data_ptr(), B, cols, send.data_ptr(), send[u8_bytes + 16:].data_ptr(),
                        cap, send[u8_bytes:].data_ptr(), s)
-    n = escape_count(send[u8_bytes:u8_bytes + 4])
-    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    n = _all_reduce_max(escape_count(send[u8_bytes:u8_bytes + 4]), group)
+    global LAST_WIRE
     if int(n.item()) > cap:
-        out = torch.empty((world * B, cols), dtype=padded.dtype, device=dev)
-        dist.all_gather_into_tensor(out, padded, group=group)
-        return out
-    recv = torch.empty(world * P, dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(recv, send, group=group)
+        LAST_WIRE = "u32"
+        del send
+        return _all_gather(torch.empty((world * B, cols), dtype=padded.dtype, device=dev), padded, group)
+    LAST_WIRE = "u8"
+    recv = _all_gather(torch.empty(world * P, dtype=torch.uint8, device=dev), send, group)
     out = torch.empty((world * B, cols), dtype=padded.dtype, device=dev)
     base = recv.data_ptr()
     for q in range(world):
@@ -201,8 +239,10 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
     elif padded.is_cuda and B and padded.shape[1] % 16 == 0:
         gathered = gather_rows_u8(padded, group)
     else:
-        gathered = torch.empty((world * B, 1 << (2 * k)), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(gathered, padded, group=group)
+        global LAST_WIRE
+        LAST_WIRE = "u32"
+        gathered = _all_gather(torch.empty((world * B, 1 << (2 * k)), dtype=local.dtype, device=local.device),
+                               padded, group)
     rows = [gathered[r * B: r * B + (shard_bounds(G, world, r)[1] - shard_bounds(G, world, r)[0])]
             for r in range(world)]
     return torch.cat(rows, 0) if rows else gathered[:0]

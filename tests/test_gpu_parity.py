@@ -576,7 +576,7 @@ def test_sparse_dev_rejects_k(ctx, dev):
 
 
 # ---------------------------------------------------------------- RCCL code paths, one GPU
-def _torchrun(args, timeout=600, nproc=1):
+def _torchrun(args, timeout=600, nproc=1, env=None):
     import socket
     import subprocess
     import sys
@@ -586,7 +586,7 @@ def _torchrun(args, timeout=600, nproc=1):
     s.close()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port)] + args
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env,
                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -675,6 +675,59 @@ def test_bench_pipelined_assembly_two_ranks(wire):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["n_gpus"] == 2 and d["config"]["assembly"] == wire
+
+
+def _synth_row(oracle_lib, g, L=100_000_000, k=12, repeat=None):
+    seq = oracle_lib.synth(L, osynth.genome_seed(g))
+    if repeat:
+        seq[:len(repeat)] = np.frombuffer(repeat, np.uint8)
+    return oracle_lib.count_dense(seq, k)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("wire", ["u4", "u8"])
+def test_config4_per_rank_workload_eight_ranks(tmp_path, oracle_lib, wire):
+    """Config 4 at its real per-rank size, eight ranks sharing the one MI355X (gloo for the
+    collectives): 64 synthetic 100 Mbp genomes at k = 12, 8 per rank, every step's matrix
+    assembled through the pipelined u4 (or u8) all-gather with ~176 K escapes per rank.  Every
+    rank's assembled [64, 4^12] matrix must carry every rank's own count rows (row signatures
+    after encode -> all-gather -> decode), and genomes 0 and 63 must equal the oracle's count
+    (reference anchor: the organisms x k-mers matrix of features.py:85-117)."""
+    r = _torchrun(["bench.py", "--gpus", "8", "--backend", "gloo", "--single-device", "--assemble", wire,
+                   "--steps", "2", "--warmup", "1", "--cpu-sample", "0", "--check-dir", str(tmp_path)],
+                  nproc=8, timeout=800)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["rows_checked"] is True and d["assembly_checked"] is True
+    assert d["n_gpus"] == 8 and d["single_device"] is True and d["config"]["assembly"] == wire
+    assert d["config"]["workload"].startswith("rehearsal")
+    assert np.array_equal(np.load(tmp_path / "row_first.npy"), _synth_row(oracle_lib, 0))
+    assert np.array_equal(np.load(tmp_path / "row_last.npy"), _synth_row(oracle_lib, 63))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("caps,wire", [({"KMH_ESC_CAP_U4": "1000"}, "u8"),
+                                       ({"KMH_ESC_CAP_U4": "1000", "KMH_ESC_CAP_U8": "0"}, "u32"),
+                                       ({}, "u4")])
+def test_config4_assembly_fallbacks_full_size(tmp_path, oracle_lib, caps, wire):
+    """The library's assembly (kmerml.kmers.matrix.gather_rows_u4) on config 4's per-rank
+    workload, eight ranks on the one GPU: with the u4 escape capacity lowered below the ~176 K
+    escapes of a rank's 8 x 4^12 block the all-reduced overflow sends every rank to u8, and with
+    the u8 capacity at 0 on to the plain u32 all-gather -- each time the assembled matrix is still
+    exact (own-row signatures on every rank, genomes 0 and 63 vs the oracle).  Genome 0 starts
+    with a 1 Mbp period-8 repeat (counts up to ~125 000: escapes of u4 and u8 alike)."""
+    env = dict(os.environ, **caps)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = _torchrun([os.path.join(here, "assembly_probe.py"), str(tmp_path), "64", "100000000", "12", "gloo",
+                   "--single-device"], nproc=8, timeout=800, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.load(open(tmp_path / "result.json"))
+    assert res == {"wire": wire, "assembly_checked": True, "world": 8}
+    rep = b"ACGTTGCA" * 125_000
+    first = np.load(tmp_path / "row_first.npy")
+    assert first.max() > 100_000
+    assert np.array_equal(first, _synth_row(oracle_lib, 0, repeat=rep))
+    assert np.array_equal(np.load(tmp_path / "row_last.npy"), _synth_row(oracle_lib, 63))
 
 
 def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
