@@ -53,11 +53,17 @@ def parse():
                    help="total genomes over all ranks (default 64 dense / 16 per GPU sparse)")
     p.add_argument("--genome-len", type=int, default=None, help="default 100 Mbp dense / 250 Mbp sparse")
     p.add_argument("--forward", action="store_true", help="sparse: forward-strand codes instead of canonical")
-    p.add_argument("--assemble", choices=["auto", "u4", "u8", "u32", "none"], default="auto",
-                   help="N > 1 matrix assembly: u4 (default) / u8 = saturating 4- / 8-bit rows + "
-                        "exact escape list on the wire, all-gather overlapped with the next step's "
-                        "count, widened to the u32 matrix on every rank; u32 = plain all-gather of "
-                        "the u32 rows after each count")
+    p.add_argument("--assemble", choices=["auto", "u4", "u4-dense", "u8", "u32", "none"], default="auto",
+                   help="N > 1 matrix assembly.  u4 (default): saturating 4-bit rows + exact escape "
+                        "list on the wire, all-gather overlapped with the next step's count, and the "
+                        "assembled matrix kept in that exact compact form on every rank (rows widened "
+                        "on access, kmerml.kmers.matrix.AssembledMatrix); u4-dense / u8: the same "
+                        "wire, every gathered row widened to the u32 matrix on every rank each step; "
+                        "u32 = plain all-gather of the u32 rows after each count")
+    p.add_argument("--simulate-ranks", type=int, default=0,
+                   help="one process on one GPU doing what ONE rank of N does per step at config 4 "
+                        "(count G/N genomes, encode u4, and the all-gather's writes modelled as N "
+                        "device copies of the slot; no xGMI): a projection, labelled as such")
     p.add_argument("--cpu-sample", type=int, default=16_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
     p.add_argument("--kernel-events", choices=["roofline", "all"], default="roofline",
@@ -265,7 +271,7 @@ def main():
     dev = torch.device("cuda", dev_index)
     # A process group for N > 1, or when torch.distributed.run launched a single rank with an
     # explicit assembly mode (exercises the RCCL code path on one GPU).
-    use_dist = world > 1 or (a.assemble in ("u4", "u8", "u32") and "RANK" in os.environ)
+    use_dist = world > 1 or (a.assemble in ("u4", "u4-dense", "u8", "u32") and "RANK" in os.environ)
     if use_dist:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
@@ -274,10 +280,14 @@ def main():
     k, G, L = a.k, a.genomes, a.genome_len
     if a.workload == "sparse":
         return run_sparse(a, world, rank, dev, dev_index)
-    lo, hi = (G * rank) // world, (G * (rank + 1)) // world
+    sim = a.simulate_ranks if world == 1 and a.simulate_ranks > 1 else 0
+    span = sim or world                       # ranks the genomes are sharded over
+    lo, hi = (G * rank) // span, (G * (rank + 1)) // span
     g_local = hi - lo
-    B = -(-G // world)
+    B = -(-G // span)
     mode = ("u4" if world > 1 else "none") if a.assemble == "auto" else a.assemble
+    if sim:
+        mode = "u4"
     assemble = mode != "none"
     bins = 1 << (2 * k)
 
@@ -306,7 +316,54 @@ def main():
             e1.record(stream)
             t_count.append((e0, e1))
 
-    if mode not in ("u4", "u8"):
+    if mode == "u4":
+        # Compact assembly (the N > 1 default): step i counts this rank's rows into
+        # `local`, encodes them into send[i % 2] (u4 + exact escapes) and all-gathers the slots
+        # into recv[i % 2] on RCCL's stream, overlapped with step i+1's count; the assembled
+        # matrix of step i IS recv[i % 2] (every rank's slot; AssembledMatrix widens rows on
+        # access).  Step i+2 waits for step i's all-gather before it reuses the buffers.
+        from kmerml.kmers.matrix import AssembledMatrix, slot_layout_u4
+        cap, P = slot_layout_u4(B, bins)
+        payload = B * bins // 2
+        local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
+        locals_ = [local]
+        send = [torch.zeros(P, dtype=torch.uint8, device=dev) for _ in range(2)]
+        recv = [torch.zeros(span * P, dtype=torch.uint8, device=dev) for _ in range(2)]
+        inflight = [None, None]
+        side = torch.cuda.Stream(dev) if sim else None
+
+        def step(i, record=False):
+            b = i % 2
+            if inflight[b] is not None:      # step i-2's all-gather (send[b] -> recv[b])
+                w = inflight[b]
+                stream.wait_event(w) if isinstance(w, torch.cuda.Event) else w.wait()
+                inflight[b] = None
+            count_into(local, record)
+            sb = send[b]
+            ctx.rows_encode_u4(local.data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
+                               cap, sb[payload:].data_ptr(), s)
+            if sim:   # the gather's HBM side: every slot of recv written from this rank's slot
+                side.wait_stream(stream)
+                with torch.cuda.stream(side):
+                    for q in range(span):
+                        recv[b][q * P:(q + 1) * P].copy_(sb)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                inflight[b] = ev
+            elif not gloo:
+                inflight[b] = dist.all_gather_into_tensor(recv[b], sb, async_op=True)
+            else:  # gloo validation path: host staging, synchronous
+                host = torch.empty(world * P, dtype=torch.uint8)
+                dist.all_gather_into_tensor(host, sb.cpu())
+                recv[b].copy_(host)
+
+        def drain():
+            for b in range(2):
+                if inflight[b] is not None:
+                    w = inflight[b]
+                    stream.wait_event(w) if isinstance(w, torch.cuda.Event) else w.wait()
+                    inflight[b] = None
+    elif mode not in ("u4-dense", "u8"):
         local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
         locals_ = [local]
 
@@ -323,7 +380,7 @@ def main():
         def drain():
             pass
     else:
-        # One all-gather per step of a packed slot per rank, u4 (default) or u8:
+        # One all-gather per step of a packed slot per rank, u4-dense or u8:
         #   [B * bins counts, saturated][esc_n u32, 12 B pad][cap escapes]
         # Step i counts straight into this rank's rows of the full matrix fulls[i % 2], encodes
         # them, and all-gathers the slots (RCCL stream); step i's other ranks' rows are widened
@@ -331,7 +388,7 @@ def main():
         # by events (step i+2 waits for step i's widening), so every step's matrix is complete
         # and exact.
         from kmerml.kmers.matrix import slot_layout, slot_layout_u4
-        if mode == "u4":
+        if mode == "u4-dense":
             cap, P = slot_layout_u4(B, bins)
             payload = B * bins // 2
         else:
@@ -360,7 +417,7 @@ def main():
                     if q == rank:
                         continue
                     slot = base + q * P
-                    if mode == "u4":
+                    if mode == "u4-dense":
                         ctx.rows_decode_u4(slot, B, bins, slot + payload + 16, cap, slot + payload,
                                            dst[q * B:].data_ptr(), side.cuda_stream)
                     else:
@@ -378,7 +435,7 @@ def main():
                 stream.wait_event(dec_done[b])
             count_into(locals_[b], record)
             sb = send[b]
-            if mode == "u4":
+            if mode == "u4-dense":
                 ctx.rows_encode_u4(locals_[b].data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
                                    cap, sb[payload:].data_ptr(), s)
             else:
@@ -429,9 +486,21 @@ def main():
 
     # sanity: every row sums to the number of valid windows (all-ACGT genomes)
     last = locals_[(a.steps - 1) % len(locals_)]
-    if mode in ("u4", "u8"):
+    if mode in ("u4-dense", "u8"):
         full = fulls[(a.steps - 1) % 2]
-    if assemble:   # every rank's block of the assembled matrix (blocks padded to B rows)
+    if mode == "u4":   # widen the last step's compact matrix (outside the timed region) to check it
+        rb = recv[(a.steps - 1) % 2]
+        esc = rb.view(span, P)[:, payload:payload + 4].contiguous().view(torch.int32)[:, 0].to(torch.int64) & 0xFFFFFFFF
+        esc_max = esc
+        am = AssembledMatrix(G if not sim else span * B, bins, span, B, recv=rb, cap=cap, P=P)
+        full = torch.zeros((span * B, bins), dtype=torch.int32, device=dev)
+        for q in range(span):
+            qlo, qhi = (am.G * q) // span, (am.G * (q + 1)) // span
+            full[q * B:q * B + (qhi - qlo)] = am.rows(qlo, qhi)
+    if sim:
+        rows = full.view(span, B, bins)[:, :g_local].reshape(-1, bins)
+        ok_sim = all(torch.equal(full[q * B:q * B + g_local], last[:g_local]) for q in range(span))
+    elif assemble:   # every rank's block of the assembled matrix (blocks padded to B rows)
         idx = [q * B + i for q in range(world) for i in range((G * (q + 1)) // world - (G * q) // world)]
         rows = full[torch.tensor(idx, dtype=torch.long, device=full.device)]
     else:
@@ -439,10 +508,12 @@ def main():
     ok = bool(torch.all(rows.sum(1, dtype=torch.int64) == max(L - k + 1, 0)).item())
     if mode == "u32":   # this rank's block of the assembled matrix is bit-identical to its own count
         ok = ok and bool(torch.equal(full[rank * B:rank * B + g_local], last[:g_local]))
-    if mode in ("u4", "u8") and int(esc_max.max().item()) > cap:
+    if sim:
+        ok = ok and ok_sim
+    if mode in ("u4", "u4-dense", "u8") and int(esc_max.max().item()) > cap:
         raise SystemExit(f"escape list overflow ({int(esc_max.max().item())} > {cap}): use --assemble u32")
     assembly_checked = None
-    if a.check_dir is not None and assemble:
+    if a.check_dir is not None and assemble and not sim:
         assembly_checked = check_assembly(full, last[:g_local], B, G, world, rank, k, a.check_dir)
         ok = ok and assembly_checked
     if world > 1:
@@ -452,10 +523,11 @@ def main():
 
     if rank == 0:
         ms = elapsed / a.steps * 1e3
-        total_bases = G * L if (assemble or world == 1) else g_local * L * world
+        total_bases = G * L if ((assemble or world == 1) and not sim) else g_local * L * world
         value = total_bases / (elapsed / a.steps)
         # per GPU: its genomes read once + the count rows it must end up holding written once
-        algo_step = g_local * L + (G if assemble else g_local) * bins * 4
+        # compact assembly: the rank writes its own rows once; the others stay in u4 form
+        algo_step = g_local * L + (G if assemble and mode != "u4" else g_local) * bins * 4
         dom = max(kernels.items(), key=lambda kv: kv[1][1]) if kernels else None
         roof = None
         if dom:
@@ -494,6 +566,10 @@ def main():
                        "parallelism": f"genome-sharded x{world}" + (f" + {mode} allgather" if assemble else ""),
                        "assembly": mode},
             "single_device": bool(a.single_device),
+            "assembled_form": ({"u4": "u4 + exact escapes on every rank (rows widened on access)",
+                                "u4-dense": "u32 rows on every rank (widened each step)",
+                                "u8": "u32 rows on every rank (widened each step)",
+                                "u32": "u32 rows on every rank"}.get(mode) if assemble else None),
             "roofline": roof,
             "step_roofline": {"algorithmic_bytes": algo_step, "achieved_GBs": round(algo_step / (ms * 1e-3) / 1e9, 1),
                               "frac": round(algo_step / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -509,6 +585,12 @@ def main():
             "cpu_procs_baseline": cpu_p,
             "cpu_threads_baseline": cpu_mt,
         }
+        if sim:
+            out["config"]["workload"] = (f"projection: ONE rank of config 4 at N = {sim} on one GPU (its {g_local} of "
+                                         f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k}, u4 encode, the all-gather "
+                                         f"modelled as {sim} device copies of its slot; no xGMI traffic, no other ranks)")
+            out["simulated_ranks"] = sim
+            out["projected_value_at_n"] = G * L / (elapsed / a.steps)
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)

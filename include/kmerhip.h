@@ -197,6 +197,13 @@ int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, 
 int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
                            const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
                            uint32_t* d_rows, void* stream);
+/* Widen rows [row0, row0 + nrows) of one u4 block (rows x cols) to u32 at d_rows (nrows x cols)
+ * with exactly their escapes: the row accessor of a matrix kept in the compact u4 + escape
+ * form after the all-gather (the organisms x k-mers matrix of
+ * /root/reference/kmerml/ml/features.py:85-117, one row per organism). */
+int kmh_rows_decode_u4_range_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
+                                 const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
+                                 uint64_t row0, uint64_t nrows, uint32_t* d_rows, void* stream);
 
 /* ---- file output (host) -------------------------------------------------------- */
 /* Write n bytes to `path`: plain when gzip_level < 0, else gzip at that level (0..9; the

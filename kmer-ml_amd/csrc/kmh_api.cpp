@@ -291,6 +291,16 @@ int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uin
     return kmh::rows_decode_u4(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, pick_stream(ctx, stream));
 }
 
+int kmh_rows_decode_u4_range_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
+                                 const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
+                                 uint64_t row0, uint64_t nrows, uint32_t* d_rows, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::rows_decode_u4_range(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, row0, nrows, d_rows,
+                                     pick_stream(ctx, stream));
+}
+
 // Host sequence -> device (padded with one non-base byte so loads past the end are safe).
 static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t** d_seq) {
     int rc = kmh::ensure(ctx, ctx->seq, (size_t)n + 64);

@@ -108,6 +108,9 @@ int rows_encode_u4(Ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t col
                    uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, hipStream_t s);
 int rows_decode_u4(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, const uint32_t* d_esc,
                    uint32_t cap, const uint32_t* d_esc_n, uint32_t* d_rows, hipStream_t s);
+int rows_decode_u4_range(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, const uint32_t* d_esc,
+                         uint32_t cap, const uint32_t* d_esc_n, uint64_t row0, uint64_t nrows, uint32_t* d_rows,
+                         hipStream_t s);
 
 // ---- sparse path (kmh_sparse.hip) ----
 // Counts the windows of d_seq[0, n) for 13 <= k <= 32 (works for any 1 <= k <= 32).

@@ -226,11 +226,13 @@ unsigned grid_waves(uint64_t n4) {   // 256-thread blocks, one 512-group step pe
 __global__ __launch_bounds__(256) void k_apply_escapes_u4(const uint32_t* __restrict__ esc,
                                                           uint32_t cap,
                                                           const uint32_t* __restrict__ esc_n,
-                                                          uint64_t cells, uint32_t* __restrict__ rows) {
+                                                          uint64_t lo, uint64_t hi, uint32_t* __restrict__ rows) {
+    // escapes whose block index lies in [lo, hi) land at rows[index - lo]; the others (other
+    // rows of the block, or garbage in a slot that came off the wire) are ignored
     const uint32_t n = min(*esc_n, cap);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t idx = esc[2 * (uint64_t)i];
-        if (idx < cells) rows[idx] = esc[2 * (uint64_t)i + 1];   // never trust a slot off the wire
+        const uint64_t idx = esc[2 * (uint64_t)i];
+        if (idx >= lo && idx < hi) rows[idx - lo] = esc[2 * (uint64_t)i + 1];
     }
 }
 
@@ -301,18 +303,26 @@ int rows_encode_u4(Ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t col
 
 int rows_decode_u4(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, const uint32_t* d_esc,
                    uint32_t cap, const uint32_t* d_esc_n, uint32_t* d_rows, hipStream_t s) {
+    return rows_decode_u4_range(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, 0, rows, d_rows, s);
+}
+
+int rows_decode_u4_range(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols, const uint32_t* d_esc,
+                         uint32_t cap, const uint32_t* d_esc_n, uint64_t row0, uint64_t nrows, uint32_t* d_rows,
+                         hipStream_t s) {
     if (!d_u4 || !d_rows || !d_esc_n || (cap && !d_esc)) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
     if (cols % 32 != 0) return fail(ctx, KMH_ERR_INVALID, "cols must be a multiple of 32");
     if (rows * cols >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "u4 blocks must hold fewer than 2^32 - 1 cells");
-    const uint64_t n32 = rows * cols / 32;
+    if (row0 > rows || nrows > rows - row0) return fail(ctx, KMH_ERR_INVALID, "row range outside the block");
+    const uint64_t n32 = nrows * cols / 32;
     if (n32 == 0) return KMH_OK;
     time_begin(ctx, s, "k_decode_u4");
     hipLaunchKernelGGL(k_decode_u4w, dim3(grid_waves(8 * n32)), dim3(256), 0, s,
-                           reinterpret_cast<const uint16_t*>(d_u4), 8 * n32, d_rows);  // 8 four-count groups per 32 counts
+                       reinterpret_cast<const uint16_t*>(d_u4 + row0 * cols / 2), 8 * n32, d_rows);  // 8 four-count groups per 32 counts
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (cap > 0) {
-        hipLaunchKernelGGL(k_apply_escapes_u4, dim3(64), dim3(256), 0, s, d_esc, cap, d_esc_n, rows * cols, d_rows);
+        hipLaunchKernelGGL(k_apply_escapes_u4, dim3(64), dim3(256), 0, s, d_esc, cap, d_esc_n, row0 * cols,
+                           (row0 + nrows) * cols, d_rows);
         KMH_HIP(ctx, hipGetLastError());
     }
     return KMH_OK;

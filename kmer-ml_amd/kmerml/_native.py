@@ -59,6 +59,8 @@ SIGNATURES = [
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
     ("kmh_rows_encode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
     ("kmh_rows_decode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _vp, _vp]),
+    ("kmh_rows_decode_u4_range_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _u64, _u64,
+                                                _vp, _vp]),
     ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
                                           _u64, _vp, _vp]),
 ]
@@ -224,6 +226,12 @@ class Context:
                                             ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
                                             ctypes.c_void_p(d_rows),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def rows_decode_u4_range(self, d_u4, rows, cols, d_esc, cap, d_esc_n, row0, nrows, d_rows, stream=None):
+        _check(lib().kmh_rows_decode_u4_range_dev(self._h, ctypes.c_void_p(d_u4), int(rows), int(cols),
+                                                  ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
+                                                  int(row0), int(nrows), ctypes.c_void_p(d_rows),
+                                                  ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- kernel timing --
     def timing(self, enable):

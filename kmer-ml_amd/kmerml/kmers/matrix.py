@@ -136,12 +136,78 @@ def escape_count(word_bytes):
     return word_bytes.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
 
 
-def gather_rows_u4(padded, group=None):
+class AssembledMatrix:
+    """The assembled [G, cols] count matrix on one rank, kept as the all-gathered u4 slots
+    (two counts per byte + each rank's exact escape list) instead of widened u32 rows: 8x less
+    HBM per rank, and no widening pass in the step.  Exact: rows(lo, hi) widens any range of
+    rows on the device (kmh_rows_decode_u4_range_dev applies exactly their escapes); dense()
+    widens everything.  Rows are genomes in input order (rank r holds block shard_bounds(G, W, r)
+    in slot r of `recv`), as in the reference's organisms x k-mers matrix (features.py:85-117).
+    A matrix that had to fall back to a dense wire format wraps the dense tensor instead."""
+
+    def __init__(self, G, cols, world, B, recv=None, cap=0, P=0, dense=None):
+        self.G, self.cols, self.world, self.B = G, cols, world, B
+        self.recv, self.cap, self.P, self._dense = recv, cap, P, dense
+        self.wire = "u4" if dense is None else LAST_WIRE
+
+    @property
+    def shape(self):
+        return (self.G, self.cols)
+
+    def _slot_rows(self, q):
+        lo, hi = shard_bounds(self.G, self.world, q)
+        return lo, hi
+
+    def rows(self, lo, hi, stream=None):
+        """Rows [lo, hi) as a new device int32 tensor (u32 counts)."""
+        import torch
+
+        if not 0 <= lo <= hi <= self.G:
+            raise IndexError(f"rows [{lo}, {hi}) outside [0, {self.G})")
+        if self._dense is not None:
+            idx = []
+            for g in range(lo, hi):
+                q = self._rank_of(g)
+                idx.append(q * self.B + g - self._slot_rows(q)[0])
+            return self._dense[torch.tensor(idx, dtype=torch.long, device=self._dense.device)]
+        dev = self.recv.device
+        out = torch.empty((hi - lo, self.cols), dtype=torch.int32, device=dev)
+        ctx = _native.context(dev.index)
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        nib = self.B * self.cols // 2
+        g = lo
+        while g < hi:
+            q = self._rank_of(g)
+            qlo, qhi = self._slot_rows(q)
+            n = min(hi, qhi) - g
+            slot = self.recv.data_ptr() + q * self.P
+            ctx.rows_decode_u4_range(slot, self.B, self.cols, slot + nib + 16, self.cap, slot + nib,
+                                     g - qlo, n, out[g - lo:].data_ptr(), s)
+            g += n
+        return out
+
+    def row(self, g):
+        return self.rows(g, g + 1)[0]
+
+    def dense(self):
+        """The whole [G, cols] matrix widened to int32 (u32 counts)."""
+        return self.rows(0, self.G)
+
+    def _rank_of(self, g):
+        for q in range(self.world):
+            lo, hi = shard_bounds(self.G, self.world, q)
+            if lo <= g < hi:
+                return q
+        raise IndexError(g)
+
+
+def gather_rows_u4(padded, group=None, compact=False, G=None):
     """All-gather [B, cols] u32 rows (device int32 tensor) from every rank as u4 + escapes.
 
     Exact for any counts: values >= 15 travel in the escape list.  If any rank has more
     escapes than the slot holds, every rank falls back to the u8 path (and from there, if
-    needed, to the plain u32 all-gather).
+    needed, to the plain u32 all-gather).  compact=True returns an AssembledMatrix of G rows
+    that keeps the gathered slots (no widening); otherwise the padded [W * B, cols] rows.
     """
     import torch
     import torch.distributed as dist
@@ -158,10 +224,14 @@ def gather_rows_u4(padded, group=None):
                        cap, send[nib:].data_ptr(), s)
     n = _all_reduce_max(escape_count(send[nib:nib + 4]), group)
     if int(n.item()) > cap:
-        return gather_rows_u8(padded, group)
+        del send
+        out = gather_rows_u8(padded, group)
+        return AssembledMatrix(G, cols, world, B, dense=out) if compact else out
     global LAST_WIRE
     LAST_WIRE = "u4"
     recv = _all_gather(torch.empty(world * P, dtype=torch.uint8, device=dev), send, group)
+    if compact:
+        return AssembledMatrix(G if G is not None else world * B, cols, world, B, recv=recv, cap=cap, P=P)
     out = torch.empty((world * B, cols), dtype=padded.dtype, device=dev)
     base = recv.data_ptr()
     for q in range(world):
@@ -206,7 +276,7 @@ def gather_rows_u8(padded, group=None):
     return out
 
 
-def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
+def count_matrix(genome_files, k, device=None, group=None, count_fn=None, compact=False):
     """Dense [G, 4^k] count matrix of `genome_files` (torch tensor, int32 storage of u32).
 
     Without an initialised torch.distributed process group this counts every genome on
@@ -214,6 +284,8 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
     all-gathered (u4 rows + exact escapes on the wire for k >= 3, u8 for k = 2), so every rank
     returns the full matrix in input order.
     count_fn(files, k) -> tensor [len(files), 4^k] replaces the HIP counter (tests).
+    compact=True (process group, u4 wire): return an AssembledMatrix that keeps the gathered u4
+    slots and widens rows on access, instead of the dense [G, 4^k] tensor.
     """
     import torch
     import torch.distributed as dist
@@ -235,6 +307,8 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None):
     padded = torch.zeros((B, 1 << (2 * k)), dtype=local.dtype, device=local.device)
     padded[: hi - lo] = local
     if padded.is_cuda and B and padded.shape[1] % 32 == 0 and B * padded.shape[1] < 2**32 - 1:
+        if compact:
+            return gather_rows_u4(padded, group, compact=True, G=G)
         gathered = gather_rows_u4(padded, group)
     elif padded.is_cuda and B and padded.shape[1] % 16 == 0:
         gathered = gather_rows_u8(padded, group)

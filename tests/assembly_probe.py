@@ -6,7 +6,8 @@ rank's own rows (bench.check_assembly); rank 0 writes result.json (wire format u
 result) and the assembled rows of genomes 0 and G - 1.  The first REPEAT_BYTES of genome 0
 are overwritten with a period-8 repeat (REPEAT), so its block has counts far above 255 (u8 and
 u4 escapes with large values).
-Usage: assembly_probe.py OUT_DIR G L K BACKEND [--single-device]"""
+--compact keeps the matrix in the AssembledMatrix form (u4 slots, rows widened on access).
+Usage: assembly_probe.py OUT_DIR G L K BACKEND [--single-device] [--compact]"""
 import json
 import os
 import sys
@@ -57,7 +58,21 @@ def main():
             offsets = np.arange(hi - lo + 1, dtype=np.uint64) * np.uint64(stride)
             ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, padded.data_ptr(), s)
         del d_seq
-        full = kmatrix.gather_rows_u4(padded, None)
+        if "--compact" in sys.argv:
+            am = kmatrix.gather_rows_u4(padded, None, compact=True, G=G)
+            assert am.shape == (G, bins)
+            full = torch.zeros((world * B, bins), dtype=torch.int32, device=dev)
+            for q in range(world):
+                qlo, qhi = kmatrix.shard_bounds(G, world, q)
+                full[q * B:q * B + (qhi - qlo)] = am.rows(qlo, qhi)
+            # single rows and a range across a slot boundary agree with the block widening
+            assert torch.equal(am.row(G - 1), full[(world - 1) * B + (G - 1 - kmatrix.shard_bounds(G, world, world - 1)[0])])
+            if G >= 2:
+                mid = kmatrix.shard_bounds(G, world, 0)[1]
+                a0, a1 = max(0, mid - 1), min(G, mid + 1)
+                assert torch.equal(am.rows(a0, a1), torch.cat([am.row(g)[None] for g in range(a0, a1)]))
+        else:
+            full = kmatrix.gather_rows_u4(padded, None)
         torch.cuda.synchronize()
         ok = check_assembly(full, padded[:hi - lo], B, G, world, rank, k, out)
         okt = torch.tensor([int(ok)], dtype=torch.int32)

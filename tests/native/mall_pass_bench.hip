@@ -129,6 +129,23 @@ int main() {
         (void)hipEventRecord(e[4]);
         (void)hipEventSynchronize(e[4]);
         const float dd = ms(e[3], e[4]);
+        // E: batches of gb genomes through an exchange region of gb x 211 MB that every batch
+        //    reuses (a small address footprint for the exchange writes)
+        for (int gb : {1, 2, 4, 8}) {
+            (void)hipEventRecord(e[3]);
+            for (int b0 = 0; b0 < G; b0 += gb) {
+                for (int g = b0; g < b0 + gb && g < G; ++g)
+                    hipLaunchKernelGGL(k_part, dim3(grid), dim3(256), 0, 0, gen + (size_t)g * L / 16, L / 16,
+                                       xa + (size_t)(g - b0) * X / 16, X / 16, sink);
+                for (int g = b0; g < b0 + gb && g < G; ++g)
+                    hipLaunchKernelGGL(k_count, dim3(grid), dim3(256), 0, 0, xa + (size_t)(g - b0) * X / 16,
+                                       X / 16, rows + (size_t)g * ROW / 16, ROW / 16, sink);
+            }
+            (void)hipEventRecord(e[4]);
+            (void)hipEventSynchronize(e[4]);
+            printf("rep %d  E(batch %d, exchange region %d MB): %.1f us/genome\n", rep, gb, (int)(gb * X >> 20),
+                   ms(e[3], e[4]) * 1e3 / G);
+        }
         printf("rep %d  A: part %.1f + count %.1f us/genome = %.1f   B: part %.1f + count %.1f = %.1f us/genome"
                "   B back-to-back %.1f   C (one resident buffer) back-to-back %.1f   A back-to-back %.1f us/genome\n",
                rep, pa * 1e3 / G, ca * 1e3 / G, (pa + ca) * 1e3 / G, pb * 1e3 / G, cb * 1e3 / G,

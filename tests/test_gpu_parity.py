@@ -663,7 +663,7 @@ def test_bench_pipelined_u4_assembly_rccl():
     assert d["rows_checked"] is True and d["config"]["assembly"] == "u4"
 
 
-@pytest.mark.parametrize("wire", ["u4", "u8"])
+@pytest.mark.parametrize("wire", ["u4", "u4-dense", "u8"])
 def test_bench_pipelined_assembly_two_ranks(wire):
     """Two ranks on the one GPU (gloo for the collectives, --single-device): every rank widens
     the other rank's slot, so the assembled matrices pass the row-sum check only if decoding,
@@ -677,6 +677,57 @@ def test_bench_pipelined_assembly_two_ranks(wire):
     assert d["rows_checked"] is True and d["n_gpus"] == 2 and d["config"]["assembly"] == wire
 
 
+def test_rows_decode_u4_range(ctx, dev):
+    """kmh_rows_decode_u4_range_dev (the AssembledMatrix row accessor): any row range of a u4
+    block widens to exactly those rows, escapes included (values 15 .. 2^32 - 1)."""
+    rng = np.random.default_rng(11)
+    B, cols = 5, 2048
+    rows = rng.poisson(6, size=(B, cols)).astype(np.uint32)
+    rows[1, 7] = 15
+    rows[3, 100] = 2**32 - 1
+    rows[4, cols - 1] = 70_000
+    d = torch.from_numpy(rows.view(np.int32)).to(dev)
+    cap, P = kmatrix.slot_layout_u4(B, cols)
+    slot = torch.zeros(P, dtype=torch.uint8, device=dev)
+    nib = B * cols // 2
+    ctx.rows_encode_u4(d.data_ptr(), B, cols, slot.data_ptr(), slot[nib + 16:].data_ptr(), cap, slot[nib:].data_ptr())
+    for r0, n in [(0, 5), (1, 2), (4, 1), (3, 2), (2, 0)]:
+        out = torch.full((max(n, 1), cols), -1, dtype=torch.int32, device=dev)
+        ctx.rows_decode_u4_range(slot.data_ptr(), B, cols, slot[nib + 16:].data_ptr(), cap, slot[nib:].data_ptr(),
+                                 r0, n, out.data_ptr())
+        torch.cuda.synchronize()
+        if n:
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), rows[r0:r0 + n])
+    with pytest.raises(ValueError):
+        ctx.rows_decode_u4_range(slot.data_ptr(), B, cols, slot[nib + 16:].data_ptr(), cap, slot[nib:].data_ptr(),
+                                 4, 2, out.data_ptr())
+
+
+@pytest.mark.parametrize("caps,wire", [({}, "u4"), ({"KMH_ESC_CAP_U4": "0"}, "u8")])
+def test_assembled_matrix_compact_two_ranks(tmp_path, caps, wire):
+    """count_matrix's compact form (AssembledMatrix: the gathered u4 slots, rows widened on
+    access) on two ranks sharing the GPU: every row range equals the ranks' own rows; a forced
+    u4 overflow wraps the u8 result instead."""
+    env = dict(os.environ, **caps)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = _torchrun([os.path.join(here, "assembly_probe.py"), str(tmp_path), "5", "2000000", "10", "gloo",
+                   "--single-device", "--compact"], nproc=2, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.load(open(tmp_path / "result.json"))
+    assert res == {"wire": wire, "assembly_checked": True, "world": 2}
+
+
+def test_bench_simulated_rank():
+    """bench.py --simulate-ranks: one process doing one rank's share of config 4 (compact u4
+    assembly, the all-gather's writes modelled by device copies), labelled as a projection."""
+    r = _torchrun(["bench.py", "--simulate-ranks", "4", "--genomes", "8", "--genome-len", "3000000",
+                   "--steps", "3", "--warmup", "1", "--cpu-sample", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["rows_checked"] is True and d["simulated_ranks"] == 4
+    assert d["config"]["workload"].startswith("projection")
+
+
 def _synth_row(oracle_lib, g, L=100_000_000, k=12, repeat=None):
     seq = oracle_lib.synth(L, osynth.genome_seed(g))
     if repeat:
@@ -685,7 +736,7 @@ def _synth_row(oracle_lib, g, L=100_000_000, k=12, repeat=None):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("wire", ["u4", "u8"])
+@pytest.mark.parametrize("wire", ["u4", "u4-dense", "u8"])
 def test_config4_per_rank_workload_eight_ranks(tmp_path, oracle_lib, wire):
     """Config 4 at its real per-rank size, eight ranks sharing the one MI355X (gloo for the
     collectives): 64 synthetic 100 Mbp genomes at k = 12, 8 per rank, every step's matrix
