@@ -60,6 +60,9 @@ def parse():
                         "on access, kmerml.kmers.matrix.AssembledMatrix); u4-dense / u8: the same "
                         "wire, every gathered row widened to the u32 matrix on every rank each step; "
                         "u32 = plain all-gather of the u32 rows after each count")
+    p.add_argument("--separate-encode", action="store_true",
+                   help="compact u4 assembly: count, then encode in a second pass (A/B of the fused "
+                        "kmh_count_dense_u4_dev)")
     p.add_argument("--simulate-ranks", type=int, default=0,
                    help="one process on one GPU doing what ONE rank of N does per step at config 4 "
                         "(count G/N genomes, encode u4, and the all-gather's writes modelled as N "
@@ -305,12 +308,14 @@ def main():
     full = torch.empty((world * B, bins), dtype=torch.int32, device=dev) if mode == "u32" else None
     t_count = []
 
-    def count_into(buf, record):
+    def count_into(buf, record, u4=None):
         e0 = torch.cuda.Event(enable_timing=True) if record else None
         e1 = torch.cuda.Event(enable_timing=True) if record else None
         if record:
             e0.record(stream)
-        if g_local:
+        if g_local and u4 is not None:
+            ctx.count_dense_u4_dev(d_seq.data_ptr(), offsets, k, buf.data_ptr(), *u4, s)
+        elif g_local:
             ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, buf.data_ptr(), s)
         if record:
             e1.record(stream)
@@ -338,10 +343,14 @@ def main():
                 w = inflight[b]
                 stream.wait_event(w) if isinstance(w, torch.cuda.Event) else w.wait()
                 inflight[b] = None
-            count_into(local, record)
             sb = send[b]
-            ctx.rows_encode_u4(local.data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
-                               cap, sb[payload:].data_ptr(), s)
+            if a.separate_encode or not g_local:
+                count_into(local, record)
+                ctx.rows_encode_u4(local.data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
+                                   cap, sb[payload:].data_ptr(), s)
+            else:   # count + u4 encode in one pass (kmh_count_dense_u4_dev)
+                count_into(local, record, u4=(sb.data_ptr(), sb[payload + 16:].data_ptr(), cap,
+                                              sb[payload:].data_ptr()))
             if sim:   # the gather's HBM side: every slot of recv written from this rank's slot
                 side.wait_stream(stream)
                 with torch.cuda.stream(side):

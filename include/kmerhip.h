@@ -192,6 +192,15 @@ int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uin
 int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
                            uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n,
                            void* stream);
+/* kmh_count_dense_dev into d_matrix (G x 4^k u32) and, in the same pass, the u4 encoding of
+ * those rows exactly as kmh_rows_encode_u4_dev(d_matrix, G, 4^k, ...) would write it: for
+ * k >= 10 the count kernel writes each bucket's nibbles and escapes straight from its LDS
+ * table (no second pass over the rows).  3 <= k <= 12, G * 4^k < 2^32 - 1.  The multi-GPU
+ * step's count + encode (each rank's slot of the all-gather that assembles the matrix of
+ * /root/reference/kmerml/ml/features.py:85-117). */
+int kmh_count_dense_u4_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                           uint32_t* d_matrix, uint8_t* d_u4, uint32_t* d_esc, uint32_t cap,
+                           uint32_t* d_esc_n, void* stream);
 /* Widen one block of u4 rows (rows x cols) to u32 at d_rows and apply its escapes (pairs with an
  * index outside the block are ignored: a slot that came off the wire never writes elsewhere). */
 int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,

@@ -291,6 +291,16 @@ int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uin
     return kmh::rows_decode_u4(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, pick_stream(ctx, stream));
 }
 
+int kmh_count_dense_u4_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                           uint32_t* d_matrix, uint8_t* d_u4, uint32_t* d_esc, uint32_t cap,
+                           uint32_t* d_esc_n, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::dense_count_u4(ctx, d_seq, offsets, G, k, d_matrix, d_u4, d_esc, cap, d_esc_n,
+                               pick_stream(ctx, stream));
+}
+
 int kmh_rows_decode_u4_range_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
                                  const uint32_t* d_esc, uint32_t cap, const uint32_t* d_esc_n,
                                  uint64_t row0, uint64_t nrows, uint32_t* d_rows, void* stream) {

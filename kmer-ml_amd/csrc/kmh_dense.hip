@@ -395,12 +395,27 @@ __device__ __forceinline__ void log_wrap(const FixLog& L, uint64_t row0, uint32_
     }
 }
 
+// Fused u4 encoding of the count rows (kmh_count_dense_u4_dev): the same block layout as
+// rows_encode_u4 -- nibbles of row g at byte g * 4^k / 2 (element 2i in the low nibble of
+// byte i), every count >= 15 as an exact (g * 4^k + column, value) pair behind *esc_n.  A
+// bucket whose u16 table wrapped is left to k_reencode (listed in redo), which encodes it
+// from the corrected u32 row after k_fixup.
+struct U4Out {
+    uint32_t* nib;       // u4 block as u32 words (8 counts each)
+    uint32_t* esc;       // (index, value) pairs
+    uint32_t cap;
+    uint32_t* esc_n;
+    uint32_t* redo;      // redo[0] = buckets listed; redo[1 + i] = g * NBK + b
+};
+
+__device__ __forceinline__ uint32_t sat4(uint32_t x) { return x < 15u ? x : 15u; }
+
 // The first nv entries of one 16-byte chunk (8 suffixes) into the table; the other slots add 0
 // (branch-free).  The eight returning adds go out back to back; a wrap (an added-to half that
 // held 0xFFFF) is looked for once per chunk through the maximum of the returned halves (an
 // add-0 slot at 0xFFFF is a false alarm that the rare path sorts out).
 __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv, const FixLog& L,
-                                            uint64_t row0) {
+                                            uint64_t row0, uint32_t* wrapped) {
     const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
     uint32_t old[8], off[8];
 #pragma unroll
@@ -421,8 +436,10 @@ __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv,
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t v = (wd[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-            if ((uint32_t)i < nv && __builtin_amdgcn_ubfe(old[i], off[i], 16) == 0xFFFFu)
+            if ((uint32_t)i < nv && __builtin_amdgcn_ubfe(old[i], off[i], 16) == 0xFFFFu) {
                 log_wrap(L, row0, v, old[i]);
+                *wrapped = 1u;   // this bucket's table no longer holds exact counts
+            }
         }
     }
 }
@@ -446,10 +463,10 @@ constexpr int batch_tiles(int qmax) {
 // queue (chunk index relative to the batch, entries used in the chunk) and streams the queue
 // with all 64 lanes active: U loads in flight per lane, 8 LDS adds per load.  A batch whose
 // chunks overflow the queue (skewed input) is walked lane by lane instead.
-template <int K, int U>
+template <int K, int U, bool ENC>
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, uint32_t ldt, GenomeMap m,
-    int S, uint32_t* __restrict__ out, FixLog L) {
+    int S, uint32_t* __restrict__ out, FixLog L, U4Out E) {
     constexpr int NBK = num_buckets<K>();
     constexpr uint32_t CPT = tile_cap<K>() / 8;   // chunks per tile
     constexpr int NW = kCountThreads / 64;
@@ -458,7 +475,8 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     static_assert((uint32_t)BT * CPT <= (1u << 20), "queue entries hold 20-bit chunk indices");
     constexpr int WORDS = (int)kCBins / 2;
     __shared__ __attribute__((aligned(16))) uint32_t tbl[WORDS];
-    __shared__ uint32_t queue[NW][QMAX];
+    __shared__ uint32_t queue[NW][QMAX];     // chunk queues; escape staging of the epilogue
+    __shared__ uint32_t wrapped, ecnt, ebase;
 
     const uint32_t w = xcd_work_id();
     const int s = (int)(w % (uint32_t)S);
@@ -473,6 +491,10 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
 
     uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
     for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x == 0) {
+        wrapped = 0u;
+        ecnt = 0u;
+    }
     __syncthreads();
 
     uint32_t* q = queue[wave];
@@ -513,18 +535,28 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if ((uint32_t)(u * 64 + lane) < total) count_chunk(tbl, v[u], (qe[u] >> 20) + 1u, L, row0);
+                if ((uint32_t)(u * 64 + lane) < total) count_chunk(tbl, v[u], (qe[u] >> 20) + 1u, L, row0, &wrapped);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {
             if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
-            for (uint32_t j = 0; j < nc; ++j) count_chunk(tbl, chunks[cbat + crel + j], j + 1 == nc ? nlast : 8u, L, row0);
+            for (uint32_t j = 0; j < nc; ++j)
+                count_chunk(tbl, chunks[cbat + crel + j], j + 1 == nc ? nlast : 8u, L, row0, &wrapped);
         }
     }
     __syncthreads();
 
-    // Widen the u16 pairs into the u32 row slice (plain stores, or adds when split).
+    // Widen the u16 pairs into the u32 row slice (plain stores, or adds when split).  ENC (S = 1
+    // only): also the slice's u4 nibbles (one u32 of 8 counts per thread and step) and its
+    // escapes, staged in the LDS of the queues and appended behind one global atomic.
+    constexpr uint32_t kStage = (uint32_t)(NW * QMAX) / 2;   // (index, value) pairs
+    uint32_t* stage = &queue[0][0];
+    const bool enc = ENC && wrapped == 0u;                     // uniform
+    if (ENC && wrapped != 0u && threadIdx.x == 0) {            // k_reencode redoes this bucket
+        const uint32_t at = atomicAdd(E.redo, 1u);
+        E.redo[1 + at] = (uint32_t)g * NBK + b;
+    }
     uint32_t* orow = out + row0;
     for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
         const uint4 x = tbl4[i];
@@ -533,11 +565,82 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         if (S == 1) {
             store_nt(reinterpret_cast<uint4*>(orow) + 2 * i, lo4);
             store_nt(reinterpret_cast<uint4*>(orow) + 2 * i + 1, hi4);
+            if (enc) {
+                const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                uint32_t w = 0u, ne = 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    w |= sat4(e[j]) << (4 * j);
+                    ne += e[j] >= 15u ? 1u : 0u;
+                }
+                E.nib[row0 / 8 + (uint64_t)i] = w;
+                if (ne) {   // ~1 in 100 threads for uniform 100 Mbp genomes at k = 12
+                    uint32_t at = atomicAdd(&ecnt, ne);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if (e[j] >= 15u) {
+                            const uint32_t idx = (uint32_t)(row0 + 8 * (uint64_t)i + j);
+                            if (at < kStage) {
+                                stage[2 * at] = idx;
+                                stage[2 * at + 1] = e[j];
+                            } else {   // a skewed bucket: past the staging, one global atomic each
+                                const uint32_t gat = atomicAdd(E.esc_n, 1u);
+                                if (gat < E.cap) {
+                                    E.esc[2 * (uint64_t)gat] = idx;
+                                    E.esc[2 * (uint64_t)gat + 1] = e[j];
+                                }
+                            }
+                            ++at;
+                        }
+                    }
+                }
+            }
         } else if (ta < tb) {
             const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if (e[j]) atomicAdd(&orow[8 * i + j], e[j]);
+        }
+    }
+    if (ENC) {
+        __syncthreads();
+        const uint32_t n = min(ecnt, kStage);
+        if (enc && threadIdx.x == 0) ebase = n ? atomicAdd(E.esc_n, n) : 0u;
+        __syncthreads();
+        if (enc)
+            for (uint32_t i = threadIdx.x; i < n; i += kCountThreads)
+                if (ebase + i < E.cap) {
+                    E.esc[2 * (uint64_t)(ebase + i)] = stage[2 * i];
+                    E.esc[2 * (uint64_t)(ebase + i) + 1] = stage[2 * i + 1];
+                }
+    }
+}
+
+// u4 encoding of the buckets whose u16 table wrapped (listed by k_bucket_count<ENC>), from the
+// u32 rows after k_fixup: one workgroup per listed bucket, escapes one global atomic each
+// (such buckets hold counts >= 65536: rare, and exact either way).
+template <int K>
+__global__ __launch_bounds__(256) void k_reencode(const uint32_t* __restrict__ rows, U4Out E) {
+    constexpr int NBK = num_buckets<K>();
+    const uint32_t n = E.redo[0];
+    for (uint32_t it = blockIdx.x; it < n; it += gridDim.x) {
+        const uint32_t gb = E.redo[1 + it];
+        const uint64_t row0 = (uint64_t)(gb / NBK) * (1ull << (2 * K)) + (uint64_t)(gb % NBK) * kCBins;
+        for (uint32_t i = threadIdx.x; i < kCBins / 8; i += 256) {
+            uint32_t w = 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t v = rows[row0 + 8 * i + j];
+                w |= sat4(v) << (4 * j);
+                if (v >= 15u) {
+                    const uint32_t at = atomicAdd(E.esc_n, 1u);
+                    if (at < E.cap) {
+                        E.esc[2 * (uint64_t)at] = (uint32_t)(row0 + 8 * i + j);
+                        E.esc[2 * (uint64_t)at + 1] = v;
+                    }
+                }
+            }
+            E.nib[row0 / 8 + i] = w;
         }
     }
 }
@@ -624,7 +727,7 @@ int run_direct(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* 
 
 template <int K>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
-                    const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s) {
+                    const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s, const U4Out* enc) {
     constexpr int NBK = num_buckets<K>();
     constexpr int U = 6;                  // chunk loads in flight per lane (queue = 64 U)
     const size_t row = (size_t)1 << (2 * K);
@@ -680,7 +783,8 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
         for (int q = g; q < h; ++q) maxt = std::max<uint64_t>(maxt, L.tbase[q + 1] - L.tbase[q]);
         // splits per (genome, bucket): at least kTargetWorkgroups count workgroups
         const uint64_t want = ((uint64_t)kTargetWorkgroups + (uint64_t)nG * NBK - 1) / ((uint64_t)nG * NBK);
-        const int S = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxt, 1)));
+        // (the fused u4 encoding needs each bucket in one workgroup: S = 1)
+        const int S = enc ? 1 : (int)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxt, 1)));
         if (S > 1) KMH_HIP(ctx, hipMemsetAsync(d_out + (size_t)g * row, 0, (size_t)nG * row * sizeof(uint32_t), s));
         if (tiles) {
             time_begin(ctx, s, "k_partition");
@@ -690,8 +794,12 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
             KMH_HIP(ctx, hipGetLastError());
         }
         time_begin(ctx, s, "k_bucket_count");
-        hipLaunchKernelGGL((k_bucket_count<K, U>), dim3((unsigned)(nG * NBK * S)), dim3(kCountThreads), 0, s,
-                           suf, toff, ldt, m, S, d_out, fl);
+        if (enc)
+            hipLaunchKernelGGL((k_bucket_count<K, U, true>), dim3((unsigned)(nG * NBK * S)), dim3(kCountThreads), 0,
+                               s, suf, toff, ldt, m, S, d_out, fl, *enc);
+        else
+            hipLaunchKernelGGL((k_bucket_count<K, U, false>), dim3((unsigned)(nG * NBK * S)), dim3(kCountThreads), 0,
+                               s, suf, toff, ldt, m, S, d_out, fl, U4Out{});
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
         g = h;
@@ -700,19 +808,23 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
     hipLaunchKernelGGL(k_fixup, dim3(64), dim3(256), 0, s, fl, d_out);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
+    if (enc) {
+        hipLaunchKernelGGL(k_reencode<K>, dim3(64), dim3(256), 0, s, d_out, *enc);
+        KMH_HIP(ctx, hipGetLastError());
+    }
     return KMH_OK;
 }
 
 template <int K>
 int count_k(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, uint32_t* d_out,
-            hipStream_t s) {
+            hipStream_t s, const U4Out* enc) {
     Layout L;
     const uint64_t *d_goff, *d_tbase;
     int rc = make_layout(ctx, offsets, G, K, K <= 9 ? (uint64_t)kTile : (uint64_t)kPTile, L);
     if (!rc) rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
     if (rc) return rc;
     if constexpr (K <= 9) return run_direct<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
-    else return run_partitioned<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s);
+    else return run_partitioned<K>(ctx, d_seq, L, d_goff, d_tbase, G, d_out, s, enc);
 }
 
 template <int K>
@@ -758,8 +870,31 @@ int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, 
                 uint32_t* d_out, hipStream_t s) {
     if (k < 1 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "dense counting needs 1 <= k <= 12");
     if (!d_seq || !d_out) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
-    KMH_DISPATCH_K(count_k, k, ctx, d_seq, offsets, G, d_out, s);
+    KMH_DISPATCH_K(count_k, k, ctx, d_seq, offsets, G, d_out, s, nullptr);
     return fail(ctx, KMH_ERR_UNSUPPORTED, "unsupported k");
+}
+
+int dense_count_u4(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, uint32_t* d_out,
+                   uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, hipStream_t s) {
+    if (k < 3 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "the fused u4 count needs 3 <= k <= 12");
+    if (!d_seq || !d_out || !d_u4 || !d_esc_n || (cap && !d_esc)) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    const uint64_t cols = 1ull << (2 * k);
+    if (G < 1 || (uint64_t)G * cols >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "u4 blocks must hold fewer than 2^32 - 1 cells");
+    if (k <= 9) {   // k_direct has no per-bucket epilogue: count, then the encoder
+        int rc = dense_count(ctx, d_seq, offsets, G, k, d_out, s);
+        return rc ? rc : rows_encode_u4(ctx, d_out, (uint64_t)G, cols, d_u4, d_esc, cap, d_esc_n, s);
+    }
+    const size_t redo_bytes = (1 + (size_t)G * (cols >> kCBits)) * sizeof(uint32_t);
+    int rc = ensure(ctx, ctx->redo, redo_bytes);
+    if (rc) return rc;
+    U4Out E{reinterpret_cast<uint32_t*>(d_u4), d_esc, cap, d_esc_n, static_cast<uint32_t*>(ctx->redo.ptr)};
+    KMH_HIP(ctx, hipMemsetAsync(d_esc_n, 0, sizeof(uint32_t), s));
+    KMH_HIP(ctx, hipMemsetAsync(E.redo, 0, sizeof(uint32_t), s));
+    switch (k) {
+    case 10: return count_k<10>(ctx, d_seq, offsets, G, d_out, s, &E);
+    case 11: return count_k<11>(ctx, d_seq, offsets, G, d_out, s, &E);
+    default: return count_k<12>(ctx, d_seq, offsets, G, d_out, s, &E);
+    }
 }
 
 int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,

@@ -39,7 +39,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // device workspace
-    DevBuf seq, suf, toff, meta, out, out2, fix, sparse[8], order;
+    DevBuf seq, suf, toff, meta, out, out2, fix, redo, sparse[8], order;
     // pinned staging for small host->device tables
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
@@ -89,6 +89,10 @@ size_t env_mb(const char* name, size_t dflt);
 
 // ---- dense path (kmh_dense.hip) ----
 // offsets: host, G+1 entries.  d_out: G x 4^k u32.
+// dense_count plus the u4 encoding of the rows (rows_encode_u4's layout), fused into the
+// count kernel's epilogue for k >= 10.
+int dense_count_u4(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, uint32_t* d_out,
+                   uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, hipStream_t s);
 int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                 uint32_t* d_out, hipStream_t s);
 int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,

@@ -89,6 +89,51 @@ def test_dense_low_complexity(ctx, dev, oracle_lib, k):
         assert np.array_equal(rows[g], oracle_lib.count_dense(seq, k)), (k, g)
 
 
+def _u4_block(ctx, dev, genomes, k, fused):
+    """(u32 rows, nibbles, sorted escape pairs, escape count) of count + u4 encode, either fused
+    (kmh_count_dense_u4_dev) or as two passes (kmh_count_dense_dev + kmh_rows_encode_u4_dev)."""
+    buf, offs = _layout(genomes)
+    d_seq = torch.from_numpy(buf.copy()).to(dev)
+    G, cols = len(genomes), 1 << (2 * k)
+    cap, P = kmatrix.slot_layout_u4(G, cols)
+    nib = G * cols // 2
+    out = torch.full((G, cols), -7, dtype=torch.int32, device=dev)
+    slot = torch.zeros(P, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    if fused:
+        ctx.count_dense_u4_dev(d_seq.data_ptr(), offs, k, out.data_ptr(), slot.data_ptr(),
+                               slot[nib + 16:].data_ptr(), cap, slot[nib:].data_ptr(), s)
+    else:
+        ctx.count_dense_dev(d_seq.data_ptr(), offs, k, out.data_ptr(), s)
+        ctx.rows_encode_u4(out.data_ptr(), G, cols, slot.data_ptr(), slot[nib + 16:].data_ptr(), cap,
+                           slot[nib:].data_ptr(), s)
+    torch.cuda.synchronize()
+    h = slot.cpu().numpy()
+    n = int(h[nib:nib + 4].view(np.uint32)[0])
+    esc = h[nib + 16:nib + 16 + 8 * min(n, cap)].view(np.uint32).reshape(-1, 2)
+    esc = esc[np.lexsort((esc[:, 1], esc[:, 0]))]
+    return out.cpu().numpy().view(np.uint32), h[:nib], esc, n
+
+
+@pytest.mark.parametrize("k", [8, 10, 12])
+def test_count_dense_u4_fused(ctx, dev, oracle_lib, k):
+    """kmh_count_dense_u4_dev writes the same rows, nibbles and escape set as count + encode,
+    on ragged random genomes, a low-complexity genome (counts > 255) and one whose u16 table
+    wraps (counts > 65535: that bucket is re-encoded from the corrected rows)."""
+    rng = np.random.default_rng(500 + k)
+    genomes = [_rand_seq(rng, 3_000_000), np.zeros(0, np.uint8), _rand_seq(rng, 70_001),
+               np.frombuffer(b"AT" * 300_000 + b"a" * 5000, np.uint8).copy(),
+               np.frombuffer(b"A" * 200_000 + b"G" + b"T" * 70_000, np.uint8).copy()]
+    r1, n1, e1, c1 = _u4_block(ctx, dev, genomes, k, fused=True)
+    r2, n2, e2, c2 = _u4_block(ctx, dev, genomes, k, fused=False)
+    for g, seq in enumerate(genomes):
+        assert np.array_equal(r1[g], oracle_lib.count_dense(seq, k)), g
+    assert np.array_equal(r1, r2)
+    assert np.array_equal(n1, n2)
+    assert c1 == c2 and c1 > 0 and np.array_equal(e1, e2)
+    assert e1[:, 1].max() > 65535
+
+
 @pytest.mark.parametrize("k", [10, 12])
 def test_dense_u16_wraps(ctx, dev, oracle_lib, k):
     """Counts past 65535 in both halves of one packed u16 word of the count table: bins 0
