@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <chrono>
 #include <atomic>
+#include <system_error>
 #include <thread>
 #include "kmh_internal.h"
 
@@ -425,13 +426,16 @@ int64_t format_blocks(uint64_t n, char* out, uint64_t cap, Line&& line) {
     const uint64_t nblk = n ? (n + per - 1) / per : 0;
     std::vector<uint64_t> start(nblk + 1, 0);
     const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({nblk, 16, std::max(1u, std::thread::hardware_concurrency())}));
-    auto parallel = [&](auto&& body) {
+    auto parallel = [&](auto&& body) {   // the line functions allocate nothing
         std::atomic<uint64_t> next{0};
         auto work = [&]() {
             for (uint64_t b = next++; b < nblk; b = next++) body(b);
         };
         std::vector<std::thread> pool;
-        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+        try {
+            for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+        } catch (const std::system_error&) {   // fewer threads: the ones started finish the work
+        }
         work();
         for (auto& t : pool) t.join();
     };
@@ -468,7 +472,12 @@ int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, u
         kmh::set_thread_error("kmh_format_lines: bad arguments");
         return KMH_ERR_INVALID;
     }
-    return format_blocks(n, out, cap, [&](uint64_t i, char* o) { return format_line(k, codes[i], counts[i], o); });
+    try {
+        return format_blocks(n, out, cap, [&](uint64_t i, char* o) { return format_line(k, codes[i], counts[i], o); });
+    } catch (const std::bad_alloc&) {
+        kmh::set_thread_error("kmh_format_lines: out of host memory");
+        return KMH_ERR_NOMEM;
+    }
 }
 
 int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const uint64_t* first,
@@ -493,7 +502,8 @@ int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const 
             d['G'] = d['g'] = '3';
         }
     } tab;
-    return format_blocks(n, out, cap, [&](uint64_t i, char* o) -> uint64_t {
+    try {
+        return format_blocks(n, out, cap, [&](uint64_t i, char* o) -> uint64_t {
         uint64_t count = counts[i];
         char num[24];
         int nd = 0;
@@ -509,7 +519,11 @@ int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const 
             o[k + 1 + nd] = '\n';
         }
         return (uint64_t)k + 2 + (uint64_t)nd;
-    });
+        });
+    } catch (const std::bad_alloc&) {
+        kmh::set_thread_error("kmh_format_lines_seq: out of host memory");
+        return KMH_ERR_NOMEM;
+    }
 }
 
 }  // extern "C"

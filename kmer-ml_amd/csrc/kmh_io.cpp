@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cstdio>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -60,22 +61,40 @@ extern "C" int kmh_write_file(const char* path, const void* data, uint64_t n, in
         const size_t nblk = n ? (n + kBlock - 1) / kBlock : 1;
         unsigned nt = threads > 0 ? (unsigned)threads : std::thread::hardware_concurrency();
         nt = std::max(1u, std::min<unsigned>({nt, 16u, (unsigned)nblk}));
-        std::vector<std::vector<uint8_t>> out(nblk);
-        std::atomic<size_t> next{0};
-        std::atomic<bool> good{true};
-        auto work = [&]() {
-            for (size_t b = next++; b < nblk; b = next++) {
-                const size_t lo = b * kBlock, len = std::min(kBlock, (size_t)n - lo);
-                if (!deflate_member(src + lo, n ? len : 0, gzip_level, out[b])) good = false;
+        std::atomic<bool> good{true}, oom{false};
+        try {
+            std::vector<std::vector<uint8_t>> out(nblk);
+            std::atomic<size_t> next{0};
+            auto work = [&]() {   // a worker never lets an exception escape its thread
+                try {
+                    for (size_t b = next++; b < nblk; b = next++) {
+                        const size_t lo = b * kBlock, len = std::min(kBlock, (size_t)n - lo);
+                        if (!deflate_member(src + lo, n ? len : 0, gzip_level, out[b])) good = false;
+                    }
+                } catch (const std::bad_alloc&) {
+                    oom = true;
+                    good = false;
+                }
+            };
+            std::vector<std::thread> pool;
+            try {
+                for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+            } catch (const std::system_error&) {   // fewer threads: the ones started finish the work
             }
-        };
-        std::vector<std::thread> pool;
-        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
-        work();
-        for (auto& t : pool) t.join();
-        ok = good;
-        for (size_t b = 0; ok && b < nblk; ++b)
-            ok = out[b].empty() || std::fwrite(out[b].data(), 1, out[b].size(), f) == out[b].size();
+            work();
+            for (auto& t : pool) t.join();
+            ok = good;
+            for (size_t b = 0; ok && b < nblk; ++b)
+                ok = out[b].empty() || std::fwrite(out[b].data(), 1, out[b].size(), f) == out[b].size();
+        } catch (const std::bad_alloc&) {
+            oom = true;
+            ok = false;
+        }
+        if (oom) {
+            std::fclose(f);
+            kmh::set_thread_error(std::string("out of host memory writing ") + path);
+            return KMH_ERR_NOMEM;
+        }
     }
     ok = (std::fclose(f) == 0) && ok;
     if (!ok) {

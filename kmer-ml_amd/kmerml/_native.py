@@ -318,7 +318,16 @@ class FastaFile:
         return ctypes.string_at(sp, sl.value) if sl.value else b""
 
     def pack(self, min_len, align=1):
-        """Kept records (char length >= min_len) joined by '\\n' -> (uint8 array, kept flags)."""
+        """Kept records (char length >= min_len) joined by '\\n' -> (uint8 array, kept flags).
+
+        Records with multi-byte UTF-8 characters go through Python's own str.upper() first
+        (generate.py:41 upper-cases before the length rule of :44): a few code points expand
+        (U+00DF -> "SS" lengthens the record; U+FB05 / U+FB06 -> "ST", U+1E97 -> "T" + U+0308 and
+        U+1E9A -> "A" + U+02BE put bases into it); every non-ASCII character of the result is
+        then written as '?', a non-base.  ASCII records are packed by kmh_fasta_pack (the
+        kernels fold their case)."""
+        if any(c != n for c, n in zip(self.char_lens, self.seq_lens)):
+            return self._pack_unicode(min_len, align)
         need = ctypes.c_uint64()
         kept = np.zeros(max(len(self), 1), np.uint8)
         _check(lib().kmh_fasta_pack(self._h, int(min_len), None, 0, ctypes.byref(need), _ptr(kept)))
@@ -326,6 +335,23 @@ class FastaFile:
         _check(lib().kmh_fasta_pack(self._h, int(min_len), _ptr(out), out.size, ctypes.byref(need),
                                     None))
         return out[:need.value], kept[:len(self)].astype(bool)
+
+    def _pack_unicode(self, min_len, align):
+        parts, kept = [], np.zeros(len(self), bool)
+        for i in range(len(self)):
+            raw = self.sequence(i)
+            if self.char_lens[i] == self.seq_lens[i]:
+                n, body = self.char_lens[i], raw
+            else:
+                up = raw.decode("utf-8", errors="surrogateescape").upper()
+                n, body = len(up), up.encode("ascii", errors="replace")
+            if n >= min_len:
+                kept[i] = True
+                parts.append(body)
+        data = b"\n".join(parts)
+        out = np.empty(len(data) + align, np.uint8)
+        out[:len(data)] = np.frombuffer(data, np.uint8)
+        return out[:len(data)], kept
 
     def close(self):
         if self._h:

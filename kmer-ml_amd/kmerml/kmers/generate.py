@@ -21,7 +21,12 @@ the reference itself, tests/golden/):
 Differences: 1 <= k <= 1024 is supported (k > 1024 raises NotImplementedError,
 k <= 0 raises ValueError; k >= 33 is counted by sorting ceil(k / 32) code words per window
 and its lines are written from the sequence); counting never falls back to the CPU --
-without the HIP library or a device it raises.
+without the HIP library or a device it raises.  Size limits per organism (its kept records
+joined): below 2^32 - 1 bytes for every k, and fewer than 2^31 windows for k >= 13 (a
+3.1 Gbp human genome fits the first and not the second: it raises NotImplementedError for
+k >= 13, which extract_from_genome_list reports as "Error processing <id>" like any other
+failure).  The reference's dict has no such limit but needs tens of bytes per distinct
+k-mer of host memory.
 """
 import os
 from pathlib import Path

@@ -97,35 +97,93 @@ class KmerFeatureBuilder:
 
     # ------------------------------------------------------------------ GPU path
     @staticmethod
-    def compat_labels(k: int) -> np.ndarray:
+    def _label_levels(k: int):
+        """The compat labels level by level.  Codes with m significant letters (leading A's
+        stripped; code 0 is "A") are exactly the range [4^(m-1), 4^m) (codes 0..3 for m = 1),
+        and a level-m label is a level-(m-1) label plus one letter: L_m = repeat(L_{m-1}, 4)
+        beside tile("ACGT").  Returns the [count, m] uint8 letter blocks, m = 1..k."""
+        lut = np.frombuffer(b"ACGT", np.uint8)
+        levels = [lut.reshape(4, 1).copy()]
+        for m in range(2, k + 1):
+            prev = levels[-1] if m > 2 else levels[0][1:]         # parents: first letter not A
+            cur = np.empty((prev.shape[0] * 4, m), dtype=np.uint8)
+            cur[:, :m - 1] = np.repeat(prev, 4, axis=0)
+            cur[:, m - 1] = np.tile(lut, prev.shape[0])
+            levels.append(cur)
+        return levels
+
+    @staticmethod
+    def compat_label_arrow(k: int):
+        """The labels of compat_labels(k) as a pyarrow string array (one buffer of letters plus
+        offsets, no Python objects)."""
+        import pyarrow as pa
+
+        if not 1 <= k <= 19:
+            raise NotImplementedError("compat labels are defined for 1 <= k <= 19")
+        levels = KmerFeatureBuilder._label_levels(k)
+        buf = np.concatenate([lv.ravel() for lv in levels])
+        lens = np.concatenate([np.full(lv.shape[0], lv.shape[1], dtype=np.int64) for lv in levels])
+        offsets = np.zeros(lens.size + 1, dtype=np.int32 if buf.size < 2**31 else np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        typ = pa.string() if offsets.dtype == np.int32 else pa.large_string()
+        return pa.Array.from_buffers(typ, lens.size, [None, pa.py_buffer(offsets), pa.py_buffer(buf)])
+
+    @staticmethod
+    def compat_labels(k: int):
         """Column label of every k-mer code (A0 C1 G2 T3, first base most significant) after
         the reference's file round trip: digits A0 T1 C2 G3, parsed as an integer (leading
         zeros lost) and decoded back (statistics.py:157, :248-272).  Exact for k <= 19
-        (labels that fit int64)."""
-        if not 1 <= k <= 19:
-            raise NotImplementedError("compat labels are defined for 1 <= k <= 19")
-        to_letter = np.frombuffer(b"ACGT", np.uint8)          # device code -> letter
-        codes = np.arange(1 << (2 * k), dtype=np.int64)
-        letters = np.empty((codes.size, k), dtype=np.uint8)
-        for i in range(k):
-            letters[:, i] = to_letter[(codes >> (2 * (k - 1 - i))) & 3]
-        # strip leading A's (digit 0), keeping one when the k-mer is all A's
-        lead = np.argmax(letters != ord('A'), axis=1)
-        lead[(letters == ord('A')).all(axis=1)] = k - 1
-        flat = letters.tobytes().decode('ascii')
-        return np.array([flat[c * k + s:(c + 1) * k] for c, s in enumerate(lead.tolist())], dtype=object)
+        (labels that fit int64).  A pandas Index of Arrow-backed strings, indexable by code."""
+        return pd.Index(pd.arrays.ArrowStringArray(KmerFeatureBuilder.compat_label_arrow(k)))
+
+    @staticmethod
+    def compat_label_order(k: int) -> np.ndarray:
+        """The codes in the order of their compat labels (Python string order, a label before
+        every label it prefixes), without sorting: the labels are the nodes of a trie -- "A",
+        then complete 4-ary subtrees of k levels under C, G and T -- and string order is its
+        pre-order.  With N(d) = (4^d - 1) / 3 nodes in d levels: rank("A") = 0, rank of a
+        one-letter label s = 1 + (s - 1) N(k), and appending letter r to a label of m - 1
+        letters gives rank + 1 + r N(k - m + 1)."""
+        N = [(4 ** d - 1) // 3 for d in range(k + 2)]
+        rank = np.array([0] + [1 + (s - 1) * N[k] for s in (1, 2, 3)], dtype=np.int64)
+        ranks = [rank]
+        prev = rank[1:]
+        for m in range(2, k + 1):
+            cur = (prev[:, None] + 1 + np.arange(4, dtype=np.int64)[None, :] * N[k - m + 1]).ravel()
+            ranks.append(cur)
+            prev = cur
+        rank = np.concatenate(ranks)
+        order = np.empty_like(rank)
+        order[rank] = np.arange(rank.size, dtype=np.int64)
+        return order
 
     def from_count_matrix(self, counts, k: int, organisms) -> pd.DataFrame:
         """Count matrix DataFrame for organisms with one k-mer file each, from the dense
-        [G, 4^k] count rows (numpy or torch, u32 stored as int32 is fine).  Equal to
-        build_from_statistics_files(metric="count") on the files the extractor writes."""
-        rows = counts.cpu().numpy() if hasattr(counts, "cpu") else np.asarray(counts)
-        rows = rows.view(np.uint32) if rows.dtype == np.int32 else rows
-        labels = self.compat_labels(k)
-        present = (rows > 0).any(axis=0)
-        order = np.argsort(labels[present].astype(str), kind='stable')
-        cols = np.nonzero(present)[0][order]
+        [G, 4^k] count rows (numpy or torch, u32 stored as int32 is fine; or a
+        kmerml.kmers.matrix.AssembledMatrix).  Equal to build_from_statistics_files(
+        metric="count") on the files the extractor writes (statistics.py:95-147 ->
+        features.py:85-117): columns = labels present in any organism, in label order."""
+        if hasattr(counts, "dense") and hasattr(counts, "rows"):     # AssembledMatrix
+            counts = counts.dense()
+        order = self.compat_label_order(k)
+        if hasattr(counts, "is_cuda") and counts.is_cuda:
+            # device counts: presence test and the column permutation on the GPU, then one copy
+            import torch
+
+            dev_order = torch.from_numpy(order).to(counts.device)
+            wide = counts.to(torch.int64) & 0xFFFFFFFF                  # u32 stored as int32
+            keep = (wide != 0).any(dim=0)[dev_order] if wide.shape[0] else torch.zeros(0, dtype=torch.bool)
+            cols_t = dev_order[keep]
+            values = wide[:, cols_t].cpu().numpy()
+            cols = cols_t.cpu().numpy()
+        else:
+            rows = counts.cpu().numpy() if hasattr(counts, "cpu") else np.asarray(counts)
+            rows = rows.view(np.uint32) if rows.dtype == np.int32 else rows
+            cols = order[(rows > 0).any(axis=0)[order]] if rows.shape[0] else order[:0]
+            values = rows[:, cols].astype(np.int64)
+        labels = self.compat_label_arrow(k).take(cols)
         self.organisms = list(organisms)
-        self.kmers = labels[cols].tolist()
-        self.feature_matrix = pd.DataFrame(rows[:, cols].astype(np.int64), index=self.organisms, columns=self.kmers)
+        columns = pd.Index(pd.arrays.ArrowStringArray(labels))
+        self.kmers = columns
+        self.feature_matrix = pd.DataFrame(values, index=self.organisms, columns=columns)
         return self.feature_matrix

@@ -57,6 +57,12 @@ EDGE_CASES = [
     ("e6_lowcomplex.fa", [1, 4, 12]),
     ("e6_lowcomplex.fa", [16, 2, 2]),
     ("e7_headers.fa", [5]),
+    # str.upper() of non-ASCII characters (generate.py:41): ß -> SS (the record grows, which
+    # moves the short-record rule of :44), U+FB05 / U+FB06 -> ST, U+1E97 -> T + U+0308,
+    # U+1E9A -> A + U+02BE: the only code points whose upper() contains A, C, G or T
+    ("e8_unicode.fa", [4]),
+    ("e8_unicode.fa", [6]),
+    ("e8_unicode.fa", [2, 3]),
 ]
 
 
@@ -91,6 +97,8 @@ def main():
             print(name, ks, {k: len(v) for k, v in files.items()})
         with open(os.path.join(HERE, "edge_cases.json"), "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)
+        if "--edge-only" in sys.argv:
+            return
 
         syn = {"generator": "tests/golden/make_golden.py", "fasta_width": 80, "cases": []}
         # (a) 1 Mbp single-record genome, several k

@@ -675,6 +675,19 @@ def test_count_genome_split(tmp_path, oracle_lib, backend, nproc):
         assert np.array_equal(got, want)
 
 
+def test_count_host_size_limits(ctx):
+    """kmh_count_host rejects an organism past its limits before reading a byte (DESIGN.md 1
+    "Limits"; generate.py's docstring): 2^31 windows at k >= 13, 2^32 - 1 bytes at any k."""
+    import ctypes
+    buf = np.zeros(64, np.uint8)      # the sizes below are claimed, never read
+    out = ctypes.c_void_p()
+    lib = _native.lib()
+    for n, k in ((2**31 + 20, 21), (2**31 + 12, 13), (2**32 - 1, 12), (2**32, 4)):
+        rc = lib.kmh_count_host(ctx._h, ctypes.c_void_p(buf.ctypes.data), n, k, 0, ctypes.byref(out))
+        assert rc == _native.KMH_ERR_UNSUPPORTED, (n, k, rc)
+        assert not out.value
+
+
 def test_count_result_views_outlive_other_views(ctx):
     """ctx.count returns numpy views of the C result (kmh_kmers_data, no copy): one view stays
     valid after the others are dropped, the garbage collector runs and host memory is reused."""
@@ -771,6 +784,40 @@ def test_bench_simulated_rank():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["simulated_ranks"] == 4
     assert d["config"]["workload"].startswith("projection")
+
+
+@pytest.mark.parametrize("k", [6, 10])
+def test_from_count_matrix_gpu_equals_file_path(tmp_path, k):
+    """Row f4 end to end: the GPU count matrix (kmerml.kmers.matrix.count_matrix, and its
+    compact AssembledMatrix form under a one-rank group is covered by the assembly tests) fed
+    through KmerFeatureBuilder.from_count_matrix gives the same count matrix as the reference's
+    file route -- the drop-in KmerExtractor's k{k}.txt files -> KmerFeatureExtractor CSVs ->
+    build_from_statistics_files (features.py:28-117, statistics.py:95-147)."""
+    import contextlib as _cl
+    import io as _io
+    from kmerml.kmers.statistics import KmerFeatureExtractor
+    from kmerml.ml.features import KmerFeatureBuilder
+    kroot, fdir = tmp_path / "kmers", tmp_path / "features"
+    files, orgs = [], []
+    for i in range(3):
+        org = f"GCF_00000{i}_s{i}"
+        seq = osynth.synth_bases(40_000 + 9_000 * i, osynth.genome_seed(20 + i)).tobytes()
+        if i == 1:
+            seq = b"ACGTTGCA" * 500 + seq[:20_000].lower() + b"NNNN" + seq[20_000:]
+        fa = tmp_path / f"{org}.fa"
+        osynth.write_fasta(fa, [(org, seq), ("short", b"ACG")])
+        files.append(str(fa))
+        orgs.append(org)
+        with _cl.redirect_stdout(_io.StringIO()):
+            KmerExtractor(output_dir=str(kroot), compress=False).extract_kmers_from_fasta(str(fa), [k], organism_id=org)
+    with _cl.redirect_stdout(_io.StringIO()):
+        kf = find_files(str(kroot), patterns=["k*.txt"], recursive=True)
+        KmerFeatureExtractor(input_paths=kf, output_dir=str(fdir)).extract_features()
+        want = KmerFeatureBuilder(str(fdir)).build_from_statistics_files()
+    m = kmatrix.count_matrix(files, k)
+    got = KmerFeatureBuilder().from_count_matrix(m, k, list(want.index))
+    assert list(want.index) == ["_".join(o.split("_")[:2]) for o in orgs]   # features.py:79-83
+    assert got.to_csv() == want.to_csv()
 
 
 def _synth_row(oracle_lib, g, L=100_000_000, k=12, repeat=None):

@@ -40,9 +40,11 @@ def _text_from_sparse(k, codes, counts, first, mult=1):
 
 
 def _pack(golden_dir, name, longest):
+    # generate.py:41,44: upper() first (non-ASCII characters can expand), then the length rule;
+    # non-ASCII characters left after upper() are non-bases ('?')
     recs = ofasta.parse_fasta(_inputs(golden_dir, name))
-    kept = [s for _, _, s in recs if len(s) >= longest]
-    return "".join(s + "\n" for s in kept).encode("utf-8", errors="surrogateescape")
+    kept = [s.upper() for _, _, s in recs if len(s.upper()) >= longest]
+    return "".join(s + "\n" for s in kept).encode("ascii", errors="replace")
 
 
 def test_c_oracle_reproduces_edge_cases(golden_dir, edge_cases, oracle_lib):
