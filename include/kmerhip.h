@@ -149,8 +149,10 @@ int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, i
 
 /* ---- sparse counting, device-resident batch (BASELINE config 5) --------------- */
 /* The reference counts every k in a Python dict, a hash table (generate.py:36,58); for
- * 13 <= k <= 21 this counts G device-resident genomes (layout as kmh_count_dense_dev)
- * with partitioned LDS hash tables.  canonical != 0 counts min(forward, reverse
+ * 13 <= k <= 32 this counts G device-resident genomes (layout as kmh_count_dense_dev)
+ * with partitioned LDS hash tables (u32 residues up to k = 21, u64 beyond; a count too large
+ * for the bits a u64 residue leaves in its table slot sends that pass to the exact
+ * sort-based fallback).  canonical != 0 counts min(forward, reverse
  * complement) codes.  Genome g's distinct k-mers (2-bit codes, A0 C1 G2 T3, first base
  * most significant) and their exact counts are written to d_codes / d_counts starting at
  * entry out_off[g] (kmh_sparse_out_offsets: the number of windows of the genomes before

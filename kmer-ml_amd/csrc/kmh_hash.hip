@@ -1,4 +1,4 @@
-// kmh_hash.hip -- device-resident sparse k-mer counting (13 <= k <= 21, forward or
+// kmh_hash.hip -- device-resident sparse k-mer counting (13 <= k <= 32, forward or
 // canonical) for BASELINE config 5: 250 Mbp genomes at k = 21, where 4^k bins cannot be
 // tabulated and almost every k-mer is distinct.  The reference counts into a Python dict
 // (a hash table, /root/reference/kmerml/kmers/generate.py:36,58); here the counting is done
@@ -8,7 +8,8 @@
 //  1. k_sp_partition  one workgroup per 32768-window tile: forward (and reverse-complement)
 //                     codes from 2-bit packed registers, bucket = top 10 bits of the code
 //                     (1024 buckets), LDS histogram + scan + scatter of the low 2k - 10 bits
-//                     (u32 residues), one coalesced store of the tile's entries and an exact
+//                     (u32 residues for k <= 21, u64 for 22 <= k <= 32 on half-size tiles),
+//                     one coalesced store of the tile's entries and an exact
 //                     bucket-major offset table toff[bucket][tile] (u16 entry indices).
 //  2. k_sp_sizes      entries per (genome, bucket).  The host splits every bucket into
 //                     P = ceil(entries / 8192) passes over equal residue ranges (one LDS hash
@@ -19,7 +20,9 @@
 //                     stores them contiguously with per-pass offsets toff2[item][pass].
 //  4. k_sp_count      one workgroup per (genome, bucket, pass): reads that pass's segment of
 //                     every split item of the bucket, inserts it into a 16384-slot LDS hash
-//                     table (linear probing, 64-bit key|count slots), then scans the table and
+//                     table (linear probing, 64-bit key|count slots; for u64 residues the count
+//                     takes the 64 - (2k - 10) bits the key leaves, and an item whose count
+//                     would overflow them goes to the fallback), then scans the table and
 //                     appends the distinct k-mers to the genome's output (one atomic cursor).
 //  5. fallback        a split item whose entries exceed its staging, or a pass whose distinct
 //                     keys exceed the table limit, emits nothing; those passes are counted by
@@ -41,11 +44,26 @@ constexpr int kSpThreads = 1024;           // threads of every workgroup here
 constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
-constexpr int kSpTile = kSpThreads * 32;   // 32768 window starts per tile (= kTile)
-constexpr int kTileChunks = kSpTile / 4;   // 16-byte chunks of a tile's entries
+constexpr int kTileChunks = 8192;          // 16-byte chunks of a tile's entries (both widths)
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
 constexpr int kQU = 4;                     // chunk loads in flight per lane
-constexpr int kCaps = 20480;               // entries staged by one split item (80 KiB)
+
+// Entry width: u32 residues (k <= 21) or u64 (22 <= k <= 32).  A u64 tile holds half the windows,
+// so a tile's entries (128 KiB) and a split item's staging (80 KiB) keep their LDS size.
+template <typename E> struct Sp;
+template <> struct Sp<uint32_t> {
+    static constexpr int WPT = 32;                 // window starts per thread
+    static constexpr int TILE = kSpThreads * WPT;  // 32768 window starts per tile (= kTile)
+    static constexpr int CAPS = 20480;             // entries staged by one split item (80 KiB)
+    static constexpr int KB = 16;                  // keys a count lane loads per round
+};
+template <> struct Sp<uint64_t> {
+    static constexpr int WPT = 16;
+    static constexpr int TILE = kSpThreads * WPT;  // 16384
+    static constexpr int CAPS = 10240;             // 80 KiB
+    static constexpr int KB = 8;
+};
+template <typename E> constexpr int epc() { return 16 / (int)sizeof(E); }   // entries per chunk
 constexpr int kMaxPasses = 256;
 constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
@@ -62,7 +80,7 @@ __device__ __forceinline__ uint64_t revcomp(uint64_t x) {
 // bits of hi).  Compile-time j after unrolling.
 template <int K>
 __device__ __forceinline__ uint64_t window(uint64_t hi, uint64_t lo, int j) {
-    constexpr uint64_t M = (1ull << (2 * K)) - 1ull;
+    constexpr uint64_t M = K == 32 ? ~0ull : (1ull << (2 * K)) - 1ull;
     const int e = 2 * (j + K);  // bit end (MSB-first) of the window
     if (e <= 64) return (hi >> (64 - e)) & M;
     return ((hi << (e - 64)) | (lo >> (128 - e))) & M;
@@ -99,10 +117,10 @@ __device__ __forceinline__ Bases load_bases(const uint8_t* __restrict__ seq, uin
 }
 
 // f(code) for every valid window of this thread (canonical: min(forward, reverse complement)).
-template <int K, int CANON, typename F>
+template <int K, int CANON, int WPT, typename F>
 __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
+    for (int j = 0; j < WPT; ++j) {
         if (((b.inv << j) >> (64 - K)) == 0ull) {
             uint64_t c = window<K>(b.hi, b.lo, j);
             if (CANON) {
@@ -114,16 +132,18 @@ __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
     }
 }
 
-template <int K, int CANON>
+template <int K, int CANON, typename E>
 __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __restrict__ seq,
                                                              GenomeMap m,
-                                                             uint32_t* __restrict__ ent,
+                                                             E* __restrict__ ent,
                                                              uint16_t* __restrict__ toff,
                                                              uint32_t ldt) {
     constexpr int R = 2 * K - kSpBucketBits;
-    constexpr uint64_t RM = (R == 32) ? 0xFFFFFFFFull : ((1ull << R) - 1ull);
+    constexpr uint64_t RM = (1ull << R) - 1ull;
+    constexpr int WPT = Sp<E>::WPT, kSpTile = Sp<E>::TILE, EPC = epc<E>();
     static_assert(kSpBuckets == kSpThreads, "one bucket per thread in the scan");
-    __shared__ __attribute__((aligned(16))) uint32_t sorted[kSpTile];
+    static_assert(R <= 8 * (int)sizeof(E), "residues fit the entry");
+    __shared__ __attribute__((aligned(16))) E sorted[kSpTile];
     __shared__ uint32_t cnt[kSpBuckets];
     __shared__ uint32_t wsum[kNW];
 
@@ -137,10 +157,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     cnt[tid] = 0u;
     __syncthreads();
 
-    const uint64_t base = tstart + 32ull * (uint64_t)tid;
+    const uint64_t base = tstart + (uint64_t)WPT * (uint64_t)tid;
     const Bases bs = (tstart + (uint64_t)kSpTile + 48 <= m.data_end) ? load_bases<true>(seq, base, ge)
                                                                      : load_bases<false>(seq, base, ge);
-    each_window<K, CANON>(bs, [&](uint64_t c) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
+    each_window<K, CANON, WPT>(bs, [&](uint64_t c) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
     __syncthreads();
 
     // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
@@ -165,17 +185,17 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     if (tid == 0) toff[(uint64_t)kSpBuckets * ldt + lt] = (uint16_t)total;
     __syncthreads();
 
-    each_window<K, CANON>(bs, [&](uint64_t c) {
+    each_window<K, CANON, WPT>(bs, [&](uint64_t c) {
         const uint32_t slot = atomicAdd(&cnt[(uint32_t)(c >> R)], 1u);
-        sorted[slot] = (uint32_t)(c & RM);
+        sorted[slot] = (E)(c & RM);
     });
     __syncthreads();
 
-    uint32_t* dst = ent + lt * (uint64_t)kSpTile;
-    const uint32_t n4 = total / 4;
+    E* dst = ent + lt * (uint64_t)kSpTile;
+    const uint32_t n4 = total / EPC;
     for (uint32_t i = tid; i < n4; i += kSpThreads)
         store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
-    if (tid < (int)(total & 3u)) __builtin_nontemporal_store(sorted[4 * n4 + tid], dst + 4 * n4 + tid);
+    if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
 }
 
 // Entries of every (genome, bucket) of a batch: one workgroup per pair.
@@ -196,12 +216,16 @@ __global__ __launch_bounds__(256) void k_sp_sizes(const uint16_t* __restrict__ t
     if (threadIdx.x == 0) nb[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-__device__ __forceinline__ uint32_t pass_of(uint32_t r, uint32_t np, int R) {
-    return (uint32_t)(((uint64_t)r * np) >> R);
+// np <= 256 and r < 2^R with R <= 54: the product fits 64 bits
+__device__ __forceinline__ uint32_t pass_of(uint64_t r, uint32_t np, int R) {
+    return (uint32_t)((r * np) >> R);
 }
 
-__device__ __forceinline__ uint32_t lane_of(const uint4& v, int i) {
-    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+// Entry i of a 16-byte chunk (4 u32 or 2 u64 entries).
+template <typename E>
+__device__ __forceinline__ E lane_of(const uint4& v, int i) {
+    if constexpr (sizeof(E) == 4) return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+    else return i == 0 ? ((uint64_t)v.y << 32 | v.x) : ((uint64_t)v.w << 32 | v.z);
 }
 
 // Split work item: tiles [t0, t1) (batch-relative) of bucket b of one genome.
@@ -216,8 +240,8 @@ struct SplitItem {
 // per-wave queue: a wave takes bt tiles at a time (one per lane), lists the chunks that
 // cover their segments (tile-in-batch << 13 | chunk-in-tile) and streams them with kQU
 // loads in flight per lane; entries outside a segment are masked by position.
-template <typename F>
-__device__ __forceinline__ void walk_bucket(const uint32_t* __restrict__ ent,
+template <typename E, typename F>
+__device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
                                             const uint16_t* __restrict__ toff, uint32_t ldt,
                                             uint32_t b, uint64_t ta, uint64_t tb, uint32_t bt,
                                             uint32_t* q, uint32_t* slo, uint32_t* shi, F&& f) {
@@ -228,7 +252,8 @@ __device__ __forceinline__ void walk_bucket(const uint32_t* __restrict__ ent,
         const bool in = (uint32_t)lane < bt && t < tb;
         const uint32_t lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
         const uint32_t hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
-        const uint32_t c0 = lo >> 2, nc = hi > lo ? ((hi + 3u) >> 2) - c0 : 0u;
+        constexpr uint32_t EPC = (uint32_t)epc<E>();
+        const uint32_t c0 = lo / EPC, nc = hi > lo ? (hi + EPC - 1u) / EPC - c0 : 0u;
         uint32_t incl = nc;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -259,26 +284,28 @@ __device__ __forceinline__ void walk_bucket(const uint32_t* __restrict__ ent,
                 for (int u = 0; u < kQU; ++u) {
                     const bool live = qe[u] != kEmpty;   // idle lanes: every entry invalid
                     const uint32_t qv = live ? qe[u] : 0u;
-                    const uint32_t tl = qv >> 13, p0 = (qv & 8191u) * 4u;
+                    const uint32_t tl = qv >> 13, p0 = (qv & 8191u) * EPC;
                     const uint32_t l = slo[tl], h = live ? shi[tl] : 0u;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) f(lane_of(v[u], i), p0 + i >= l && p0 + i < h);
+                    for (int i = 0; i < (int)EPC; ++i) f(lane_of<E>(v[u], i), p0 + i >= l && p0 + i < h);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {  // skewed batch: each lane walks its own segment
-            for (uint32_t j = lo; j < hi; ++j) f(ent[t * (uint64_t)kSpTile + j], true);
+            for (uint32_t j = lo; j < hi; ++j) f(ent[t * (uint64_t)Sp<E>::TILE + j], true);
         }
     }
 }
 
+template <typename E>
 __global__ __launch_bounds__(kSpThreads) void k_sp_split(
-    const uint32_t* __restrict__ ent, const uint16_t* __restrict__ toff, uint32_t ldt,
-    const SplitItem* __restrict__ items, int R, uint32_t* __restrict__ out,
+    const E* __restrict__ ent, const uint16_t* __restrict__ toff, uint32_t ldt,
+    const SplitItem* __restrict__ items, int R, E* __restrict__ out,
     uint16_t* __restrict__ toff2, uint32_t* __restrict__ gb_fail) {
-    __shared__ __attribute__((aligned(16))) uint32_t sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
+    constexpr int kCaps = Sp<E>::CAPS, EPC = epc<E>();
+    __shared__ __attribute__((aligned(16))) E sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
     __shared__ uint32_t hist[kMaxPasses + 32];   // + dummy passes
     __shared__ uint32_t q[kNW][kQueue];
     __shared__ uint32_t slo[kNW][64], shi[kNW][64];
@@ -289,7 +316,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < kMaxPasses) hist[tid] = 0u;
     __syncthreads();
-    uint32_t bt = (uint32_t)kQueue / 2u / (it.per / 4u + 2u);
+    uint32_t bt = (uint32_t)kQueue / 2u / (it.per / (uint32_t)EPC + 2u);
     bt = bt < 1u ? 1u : (bt > 64u ? 64u : bt);
     const uint32_t np = it.np;
     // Branch-free LDS atomics: an entry outside its segment counts into one of 32 dummy
@@ -297,7 +324,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // tail of `sorted`, so no exec-mask branch surrounds an atomic.
     const uint32_t dpass = (uint32_t)kMaxPasses + (uint32_t)(lane & 31);
     walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave],
-                [&](uint32_t r, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
+                [&](E r, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
     __syncthreads();
     // exclusive scan of the pass histogram (threads 0..255)
     uint32_t n0 = 0u, incl = 0u;
@@ -328,16 +355,16 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     __syncthreads();
     const uint32_t total = total_sh;
     if (total > (uint32_t)kCaps) return;  // staging overflow: the bucket goes to the fallback
-    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], [&](uint32_t r, bool ok) {
+    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], [&](E r, bool ok) {
         const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
         sorted[ok ? slot : (uint32_t)kCaps + (uint32_t)lane] = r;
     });
     __syncthreads();
-    uint32_t* dst = out + (uint64_t)item * kCaps;
-    const uint32_t n4 = total / 4;
+    E* dst = out + (uint64_t)item * kCaps;
+    const uint32_t n4 = total / EPC;
     for (uint32_t i = tid; i < n4; i += kSpThreads)
         store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
-    if (tid < (int)(total & 3u)) __builtin_nontemporal_store(sorted[4 * n4 + tid], dst + 4 * n4 + tid);
+    if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
 }
 
 // Count work item: pass p of bucket b of genome g; its entries are segment p of split items
@@ -441,16 +468,18 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
         citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, s0, s1, (uint32_t)gb, n};
 }
 
-template <int SB, int NT>
+template <int SB, int NT, typename E>
 __global__ __launch_bounds__(NT) void k_sp_count(
-    const uint32_t* __restrict__ split, const uint16_t* __restrict__ toff2,
+    const E* __restrict__ split, const uint16_t* __restrict__ toff2,
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
     const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
     uint32_t* __restrict__ counts, unsigned long long* __restrict__ nk,
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed,
     unsigned long long* __restrict__ prof) {
-    // Slot = key << 32 | count; a slot is empty iff its count is 0, so every 32-bit residue
-    // (k = 21 uses all 32 bits) is a valid key.  Emission scans the table: for each of the
+    // Slot = key << CB | count (CB = 32 for u32 residues; 64 - R for u64 residues of R bits); a
+    // slot is empty iff its count is 0, so every residue (k = 21 uses all 32 bits) is a valid
+    // key.  A u64-residue count that would overflow its CB bits fails the item (the fallback
+    // recounts it).  Emission scans the table: for each of the
     // kSlots / NT slot rows a wave reads 64 consecutive slots (conflict-free) and compacts
     // the occupied ones to consecutive output positions (ballot + mbcnt), so the stores are
     // coalesced and the insert loop keeps no record of the slots it claimed.
@@ -463,9 +492,17 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     __shared__ unsigned long long obase;
     constexpr uint32_t kMaxIter = 8u * 1024u;     // probes of one call (8 keys per lane)
     constexpr uint32_t SM = kSlots - 1u;
+    constexpr int KB = Sp<E>::KB, kCaps = Sp<E>::CAPS;
+    constexpr bool WIDE = sizeof(E) == 8;
+    const int CB = WIDE ? 64 - R : 32;
+    const unsigned long long CM = (1ull << CB) - 1ull;
     // slot hash: top bits of the low 32 bits of a 24 x 24-bit product (v_mul_u32_u24, full
-    // rate; v_mul_lo_u32 is quarter rate) of the key folded to 24 bits
-    auto slot_of = [](uint32_t x) -> uint32_t {
+    // rate; v_mul_lo_u32 is quarter rate) of the key folded to 24 bits (a u64 key first folded
+    // to 32 bits)
+    auto slot_of = [](E key) -> uint32_t {
+        uint32_t x;
+        if constexpr (WIDE) x = (uint32_t)key ^ (uint32_t)(key >> 29) * 0x9E3779B1u;
+        else x = key;
         return (uint32_t)__umul24(x ^ (x >> 15), 0x9E3779u) >> (32 - kSlotBits);
     };
 
@@ -488,7 +525,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
     // a full-rate 24-bit multiply, and the runaway guard is a wave-uniform (scalar)
     // iteration count instead of a per-lane probe counter.
     unsigned long long iters = 0, calls = 0;
-    auto insert_keys = [&](uint32_t (&r)[8], int n) {
+    auto insert_keys = [&](E (&r)[8], int n) {
         ++calls;
         uint32_t s = slot_of(r[0]);
         for (uint32_t guard = 0; __ballot(n > 0); ++guard) {
@@ -502,10 +539,13 @@ __global__ __launch_bounds__(NT) void k_sp_count(
             // are selects, so the only branches are the uniform guard and the loop edge.
             const bool act = n > 0;
             unsigned long long* slot = act ? &tbl[s] : &dummy[tid];
-            const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)r[0] << 32) | 1ull);
+            const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)r[0] << CB) | 1ull);
             const bool won = old == 0ull;
-            const bool match = !won && (uint32_t)(old >> 32) == r[0];
-            atomicAdd(slot, match ? 1ull : 0ull);
+            const bool match = !won && (E)(old >> CB) == r[0];
+            const unsigned long long prev = atomicAdd(slot, match ? 1ull : 0ull);
+            if constexpr (WIDE) {   // the add that finds the count field full carried into the key
+                if (match && (prev & CM) == CM) fail[par] = 1u;
+            }
             const bool done = act && (won || match);
 #pragma unroll
             for (int i = 0; i < 7; ++i) r[i] = done ? r[i + 1] : r[i];
@@ -543,15 +583,15 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         }
         const uint32_t n = __shfl(incl, 63), excl = incl - len;
         // segment base in entries of `split`, minus the segment's exclusive start
-        const uint64_t sb = (uint64_t)j * kCaps + lo - excl;
+        const uint64_t sb = (uint64_t)j * kCaps + lo - excl;   // kCaps: entries per split item
         const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
         const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
         const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
-        for (uint32_t c = ea; c < eb; c += 1024u) {
-            uint32_t r[16];
+        for (uint32_t c = ea; c < eb; c += 64u * KB) {
+            E r[KB];
             int cnt = 0;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
+            for (int u = 0; u < KB; ++u) {
                 const uint32_t e0 = c + 64u * (uint32_t)u;        // entry of lane 0
                 const uint32_t e = e0 + (uint32_t)lane;
                 const bool ok = e < eb;
@@ -570,19 +610,21 @@ __global__ __launch_bounds__(NT) void k_sp_count(
                 }
                 const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
                                       (uint32_t)__shfl((int)sb_lo, sj);
-                const uint32_t v = split[base + es];
-                r[u] = ok ? v : 0u;
+                const E v = split[base + es];
+                r[u] = ok ? v : (E)0;
                 cnt += ok ? 1 : 0;   // valid entries of a lane are a prefix of r
             }
-            // two calls of 8 keys (a lane's valid keys are a prefix of r)
-            uint32_t a8[8], b8[8];
+            // calls of 8 keys (a lane's valid keys are a prefix of r)
+            E a8[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                a8[u] = r[u];
-                b8[u] = r[u + 8];
-            }
+            for (int u = 0; u < 8; ++u) a8[u] = r[u];
             insert_keys(a8, cnt < 8 ? cnt : 8);
-            if (__ballot(cnt > 8)) insert_keys(b8, cnt > 8 ? cnt - 8 : 0);
+            if constexpr (KB == 16) {
+                E b8[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) b8[u] = r[u + 8];
+                if (__ballot(cnt > 8)) insert_keys(b8, cnt > 8 ? cnt - 8 : 0);
+            }
         }
     }
     lds_barrier();
@@ -597,7 +639,7 @@ __global__ __launch_bounds__(NT) void k_sp_count(
 #pragma unroll
     for (int q = 0; q < kRows; ++q) {
         x[q] = tbl[q * NT + tid];
-        mine += (uint32_t)__builtin_popcountll(__ballot((uint32_t)x[q] != 0u));
+        mine += (uint32_t)__builtin_popcountll(__ballot((x[q] & CM) != 0ull));
     }
 #pragma unroll
     for (int q = 0; q < kRows; ++q) tbl[q * NT + tid] = 0ull;
@@ -627,15 +669,15 @@ __global__ __launch_bounds__(NT) void k_sp_count(
         uint32_t run = 0u;
 #pragma unroll
         for (int q = 0; q < kRows; ++q) {
-            const bool occ = (uint32_t)x[q] != 0u;
+            const bool occ = (x[q] & CM) != 0ull;
             const uint64_t m = __ballot(occ);
             if (occ) {
                 const uint64_t i = at + run + (uint32_t)__builtin_popcountll(m & below);
                 // plain stores: the wave's rows form one contiguous run, and write-back
                 // stores merge the partial lines at row boundaries in L2 (exactly 12 B per
                 // distinct k-mer reach HBM); non-temporal stores wrote 32 % more bytes
-                codes[i] = hib | (x[q] >> 32);
-                counts[i] = (uint32_t)x[q];
+                codes[i] = hib | (x[q] >> CB);
+                counts[i] = (uint32_t)(x[q] & CM);
             }
             run += (uint32_t)__builtin_popcountll(m);
         }
@@ -655,22 +697,24 @@ __global__ __launch_bounds__(NT) void k_sp_count(
 }
 
 // Fallback, step 1: the residues of bucket b, pass p of genome g, in any order.
-__global__ __launch_bounds__(256) void k_sp_gather(const uint32_t* __restrict__ ent,
+template <typename E>
+__global__ __launch_bounds__(256) void k_sp_gather(const E* __restrict__ ent,
                                                    const uint16_t* __restrict__ toff, uint32_t ldt,
                                                    uint64_t ta, uint64_t tb, uint32_t b, uint32_t p,
-                                                   uint32_t np, int R, uint32_t* __restrict__ out,
+                                                   uint32_t np, int R, E* __restrict__ out,
                                                    uint32_t* __restrict__ n) {
     const uint64_t t = ta + (uint64_t)blockIdx.x;
     if (t >= tb) return;
     const uint32_t lo = toff[(uint64_t)b * ldt + t], hi = toff[(uint64_t)(b + 1) * ldt + t];
     for (uint32_t j = lo + threadIdx.x; j < hi; j += 256) {
-        const uint32_t r = ent[t * (uint64_t)kSpTile + j];
+        const E r = ent[t * (uint64_t)Sp<E>::TILE + j];
         if (pass_of(r, np, R) == p) out[atomicAdd(n, 1u)] = r;
     }
 }
 
 // Fallback, step 3: append the run-length encoded keys to genome g's output.
-__global__ __launch_bounds__(256) void k_sp_append(const uint32_t* __restrict__ keys,
+template <typename E>
+__global__ __launch_bounds__(256) void k_sp_append(const E* __restrict__ keys,
                                                    const uint32_t* __restrict__ runs,
                                                    const uint32_t* __restrict__ nruns, uint64_t hib,
                                                    uint64_t off, unsigned long long* __restrict__ nk,
@@ -692,58 +736,60 @@ void* carve(char*& p, size_t bytes) {
     return r;
 }
 
-template <int K, int CANON>
+template <int K, int CANON, typename E>
 void launch_partition(unsigned tiles, hipStream_t s, const uint8_t* seq, const GenomeMap& m,
-                      uint32_t* ent, uint16_t* toff, uint32_t ldt) {
-    hipLaunchKernelGGL((k_sp_partition<K, CANON>), dim3(tiles), dim3(kSpThreads), 0, s, seq, m, ent,
+                      E* ent, uint16_t* toff, uint32_t ldt) {
+    hipLaunchKernelGGL((k_sp_partition<K, CANON, E>), dim3(tiles), dim3(kSpThreads), 0, s, seq, m, ent,
                        toff, ldt);
 }
 
-template <int K>
+template <int K, typename E>
 void partition_k(int canonical, unsigned tiles, hipStream_t s, const uint8_t* seq,
-                 const GenomeMap& m, uint32_t* ent, uint16_t* toff, uint32_t ldt) {
-    if (canonical) launch_partition<K, 1>(tiles, s, seq, m, ent, toff, ldt);
-    else launch_partition<K, 0>(tiles, s, seq, m, ent, toff, ldt);
+                 const GenomeMap& m, E* ent, uint16_t* toff, uint32_t ldt) {
+    if (canonical) launch_partition<K, 1, E>(tiles, s, seq, m, ent, toff, ldt);
+    else launch_partition<K, 0, E>(tiles, s, seq, m, ent, toff, ldt);
 }
 
+template <typename E>
 void launch_partition_k(int k, int canonical, unsigned tiles, hipStream_t s, const uint8_t* seq,
-                        const GenomeMap& m, uint32_t* ent, uint16_t* toff, uint32_t ldt) {
-    switch (k) {
-    case 13: partition_k<13>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 14: partition_k<14>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 15: partition_k<15>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 16: partition_k<16>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 17: partition_k<17>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 18: partition_k<18>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 19: partition_k<19>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    case 20: partition_k<20>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
-    default: partition_k<21>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
+                        const GenomeMap& m, E* ent, uint16_t* toff, uint32_t ldt) {
+#define KMH_PK(KK) case KK: partition_k<KK, E>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
+    if constexpr (sizeof(E) == 4) {
+        switch (k) { KMH_PK(13) KMH_PK(14) KMH_PK(15) KMH_PK(16) KMH_PK(17) KMH_PK(18) KMH_PK(19) KMH_PK(20)
+                     default: partition_k<21, E>(canonical, tiles, s, seq, m, ent, toff, ldt); break; }
+    } else {
+        switch (k) { KMH_PK(22) KMH_PK(23) KMH_PK(24) KMH_PK(25) KMH_PK(26) KMH_PK(27) KMH_PK(28) KMH_PK(29)
+                     KMH_PK(30) KMH_PK(31)
+                     default: partition_k<32, E>(canonical, tiles, s, seq, m, ent, toff, ldt); break; }
     }
+#undef KMH_PK
 }
 
 // Fallback for pass p of bucket b of genome g: gather, radix sort, run-length encode, append.
+template <typename E>
 int fallback_pass(Ctx* ctx, uint32_t g, uint32_t b, uint32_t p, uint32_t np, uint32_t n,
-                  const uint32_t* ent, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
+                  const E* ent, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
                   int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
                   hipStream_t s) {
     size_t t_sort = 0, t_rle = 0;
+    E* nulk = nullptr;
     uint32_t* nul = nullptr;
-    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, nul, nul, (int)n, 0, R, s));
-    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, nul, nul, nul, nul, (int)n, s));
+    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, nulk, nulk, (int)n, 0, R, s));
+    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, nulk, nulk, nul, nul, (int)n, s));
     const size_t temp = std::max(t_sort, t_rle);
-    const size_t arr = ((size_t)n * 4 + 255) & ~(size_t)255;
+    const size_t arr = ((size_t)n * sizeof(E) + 255) & ~(size_t)255;
     int rc = ensure(ctx, ctx->sparse[5], 4 * arr + temp + 1024);
     if (rc) return rc;
     char* p8 = static_cast<char*>(ctx->sparse[5].ptr);
-    uint32_t* a = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
-    uint32_t* bsorted = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
-    uint32_t* ukeys = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
+    E* a = static_cast<E*>(carve(p8, (size_t)n * sizeof(E)));
+    E* bsorted = static_cast<E*>(carve(p8, (size_t)n * sizeof(E)));
+    E* ukeys = static_cast<E*>(carve(p8, (size_t)n * sizeof(E)));
     uint32_t* runs = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
     uint32_t* small = static_cast<uint32_t*>(carve(p8, 256));
     void* tmp = carve(p8, temp);
     KMH_HIP(ctx, hipMemsetAsync(small, 0, 256, s));
     if (tb > ta) {
-        hipLaunchKernelGGL(k_sp_gather, dim3((unsigned)(tb - ta)), dim3(256), 0, s, ent, toff, ldt, ta, tb,
+        hipLaunchKernelGGL(k_sp_gather<E>, dim3((unsigned)(tb - ta)), dim3(256), 0, s, ent, toff, ldt, ta, tb,
                            b, p, np, R, a, small);
         KMH_HIP(ctx, hipGetLastError());
     }
@@ -755,7 +801,7 @@ int fallback_pass(Ctx* ctx, uint32_t g, uint32_t b, uint32_t p, uint32_t np, uin
     KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(tmp, t, a, bsorted, (int)m, 0, R, s));
     t = temp;
     KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(tmp, t, bsorted, ukeys, runs, small + 1, (int)m, s));
-    hipLaunchKernelGGL(k_sp_append, dim3(1), dim3(256), 0, s, ukeys, runs, small + 1,
+    hipLaunchKernelGGL(k_sp_append<E>, dim3(1), dim3(256), 0, s, ukeys, runs, small + 1,
                        (uint64_t)b << R, out_off, nk + g, codes, counts);
     KMH_HIP(ctx, hipGetLastError());
     KMH_HIP(ctx, hipStreamSynchronize(s));
@@ -775,11 +821,13 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
     return tot;
 }
 
-int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
-                     int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
-                     hipStream_t s) {
-    if (k < 13 || k > 21) return fail(ctx, KMH_ERR_UNSUPPORTED, "device sparse counting needs 13 <= k <= 21");
-    if (!d_seq || !d_codes || !d_counts || !d_nkmers) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+namespace {
+
+template <typename E>
+int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                          int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
+                          hipStream_t s) {
+    constexpr int kSpTile = Sp<E>::TILE, kCaps = Sp<E>::CAPS;
     Layout L;
     int rc = make_layout(ctx, offsets, G, k, (uint64_t)kSpTile, L);
     if (rc) return rc;
@@ -793,7 +841,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     KMH_HIP(ctx, hipMemsetAsync(d_nkmers, 0, (size_t)G * sizeof(uint64_t), s));
     if (L.ntiles == 0) return KMH_OK;
 
-    const size_t tile_bytes = (size_t)kSpTile * sizeof(uint32_t);
+    const size_t tile_bytes = (size_t)kSpTile * sizeof(E);
     const size_t budget = env_mb("KMH_SP_BUDGET_MB", 16384) << 20;
     // LDS hash table of the count kernel: 2^14 slots.  Experiment builds (-DKMH_EXPERIMENTS)
     // also take KMH_SP_TABLE_BITS 12..13: smaller tables, several count workgroups per CU
@@ -829,7 +877,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     rc = ensure(ctx, ctx->sparse[2], std::max<uint64_t>(max_tiles, 1) * tile_bytes);
     if (!rc) rc = ensure(ctx, ctx->sparse[3], (size_t)ldt * (kSpBuckets + 1) * sizeof(uint16_t));
     if (rc) return rc;
-    uint32_t* ent = static_cast<uint32_t*>(ctx->sparse[2].ptr);
+    E* ent = static_cast<E*>(ctx->sparse[2].ptr);
     uint16_t* toff = static_cast<uint16_t*>(ctx->sparse[3].ptr);
 
     // Experiment builds: KMH_SP_PROF=1 or 2 prints the host phases of every batch (2: without
@@ -878,11 +926,11 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         if (nci == 0) continue;
         const double h2 = hprof ? now_ms() : 0.0;
         // split output + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
-        const size_t sbytes = nsi * (size_t)kCaps * 4;
+        const size_t sbytes = nsi * (size_t)kCaps * sizeof(E);
         const size_t t2bytes = (nsi * kT2 * 2 + 255) & ~(size_t)255;
         rc = ensure(ctx, ctx->sparse[6], sbytes + t2bytes);
         if (rc) return rc;
-        uint32_t* d_split = static_cast<uint32_t*>(ctx->sparse[6].ptr);
+        E* d_split = static_cast<E*>(ctx->sparse[6].ptr);
         uint16_t* d_toff2 = reinterpret_cast<uint16_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes);
         const size_t sib = (nsi * sizeof(SplitItem) + 255) & ~(size_t)255;
         const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
@@ -901,7 +949,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         time_begin(ctx, s, "k_sp_split");
-        hipLaunchKernelGGL(k_sp_split, dim3((unsigned)nsi), dim3(kSpThreads), 0, s, ent, toff, ldt, d_sitems, R,
+        hipLaunchKernelGGL(k_sp_split<E>, dim3((unsigned)nsi), dim3(kSpThreads), 0, s, ent, toff, ldt, d_sitems, R,
                            d_split, d_toff2, d_gbfail);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
@@ -921,7 +969,7 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
             KMH_HIP(ctx, hipMemsetAsync(d_prof, 0, 256, s));
         }
 #define KMH_SP_COUNT(SB, NT)                                                                         \
-    hipLaunchKernelGGL((k_sp_count<SB, NT>), dim3(cgrid), dim3(NT), 0, s, d_split, d_toff2, d_citems,   \
+    hipLaunchKernelGGL((k_sp_count<SB, NT, E>), dim3(cgrid), dim3(NT), 0, s, d_split, d_toff2, d_citems, \
                        (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts,                               \
                        reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed, d_prof)
 #ifdef KMH_EXPERIMENTS
@@ -978,6 +1026,18 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
                          h1 - h0, h2 - h1, nsi, nci, h3 - h2, h4 - h3, now_ms() - h4, ids.size());
     }
     return KMH_OK;
+}
+
+}  // namespace
+
+int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                     int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
+                     hipStream_t s) {
+    if (k < 13 || k > 32) return fail(ctx, KMH_ERR_UNSUPPORTED, "device sparse counting needs 13 <= k <= 32");
+    if (!d_seq || !d_codes || !d_counts || !d_nkmers) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    // residues of 2k - 10 bits: u32 entries up to k = 21, u64 beyond
+    if (k <= 21) return sparse_count_dev_impl<uint32_t>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers, s);
+    return sparse_count_dev_impl<uint64_t>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers, s);
 }
 
 }  // namespace kmh

@@ -202,7 +202,7 @@ class Context:
 
     # -- sparse counting, device-resident (BASELINE config 5) --
     def count_sparse_dev(self, d_seq, offsets, k, canonical, d_codes, d_counts, d_nkmers, stream=None):
-        """Distinct k-mers of G device-resident genomes (13 <= k <= 21); genome g's entries
+        """Distinct k-mers of G device-resident genomes (13 <= k <= 32); genome g's entries
         start at sparse_out_offsets(offsets, k)[g].  Synchronises the stream."""
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         _check(lib().kmh_count_sparse_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1, int(k),

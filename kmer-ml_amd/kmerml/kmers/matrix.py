@@ -325,7 +325,7 @@ def count_matrix(genome_files, k, device=None, group=None, count_fn=None, compac
 def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
     """Sparse k-mer counts of this rank's block of `genome_files` (BASELINE config 5).
 
-    For 13 <= k <= 21 the genomes are counted on the GPU with the partitioned hash-table path
+    For 13 <= k <= 32 the genomes are counted on the GPU with the partitioned hash-table path
     (kmh_count_sparse_dev); any other 1 <= k <= 32 genome by genome with the GPU sort path of
     kmh_count_host (dense table for k <= 12).  The 4^k columns cannot be assembled densely (4^21 ~ 4.4e12), so
     nothing is exchanged: with a torch.distributed process group, rank r counts block
@@ -347,7 +347,7 @@ def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
     if hi == lo:
         return lo, []
     buf, offsets = pack_genomes(files[lo:hi], k)
-    if not 13 <= k <= 21:   # outside the batched hash-table path: one GPU count per genome
+    if not 13 <= k <= 32:   # outside the batched hash-table path: one GPU count per genome
         ctx = _native.context(device)
         rows = []
         for g in range(hi - lo):
@@ -369,10 +369,10 @@ def sparse_rows(genome_files, k, canonical=True, device=None, group=None):
     rows = []
     for g in range(hi - lo):
         a = int(out_off[g])
-        c = d_codes[a:a + int(n[g])]
-        order = torch.argsort(c)
-        rows.append((c[order].cpu().numpy().view(np.uint64),
-                     d_counts[a:a + int(n[g])][order].cpu().numpy().view(np.uint32)))
+        # codes use all 64 bits at k = 32: order them as unsigned (torch sorts int64 signed)
+        c = d_codes[a:a + int(n[g])].cpu().numpy().view(np.uint64)
+        order = np.argsort(c, kind="stable")
+        rows.append((c[order], d_counts[a:a + int(n[g])].cpu().numpy().view(np.uint32)[order]))
     return lo, rows
 
 

@@ -546,7 +546,8 @@ def _ragged_genomes(rng, sizes):
     return gs
 
 
-@pytest.mark.parametrize("k,canonical", [(13, 0), (13, 1), (17, 1), (20, 0), (21, 0), (21, 1)])
+@pytest.mark.parametrize("k,canonical", [(13, 0), (13, 1), (17, 1), (20, 0), (21, 0), (21, 1),
+                                         (22, 0), (22, 1), (25, 0), (25, 1), (31, 1), (32, 0), (32, 1)])
 def test_sparse_dev_vs_oracle(ctx, dev, oracle_lib, k, canonical):
     rng = np.random.default_rng(100 + k * 2 + canonical)
     genomes = _ragged_genomes(rng, [400_000, 32768 + 21, 1_000_003, 17])
@@ -557,16 +558,17 @@ def test_sparse_dev_vs_oracle(ctx, dev, oracle_lib, k, canonical):
         assert np.array_equal(got[g][1], wn), g
 
 
-def test_sparse_dev_passes_and_fallback(ctx, dev, oracle_lib, monkeypatch):
+@pytest.mark.parametrize("k", [21, 27])
+def test_sparse_dev_passes_and_fallback(ctx, dev, oracle_lib, monkeypatch, k):
     """Every bucket split into many passes, and tables capped so most passes overflow into
-    the sort fallback: the counts must not change."""
+    the sort fallback: the counts must not change (u32 residues at k = 21, u64 at k = 27)."""
     rng = np.random.default_rng(7)
     genomes = _ragged_genomes(rng, [600_000, 70_001])
-    want = [oracle_lib.count_sparse(s, 21, canonical=True)[:2] for s in genomes]
+    want = [oracle_lib.count_sparse(s, k, canonical=True)[:2] for s in genomes]
     for target, limit in (("37", "12288"), ("100000", "40"), ("61", "9")):
         monkeypatch.setenv("KMH_SP_TARGET", target)
         monkeypatch.setenv("KMH_SP_LIMIT", limit)
-        got = _sparse_dev(ctx, dev, genomes, 21, 1)
+        got = _sparse_dev(ctx, dev, genomes, k, 1)
         for g in range(len(genomes)):
             assert np.array_equal(got[g][0], want[g][0]), (target, limit, g)
             assert np.array_equal(got[g][1], want[g][1]), (target, limit, g)
@@ -587,18 +589,21 @@ def test_sparse_dev_multi_batch(ctx, dev, oracle_lib, monkeypatch):
             assert np.array_equal(got[g][1], want[g][1]), (limit, g)
 
 
-def test_sparse_dev_low_complexity(ctx, dev, oracle_lib):
-    # poly-T: at k = 21 the forward code's low 32 bits are all ones (a residue that must not
-    # be mistaken for an empty slot)
+@pytest.mark.parametrize("k", [21, 22, 32])
+def test_sparse_dev_low_complexity(ctx, dev, oracle_lib, k):
+    """poly-T: at k = 21 the forward code's low 32 bits are all ones (a residue that must not
+    be mistaken for an empty slot).  At k = 32 a table slot keeps 10 count bits beside its
+    54-bit key: the repeats here count up to ~300 000, so their passes overflow into the exact
+    fallback; at k = 22 the count keeps 30 bits."""
     genomes = [np.full(300_000, ord("A"), np.uint8),
                np.full(70_000, ord("T"), np.uint8),
                np.frombuffer(b"A" * 5 + b"T" * 16 + b"G" * 3, np.uint8).copy(),
                np.frombuffer(b"AC" * 150_000, np.uint8).copy(),
                np.frombuffer(b"ACGTTTGACCA" * 30_000, np.uint8).copy()]
     for canonical in (0, 1):
-        got = _sparse_dev(ctx, dev, genomes, 21, canonical)
+        got = _sparse_dev(ctx, dev, genomes, k, canonical)
         for g, seq in enumerate(genomes):
-            wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=bool(canonical))
+            wc, wn, _ = oracle_lib.count_sparse(seq, k, canonical=bool(canonical))
             assert np.array_equal(got[g][0], wc)
             assert np.array_equal(got[g][1], wn)
 
@@ -612,11 +617,39 @@ def test_sparse_dev_config5_genome(ctx, dev, oracle_lib):
     assert np.array_equal(got[0], wc) and np.array_equal(got[1], wn)
 
 
-def test_sparse_dev_rejects_k(ctx, dev):
+@pytest.mark.parametrize("k,canonical", [(25, 1), (32, 0)])
+def test_sparse_dev_long_k_genome(ctx, dev, oracle_lib, k, canonical):
+    """The u64-residue hash path on a 12 Mbp synthetic genome plus a second one that shares a
+    4 Mbp stretch with it (every k-mer of the stretch counted twice per genome pair)."""
+    a = osynth.synth_bases(12_000_000, osynth.genome_seed(40 + k))
+    b = np.concatenate([a[2_000_000:6_000_000], osynth.synth_bases(3_000_000, osynth.genome_seed(90))])
+    got = _sparse_dev(ctx, dev, [a, b], k, canonical)
+    for g, seq in enumerate((a, b)):
+        wc, wn, _ = oracle_lib.count_sparse(seq, k, canonical=bool(canonical))
+        assert got[g][0].size == wc.size
+        assert np.array_equal(got[g][0], wc) and np.array_equal(got[g][1], wn)
+
+
+def test_sparse_dev_multi_batch_long_k(ctx, dev, oracle_lib, monkeypatch):
+    """u64 residues with one genome per batch and capped tables."""
+    rng = np.random.default_rng(13)
+    genomes = _ragged_genomes(rng, [300_000, 70_001, 150_000])
+    want = [oracle_lib.count_sparse(s, 30, canonical=False)[:2] for s in genomes]
+    monkeypatch.setenv("KMH_SP_BUDGET_MB", "1")
+    for limit in ("16384", "50"):
+        monkeypatch.setenv("KMH_SP_LIMIT", limit)
+        got = _sparse_dev(ctx, dev, genomes, 30, 0)
+        for g in range(len(genomes)):
+            assert np.array_equal(got[g][0], want[g][0]), (limit, g)
+            assert np.array_equal(got[g][1], want[g][1]), (limit, g)
+
+
+@pytest.mark.parametrize("k", [12, 33])
+def test_sparse_dev_rejects_k(ctx, dev, k):
     d = torch.zeros(64, dtype=torch.uint8, device=dev)
     o = torch.zeros(8, dtype=torch.int64, device=dev)
     with pytest.raises(NotImplementedError):
-        ctx.count_sparse_dev(d.data_ptr(), np.array([0, 64], np.uint64), 12, 0, o.data_ptr(), o.data_ptr(),
+        ctx.count_sparse_dev(d.data_ptr(), np.array([0, 64], np.uint64), k, 0, o.data_ptr(), o.data_ptr(),
                              o.data_ptr())
 
 
@@ -886,7 +919,7 @@ def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
 @pytest.mark.parametrize("k,canonical", [(21, True), (9, False), (25, True), (32, False)])
 def test_sparse_rows_from_fasta(tmp_path, oracle_lib, k, canonical):
     """kmerml.kmers.matrix.sparse_rows: FASTA files -> per-genome sorted sparse counts (the
-    batched hash-table path for 13 <= k <= 21, per-genome GPU counts otherwise)."""
+    batched hash-table path for 13 <= k <= 32, per-genome GPU counts otherwise)."""
     files, seqs = [], []
     for i in range(3):
         p = tmp_path / f"g{i}.fa"
