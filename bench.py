@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--separate-encode", action="store_true",
                    help="compact u4 assembly: count, then encode in a second pass (A/B of the fused "
                         "kmh_count_dense_u4_dev)")
+    p.add_argument("--no-config5", action="store_true",
+                   help="dense N = 1: skip the config-5 measurement (16 x 250 Mbp, k = 21 canonical, "
+                        "3 timed steps) that the default run appends to its JSON line as \"config5\"")
     p.add_argument("--simulate-ranks", type=int, default=0,
                    help="one process on one GPU doing what ONE rank of N does per step at config 4 "
                         "(count G/N genomes, encode u4, and the all-gather's writes modelled as N "
@@ -594,6 +597,15 @@ def main():
             "cpu_procs_baseline": cpu_p,
             "cpu_threads_baseline": cpu_mt,
         }
+        if world == 1 and not sim and not a.no_config5 and G == 64 and L == 100_000_000 and k == 12:
+            # BASELINE config 5 measured in the same run (its own line: bench.py --workload sparse)
+            torch.cuda.empty_cache()
+            sa = argparse.Namespace(k=21, genomes=16, genome_len=250_000_000, steps=3, warmup=1,
+                                    cpu_sample=0, forward=False, backend=a.backend, pmc_summary=a.pmc_summary)
+            try:
+                out["config5"] = run_sparse(sa, 1, 0, dev, dev_index, emit=False)
+            except Exception as e:   # never lose the config-3 line over the extra measurement
+                out["config5"] = {"error": f"{type(e).__name__}: {e}"}
         if sim:
             out["config"]["workload"] = (f"projection: ONE rank of config 4 at N = {sim} on one GPU (its {g_local} of "
                                          f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k}, u4 encode, the all-gather "
@@ -610,7 +622,7 @@ def main():
         raise SystemExit("row-sum check failed")
 
 
-def run_sparse(a, world, rank, dev, dev_index):
+def run_sparse(a, world, rank, dev, dev_index, emit=True):
     """Config 5: k = 21 canonical k-mers of 250 Mbp genomes counted with the device hash-table
     path (kmh_count_sparse_dev); each rank counts its contiguous block of genomes and keeps
     its sparse rows (the full 4^21-column matrix would not fit: no all-gather)."""
@@ -648,6 +660,7 @@ def run_sparse(a, world, rank, dev, dev_index):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    os.environ["KMH_TIMING_ONLY"] = "k_sp_partition,k_sp_split,k_sp_count"
     ctx.timing(True)
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -717,6 +730,8 @@ def run_sparse(a, world, rank, dev, dev_index):
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        if not emit:
+            return out
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

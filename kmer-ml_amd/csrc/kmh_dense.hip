@@ -729,7 +729,10 @@ template <int K>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s, const U4Out* enc) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int U = 6;                  // chunk loads in flight per lane (queue = 64 U)
+#ifndef KMH_COUNT_U
+#define KMH_COUNT_U 6
+#endif
+    constexpr int U = KMH_COUNT_U;        // chunk loads in flight per lane (queue = 64 U)
     const size_t row = (size_t)1 << (2 * K);
     // Genomes per batch: the suffix buffer of one batch stays within the budget (8 GiB: 36
     // genomes of 100 Mbp at k = 12).  Measured (profiles/ab2_r02.sh, config 3): 2 / 4 / 8 GiB
