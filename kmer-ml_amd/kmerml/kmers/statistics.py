@@ -123,7 +123,12 @@ class KmerFeatureExtractor:
         cols = {'kmer': labels, 'count': df['count'].to_numpy(), 'k': np.full(len(labels), k_val, dtype=np.int64)}
         if len(labels) == 0:
             return pd.DataFrame(cols)
-        f = label_features([str(x) for x in labels])
+        codes = label_codes(df['kmer'].to_numpy(), k_val)
+        if codes is not None:   # every label is a k-mer: rows of the per-k table (feature_table)
+            t = feature_table(k_val)
+            f = {name: col[codes] for name, col in t.items()}
+        else:
+            f = label_features([str(x) for x in labels])
         if 'gc_content' in required_features:
             cols['gc_percent'] = f['gc_percent']
         if 'base_counts' in required_features:
@@ -202,6 +207,113 @@ def write_csv(df, path):
         return
     with open(path, 'w', newline='') as f:
         f.write(text)
+
+
+_DIGIT_CODE = np.array([0, 3, 1, 2, -1, -1, -1, -1, -1, -1], dtype=np.int64)   # file digit -> A0 C1 G2 T3
+
+
+def label_codes(values, k):
+    """2-bit codes (A0 C1 G2 T3, first base most significant) of integer-parsed labels of a
+    k{k}.txt file, or None unless every label is one: an integer whose decimal digits are the
+    reference's A0 T1 C2 G3 digits of a k-mer with its leading A's (zeros) lost
+    (statistics.py:253-272 parses them so).  Code c's table row then holds the features of
+    exactly the label the reference computes them on."""
+    if values.dtype.kind not in 'iu' or not 1 <= k <= 19 or len(values) == 0:
+        return None
+    v = values.astype(np.int64)
+    if v.min() < 0:
+        return None
+    codes = np.zeros(len(v), dtype=np.int64)
+    for i in range(k):
+        d = _DIGIT_CODE[v % 10]
+        if (d < 0).any():
+            return None
+        codes |= d << (2 * i)
+        v //= 10
+    return codes if not v.any() else None
+
+
+_TABLES = {}
+
+
+def feature_table(k):
+    """The statistics.py:188-238 features of every label of a dense k (the compat label of each
+    of the 4^k codes: the k-mer with its leading A's stripped, one kept for A...A), computed
+    once per k on the GPU (torch on cuda; on the CPU without one) and indexed by code.  Same
+    IEEE operations as the reference, per value: gc = (g + c) / L * 100; expected =
+    c / L * (g / L) * (L - 1); entropy summed in set(kmer) order (_entropy_order per
+    first-appearance pattern) with math.log2 of the same quotients."""
+    if k in _TABLES:
+        return _TABLES[k]
+    import torch
+
+    dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+    i64 = torch.int64
+    c = torch.arange(1 << (2 * k), dtype=i64, device=dev)
+    # stripped length m: significant base-4 digits (at least 1)
+    m = torch.ones_like(c)
+    for j in range(1, k):
+        m += (c >= (1 << (2 * j))).to(i64)
+    digit = [(c >> (2 * (k - 1 - i))) & 3 for i in range(k)]
+    valid = [(k - i) <= m for i in range(k)]                       # position i is in the label
+    cnt = [torch.zeros_like(c) for _ in range(4)]
+    first = [torch.full_like(c, 1 << 20) for _ in range(4)]
+    for i in range(k):
+        for b in range(4):
+            hit = valid[i] & (digit[i] == b)
+            cnt[b] += hit.to(i64)
+            first[b] = torch.where(hit & (first[b] > i), torch.full_like(c, i), first[b])
+    cpg = torch.zeros_like(c)
+    rep = torch.zeros(c.shape, dtype=torch.bool, device=dev)
+    for i in range(k - 1):
+        cpg += (valid[i] & (digit[i] == 1) & (digit[i + 1] == 2)).to(i64)
+    for i in range(k - 3):
+        rep |= valid[i] & (digit[i] == digit[i + 2]) & (digit[i + 1] == digit[i + 3])
+    Lf = m.to(torch.float64)
+    A, C, G, T = cnt
+    out = {'A_count': A, 'C_count': C, 'G_count': G, 'T_count': T, 'cpg_count': cpg,
+           'has_repeat': rep.to(i64)}
+    out['gc_percent'] = ((G + C).to(torch.float64) / Lf) * 100
+    c_freq, g_freq = C.to(torch.float64) / Lf, G.to(torch.float64) / Lf
+    prod = c_freq * g_freq
+    expected = torch.where(prod > 0, prod * (Lf - 1), torch.full_like(prod, 0.001))
+    out['cpg_obs_exp'] = torch.where(expected > 0, cpg.to(torch.float64) / expected, torch.zeros_like(prod))
+    # entropy: first-appearance pattern -> the set order of this interpreter
+    letters = 'ACGT'
+    key = torch.zeros_like(c)
+    order_rank = torch.stack(first).argsort(dim=0, stable=True)      # letters by first position
+    present_sorted = torch.stack(first).gather(0, order_rank) < (1 << 20)
+    for r in range(4):
+        key = key * 5 + torch.where(present_sorted[r], order_rank[r] + 1, torch.zeros_like(c))
+    keys = torch.unique(key).tolist()
+    lut_order = torch.full((625, 4), -1, dtype=i64)
+    for kv in keys:
+        ds, x = [], kv
+        for _ in range(4):
+            ds.append(x % 5)
+            x //= 5
+        pat = ''.join(letters[d - 1] for d in reversed(ds) if d)
+        seq = [letters.index(ch) for ch in _entropy_order(pat)]
+        lut_order[kv, :len(seq)] = torch.tensor(seq, dtype=i64)
+    lut_order = lut_order.to(dev)
+    lg = torch.zeros((k + 1, k + 1), dtype=torch.float64)               # log2(n / L) as math.log2
+    for L in range(1, k + 1):
+        for n in range(1, L + 1):
+            lg[n, L] = math.log2(n / L)
+    lg = lg.to(dev)
+    cnt_t = torch.stack(cnt)
+    ent = torch.zeros_like(Lf)
+    for r in range(4):
+        b = lut_order[key, r]
+        has = b >= 0
+        n = cnt_t.gather(0, b.clamp(min=0)[None])[0]
+        p = n.to(torch.float64) / Lf
+        term = p * lg[n, m]                       # one rounding, as prob * math.log2(prob)
+        ent = torch.where(has, ent - term, ent)
+    out['shannon_entropy'] = ent
+    table = {name: v.cpu().numpy() for name, v in out.items()}
+    _TABLES[k] = table
+    return table
 
 
 def _entropy_order(pattern):

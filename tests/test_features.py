@@ -196,3 +196,44 @@ def test_fast_csv_equals_pandas(features2):
     assert csv_text(odd) == odd.to_csv(index=False)
     assert csv_text(pd.DataFrame({"kmer": ["a,b"], "count": [1]})) is None   # quoting: pandas path
     assert csv_text(pd.DataFrame({"x": [float("nan")]})) is None
+
+
+def test_feature_table_matches_label_features():
+    """The per-k feature table (statistics.feature_table, computed once per k on the GPU when
+    there is one) holds, bit for bit, the features label_features computes for each code's
+    compat label -- the function pinned to the reference's CSVs above."""
+    from kmerml.kmers.statistics import feature_table, label_features
+    for k in range(1, 8):
+        t = feature_table(k)
+        f = label_features(list(KmerFeatureBuilder.compat_labels(k)))
+        for name, want in f.items():
+            want = np.asarray(want)
+            got = t[name]
+            if want.dtype.kind == 'f':
+                assert np.array_equal(got.view(np.int64), want.view(np.int64)), (k, name)
+            else:
+                assert np.array_equal(got, want), (k, name)
+
+
+def test_feature_frame_table_path_equals_label_path(monkeypatch):
+    """feature_frame takes table rows for integer-parsed k-mer labels and the per-label path
+    for anything else (a digit outside 0-3, more digits than k); both give the same frame."""
+    import kmerml.kmers.statistics as st
+    rng = np.random.default_rng(5)
+    k = 7
+    codes = rng.choice(4 ** k, 3000, replace=False)
+    codes[:3] = [0, 1, 4 ** k - 1]
+    dig = np.array([0, 2, 3, 1])
+    lab = np.zeros(codes.size, np.int64)
+    for i in range(k):
+        lab = lab * 10 + dig[(codes >> (2 * (k - 1 - i))) & 3]
+    df = pd.DataFrame({'kmer': lab, 'count': rng.integers(1, 50, codes.size)})
+    assert np.array_equal(st.label_codes(df['kmer'].to_numpy(), k), codes)
+    fast = st.KmerFeatureExtractor.feature_frame(df, k, st.DEFAULT_FEATURES)
+    monkeypatch.setattr(st, "label_codes", lambda v, kk: None)
+    slow = st.KmerFeatureExtractor.feature_frame(df, k, st.DEFAULT_FEATURES)
+    assert fast.to_csv() == slow.to_csv()
+    monkeypatch.undo()
+    assert st.label_codes(np.array([104], np.int64), 3) is None          # digit 4
+    assert st.label_codes(np.array([1233], np.int64), 3) is None         # 4 digits at k = 3
+    assert st.label_codes(np.array(["12"], dtype=object), 2) is None     # text labels

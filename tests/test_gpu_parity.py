@@ -853,6 +853,24 @@ def test_from_count_matrix_gpu_equals_file_path(tmp_path, k):
     assert got.to_csv() == want.to_csv()
 
 
+def test_feature_table_on_gpu():
+    """statistics.feature_table computed on the GPU (float64 divisions, products and the
+    set-ordered entropy sums in torch on cuda) equals the host's label_features bit for bit."""
+    from kmerml.kmers import statistics as st
+    from kmerml.ml.features import KmerFeatureBuilder
+    assert torch.cuda.is_available()
+    st._TABLES.pop(9, None)
+    t = st.feature_table(9)
+    f = st.label_features(list(KmerFeatureBuilder.compat_labels(9)))
+    for name, want in f.items():
+        want = np.asarray(want)
+        got = t[name]
+        if want.dtype.kind == 'f':
+            assert np.array_equal(got.view(np.int64), want.view(np.int64)), name
+        else:
+            assert np.array_equal(got, want), name
+
+
 def _synth_row(oracle_lib, g, L=100_000_000, k=12, repeat=None):
     seq = oracle_lib.synth(L, osynth.genome_seed(g))
     if repeat:
