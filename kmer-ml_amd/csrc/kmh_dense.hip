@@ -296,7 +296,11 @@ __global__ __launch_bounds__(kPThreads, 2) void k_partition(const uint8_t* __res
             rb = load16(seq, base + 16, ge);
             rn = load16(seq, base + 32, ge);
         }
-        visit_raw<K>(ra, rb, rn, tail_mask(base, ge), tail_mask(base + 16, ge), tail_mask(base + 32, ge), km);
+        // tiles whose bytes all lie inside the genome (all but its last) need no tail masks
+        if (tstart + (uint64_t)kPTile + 16 <= ge)   // uniform per workgroup
+            visit_raw<K>(ra, rb, rn, 0u, 0u, 0u, km);
+        else
+            visit_raw<K>(ra, rb, rn, tail_mask(base, ge), tail_mask(base + 16, ge), tail_mask(base + 32, ge), km);
     }
     lds_barrier();
 

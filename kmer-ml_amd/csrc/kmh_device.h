@@ -44,8 +44,10 @@ __device__ __forceinline__ void enc4(uint32_t w, uint32_t& c8, uint32_t& i4) {
     const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, cb);  // "ACGT"[cb]
     const uint32_t e = (w & 0xDFDFDFDFu) ^ expect;                       // 0 byte = base
     const uint32_t nz = (((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e) & 0x80808080u;
-    i4 = ((nz >> 7) * 0x08040201u) >> 24;
-    c8 = (cb * 0x40100401u) >> 24;
+    // byte-weighted sums on the full-rate dot-product unit (v_dot4_u32_u8) instead of
+    // quarter-rate 32-bit multiplies: byte 0 gets the top bits
+    i4 = __builtin_amdgcn_udot4(nz >> 7, 0x01020408u, 0u, false);
+    c8 = __builtin_amdgcn_udot4(cb, 0x01041040u, 0u, false);
 }
 
 // 16 bytes -> 32-bit code word (first base in bits 31:30) + 16-bit invalid mask (first
