@@ -55,13 +55,11 @@ template <> struct Sp<uint32_t> {
     static constexpr int WPT = 32;                 // window starts per thread
     static constexpr int TILE = kSpThreads * WPT;  // 32768 window starts per tile (= kTile)
     static constexpr int CAPS = 20480;             // entries staged by one split item (80 KiB)
-    static constexpr int KB = 16;                  // keys a count lane loads per round
 };
 template <> struct Sp<uint64_t> {
     static constexpr int WPT = 16;
     static constexpr int TILE = kSpThreads * WPT;  // 16384
     static constexpr int CAPS = 10240;             // 80 KiB
-    static constexpr int KB = 8;
 };
 template <typename E> constexpr int epc() { return 16 / (int)sizeof(E); }   // entries per chunk
 constexpr int kMaxPasses = 256;
@@ -240,19 +238,47 @@ struct SplitItem {
 // per-wave queue: a wave takes bt tiles at a time (one per lane), lists the chunks that
 // cover their segments (tile-in-batch << 13 | chunk-in-tile) and streams them with kQU
 // loads in flight per lane; entries outside a segment are masked by position.
-template <typename E, typename F>
+//
+// Kept chunks (the split kernel walks a bucket twice, histogram then scatter): a wave whose
+// tiles form a single (first and last) queue step of at most 64 * kQU chunks -- the common case -- keeps them
+// in registers (kv, kq) on the first walk (REUSE = false sets kept) and the second walk
+// (REUSE = true) takes them from there instead of reading the entries again; the segment
+// bounds stay in the wave's LDS slo / shi, which nothing writes in between.
+struct Kept {
+    uint4 v[kQU];
+    uint32_t q[kQU];
+    bool kept;
+};
+
+template <bool REUSE, typename E, typename F>
 __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
                                             const uint16_t* __restrict__ toff, uint32_t ldt,
                                             uint32_t b, uint64_t ta, uint64_t tb, uint32_t bt,
-                                            uint32_t* q, uint32_t* slo, uint32_t* shi, F&& f) {
+                                            uint32_t* q, uint32_t* slo, uint32_t* shi, Kept& kc, F&& f) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint4* chunks = reinterpret_cast<const uint4*>(ent);
+    constexpr uint32_t EPC = (uint32_t)epc<E>();
+    if constexpr (REUSE) {
+        if (kc.kept) {   // wave-uniform
+#pragma unroll
+            for (int u = 0; u < kQU; ++u) {
+                const bool live = kc.q[u] != kEmpty;
+                const uint32_t qv = live ? kc.q[u] : 0u;
+                const uint32_t tl = qv >> 13, p0 = (qv & 8191u) * EPC;
+                const uint32_t l = slo[tl], h = live ? shi[tl] : 0u;
+#pragma unroll
+                for (int i = 0; i < (int)EPC; ++i) f(lane_of<E>(kc.v[u], i), p0 + i >= l && p0 + i < h);
+            }
+            return;
+        }
+    } else {
+        kc.kept = false;
+    }
     for (uint64_t tw = ta + (uint64_t)wave * bt; tw < tb; tw += (uint64_t)kNW * bt) {
         const uint64_t t = tw + (uint64_t)lane;
         const bool in = (uint32_t)lane < bt && t < tb;
         const uint32_t lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
         const uint32_t hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
-        constexpr uint32_t EPC = (uint32_t)epc<E>();
         const uint32_t c0 = lo / EPC, nc = hi > lo ? (hi + EPC - 1u) / EPC - c0 : 0u;
         uint32_t incl = nc;
 #pragma unroll
@@ -289,6 +315,18 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
 #pragma unroll
                     for (int i = 0; i < (int)EPC; ++i) f(lane_of<E>(v[u], i), p0 + i >= l && p0 + i < h);
                 }
+                if constexpr (!REUSE) {
+                    // the wave's only step, in one round: keep the chunks for the second walk
+                    if (total <= 64u * (uint32_t)kQU && tw == ta + (uint64_t)wave * bt &&
+                        tw + (uint64_t)kNW * bt >= tb) {
+                        kc.kept = true;
+#pragma unroll
+                        for (int u = 0; u < kQU; ++u) {
+                            kc.v[u] = v[u];
+                            kc.q[u] = qe[u];
+                        }
+                    }
+                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -323,8 +361,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
     // tail of `sorted`, so no exec-mask branch surrounds an atomic.
     const uint32_t dpass = (uint32_t)kMaxPasses + (uint32_t)(lane & 31);
-    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave],
-                [&](E r, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
+    Kept kc;
+    walk_bucket<false>(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc,
+                       [&](E r, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
     __syncthreads();
     // exclusive scan of the pass histogram (threads 0..255)
     uint32_t n0 = 0u, incl = 0u;
@@ -355,7 +394,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     __syncthreads();
     const uint32_t total = total_sh;
     if (total > (uint32_t)kCaps) return;  // staging overflow: the bucket goes to the fallback
-    walk_bucket(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], [&](E r, bool ok) {
+    walk_bucket<true>(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc, [&](E r, bool ok) {
         const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
         sorted[ok ? slot : (uint32_t)kCaps + (uint32_t)lane] = r;
     });
@@ -468,108 +507,151 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
         citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, s0, s1, (uint32_t)gb, n};
 }
 
-template <int SB, int NT, typename E>
-__global__ __launch_bounds__(NT) void k_sp_count(
+// Count work item: deduplication by a counting sort on the key's position inside its pass.
+// The keys of pass p of a bucket are the residues r with floor(r * np / 2^R) = p, so
+// (r * np) mod 2^R is increasing in r and spread evenly over [0, 2^R): its top 13 bits give
+// 8192 bins of about one key each (8192 keys per item).  Equal keys share a bin, so after a
+// counting sort (histogram, scan, scatter: one LDS atomic per key per pass over the keys,
+// no probing and no per-lane tail) a thread dedups its own 8 bins by comparing the few keys
+// of each.  A bin of more than kBig keys (a repeated k-mer) goes through a small LDS hash
+// table instead, so repeats cost what they cost the hash kernel before.
+constexpr int kBinBits = 13, kBins = 1 << kBinBits;
+constexpr int kBig = 32;         // keys of a bin deduplicated by comparison
+constexpr int kHSlots = 1024;    // hash table of the big bins
+constexpr int kMaxBig = 256;     // big bins of one item (more: the item goes to the fallback)
+constexpr int kCntThreads = 512; // two count workgroups per CU (74 KiB of LDS each) hide each
+                                 // other's load latency
+template <typename E> struct Cnt;
+template <> struct Cnt<uint32_t> { static constexpr int CAP = 8192; };   // keys of one item
+template <> struct Cnt<uint64_t> { static constexpr int CAP = 4096; };
+
+#ifdef KMH_EXPERIMENTS
+__device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks of k_sp_count
+#define KMH_PT(i) if (lane == 0) { const unsigned long long t_ = clock64(); pt[i] += t_ - tl; tl = t_; }
+#else
+#define KMH_PT(i)
+#endif
+
+template <typename E>
+__global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_count(
     const E* __restrict__ split, const uint16_t* __restrict__ toff2,
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
     const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
     uint32_t* __restrict__ counts, unsigned long long* __restrict__ nk,
-    const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed,
-    unsigned long long* __restrict__ prof) {
-    // Slot = key << CB | count (CB = 32 for u32 residues; 64 - R for u64 residues of R bits); a
-    // slot is empty iff its count is 0, so every residue (k = 21 uses all 32 bits) is a valid
-    // key.  A u64-residue count that would overflow its CB bits fails the item (the fallback
-    // recounts it).  Emission scans the table: for each of the
-    // kSlots / NT slot rows a wave reads 64 consecutive slots (conflict-free) and compacts
-    // the occupied ones to consecutive output positions (ballot + mbcnt), so the stores are
-    // coalesced and the insert loop keeps no record of the slots it claimed.
-    constexpr int kSlots = 1 << SB, kSlotBits = SB, kNW = NT / 64;
-    constexpr int kRows = kSlots / NT;             // slot rows per thread in the scan
-    constexpr int kCap = kSlots * 3 / 4;           // distinct keys one table may hold
-    __shared__ unsigned long long tbl[kSlots];
-    __shared__ unsigned long long dummy[NT];     // CAS target of lanes without a key
-    __shared__ uint32_t wtot[kNW], fail[2];
-    __shared__ unsigned long long obase;
-    constexpr uint32_t kMaxIter = 8u * 1024u;     // probes of one call (8 keys per lane)
-    constexpr uint32_t SM = kSlots - 1u;
-    constexpr int KB = Sp<E>::KB, kCaps = Sp<E>::CAPS;
+    const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
+    constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
+    constexpr int BQ = BPT / 4;   // uint4 words of a thread's bins
+    constexpr int kCaps = Sp<E>::CAPS, U = 4;
     constexpr bool WIDE = sizeof(E) == 8;
-    const int CB = WIDE ? 64 - R : 32;
-    const unsigned long long CM = (1ull << CB) - 1ull;
-    // slot hash: top bits of the low 32 bits of a 24 x 24-bit product (v_mul_u32_u24, full
-    // rate; v_mul_lo_u32 is quarter rate) of the key folded to 24 bits (a u64 key first folded
-    // to 32 bits)
-    auto slot_of = [](E key) -> uint32_t {
-        uint32_t x;
-        if constexpr (WIDE) x = (uint32_t)key ^ (uint32_t)(key >> 29) * 0x9E3779B1u;
-        else x = key;
-        return (uint32_t)__umul24(x ^ (x >> 15), 0x9E3779u) >> (32 - kSlotBits);
-    };
+    static_assert(BPT % 4 == 0 && HPT >= 1 && C % NT == 0, "thread layout");
+    __shared__ __attribute__((aligned(16))) uint32_t hist[kBins];
+    __shared__ __attribute__((aligned(16))) E sorted[C];
+    __shared__ unsigned long long htab[kHSlots];
+    __shared__ uint32_t bigl[kMaxBig];
+    __shared__ uint32_t wtot[kNW];
+    __shared__ uint32_t nbig, bad;
+    __shared__ unsigned long long obase;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t cap = limit < (uint32_t)kCap ? limit : (uint32_t)kCap;
-    const uint64_t below = (1ull << lane) - 1ull;   // lanes before this one
-    // The table is zero at the top of every item: zeroed once here, then by the emission of
-    // each item (every thread clears the slots it has just read).  fail[par] collects the
-    // probe-guard failures of the current item; the other flag is cleared for the next one.
-    uint4* t4 = reinterpret_cast<uint4*>(tbl);
-    for (int i = tid; i < kSlots / 2; i += NT) t4[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid < 2) fail[tid] = 0u;
-    lds_barrier();
-    uint32_t par = 0u;
+    // hash slot = key << CB | count (CB = 32 for u32 residues, 64 - R for u64: a count that
+    // would overflow its field fails the item)
+    const int CB = WIDE ? 64 - R : 32;
+    const unsigned long long CM = (1ull << CB) - 1ull;
+    const unsigned long long RMK = (1ull << R) - 1ull;   // R <= 54
+    const int SH = R - kBinBits;                         // R >= 16
+    const uint32_t cap = limit < (uint32_t)C ? limit : (uint32_t)C;
 
-    // Each lane walks its own keys one probe per iteration: CAS(empty -> key|1) claims a
-    // slot, a slot holding the key gets +1, anything else sends the key to the next slot,
-    // so an iteration waits on a single LDS round trip.  The key list advances by an
-    // unconditional select (a conditional shift compiled to phi copies), the slot hash is
-    // a full-rate 24-bit multiply, and the runaway guard is a wave-uniform (scalar)
-    // iteration count instead of a per-lane probe counter.
-    unsigned long long iters = 0, calls = 0;
-    auto insert_keys = [&](E (&r)[8], int n) {
-        ++calls;
-        uint32_t s = slot_of(r[0]);
-        for (uint32_t guard = 0; __ballot(n > 0); ++guard) {
-            ++iters;
-            if (guard == kMaxIter) {  // wave-uniform: a table this full goes to the fallback
-                if (n > 0) fail[par] = 1u;
-                break;
-            }
-            // Branch-free body: every lane issues the CAS and the add (a lane without keys
-            // works on its own dummy slot, a lane without a match adds 0), and all updates
-            // are selects, so the only branches are the uniform guard and the loop edge.
-            const bool act = n > 0;
-            unsigned long long* slot = act ? &tbl[s] : &dummy[tid];
-            const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)r[0] << CB) | 1ull);
-            const bool won = old == 0ull;
-            const bool match = !won && (E)(old >> CB) == r[0];
-            const unsigned long long prev = atomicAdd(slot, match ? 1ull : 0ull);
-            if constexpr (WIDE) {   // the add that finds the count field full carried into the key
-                if (match && (prev & CM) == CM) fail[par] = 1u;
-            }
-            const bool done = act && (won || match);
+    uint4* h4 = reinterpret_cast<uint4*>(hist);
+    auto zero_bins = [&] {
 #pragma unroll
-            for (int i = 0; i < 7; ++i) r[i] = done ? r[i + 1] : r[i];
-            n -= done ? 1 : 0;
-            uint32_t h = slot_of(r[0]);
-            asm volatile("" : "+v"(h));   // keep the hash unconditional (no branch around it)
-            s = done ? h : ((s + 1u) & SM);
-        }
+        for (int q = 0; q < BQ; ++q) h4[BQ * tid + q] = make_uint4(0u, 0u, 0u, 0u);
     };
+    zero_bins();
+#pragma unroll
+    for (int q = 0; q < HPT; ++q) htab[q * NT + tid] = 0ull;
+    if (tid == 0) nbig = bad = 0u;
+    lds_barrier();
+#ifdef KMH_EXPERIMENTS
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = clock64();
+#endif
 
-    // Persistent: NT-thread workgroups walk the items.
+    // Persistent: the workgroups walk the items.  Every branch on item data below is
+    // workgroup-uniform (the values come from LDS after a barrier or are computed alike by
+    // every wave), so all threads meet the same barriers.
     for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
     const CountItem it = items[item];
     if (gb_fail[it.gb]) continue;  // the split overflowed: the fallback counts this bucket
-    const unsigned long long c0 = prof ? clock64() : 0ull;
+    const uint32_t np = it.np;
+    auto bin_of = [&](E r) -> uint32_t { return (uint32_t)((((uint64_t)r * np) & RMK) >> SH); };
 
-    // The item's entries are segment p of each split item in [s0, s1).  Per group of up to
-    // 64 split items every wave reads the segment bounds (lane j: split item g + j), scans
-    // their lengths, and takes an equal share of the group's entries (concatenated in
-    // split-item order): entry e lies in the last segment whose exclusive start is <= e.
-    // Equal shares matter: the workgroup waits at the barrier for its slowest wave.
-    for (uint32_t g = it.s0; g < it.s1; g += 64u) {
-        const uint32_t ns = min(64u, it.s1 - g);
-        const uint32_t j = g + (uint32_t)lane;
+    // f(key) for every key of the item.  Per group of up to 64 split items every wave reads the
+    // segment bounds (lane j: split item g + j), scans their lengths and takes an equal share
+    // of the group's entries (concatenated in split-item order: entry e lies in the last
+    // segment whose exclusive start is <= e), U loads of 64 entries in flight.  Returns the
+    // item's key count.
+    auto walk = [&](auto&& f) -> uint32_t {
+        uint32_t ntot = 0u;
+        for (uint32_t g = it.s0; g < it.s1; g += 64u) {
+            const uint32_t ns = min(64u, it.s1 - g);
+            const uint32_t j = g + (uint32_t)lane;
+            uint32_t lo = 0u, len = 0u;
+            if ((uint32_t)lane < ns) {
+                lo = toff2[(uint64_t)j * kT2 + it.p];
+                len = (uint32_t)toff2[(uint64_t)j * kT2 + it.p + 1] - lo;
+            }
+            uint32_t incl = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t x = __shfl_up(incl, d);
+                if (lane >= d) incl += x;
+            }
+            const uint32_t n = __shfl(incl, 63), excl = incl - len;
+            ntot += n;
+            const uint64_t sb = (uint64_t)j * kCaps + lo - excl;   // segment base - its start
+            const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
+            const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
+            const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
+            for (uint32_t c = ea; c < eb; c += 64u * U) {
+                E r[U];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t e0 = c + 64u * (uint32_t)u;   // entry of lane 0
+                    const uint32_t e = e0 + (uint32_t)lane;
+                    ok[u] = e < eb;
+                    // lanes past the share read a valid entry (lane 0's, or entry c)
+                    const uint32_t e1 = e0 < eb ? e0 : c;
+                    const uint32_t es = ok[u] ? e : e1;
+                    int sj = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
+                    for (;;) {
+                        const uint32_t nx = __shfl(excl, sj < 63 ? sj + 1 : 63);
+                        const bool adv = sj + 1 < (int)ns && nx <= es;
+                        if (!__ballot(adv)) break;
+                        sj += adv ? 1 : 0;
+                    }
+                    const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
+                                          (uint32_t)__shfl((int)sb_lo, sj);
+                    r[u] = split[base + es];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (ok[u]) f(r[u]);
+            }
+        }
+        return ntot;
+    };
+
+    // 1. histogram of the bins.  An item of at most 64 split items (all but items of huge
+    //    buckets) is read once: every wave's share (<= C / kNW keys) is loaded in one round
+    //    of KPL loads per lane and kept in registers for the scatter.
+    constexpr int KPL = C / NT;                 // keys per lane of a single-group share
+    const bool single = it.s1 - it.s0 <= 64u;   // uniform
+    E kr[KPL];
+    uint32_t kn = 0u;                           // valid keys of this lane (a prefix of kr)
+    uint32_t ntot;
+    if (single) {
+        const uint32_t ns = it.s1 - it.s0;
+        const uint32_t j = it.s0 + (uint32_t)lane;
         uint32_t lo = 0u, len = 0u;
         if ((uint32_t)lane < ns) {
             lo = toff2[(uint64_t)j * kT2 + it.p];
@@ -582,25 +664,19 @@ __global__ __launch_bounds__(NT) void k_sp_count(
             if (lane >= d) incl += x;
         }
         const uint32_t n = __shfl(incl, 63), excl = incl - len;
-        // segment base in entries of `split`, minus the segment's exclusive start
-        const uint64_t sb = (uint64_t)j * kCaps + lo - excl;   // kCaps: entries per split item
+        ntot = n;
+        const uint64_t sb = (uint64_t)j * kCaps + lo - excl;
         const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
         const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
         const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
-        for (uint32_t c = ea; c < eb; c += 64u * KB) {
-            E r[KB];
-            int cnt = 0;
+        if (n <= (uint32_t)C && ea < eb) {
 #pragma unroll
-            for (int u = 0; u < KB; ++u) {
-                const uint32_t e0 = c + 64u * (uint32_t)u;        // entry of lane 0
+            for (int u = 0; u < KPL; ++u) {
+                const uint32_t e0 = ea + 64u * (uint32_t)u;
                 const uint32_t e = e0 + (uint32_t)lane;
-                const bool ok = e < eb;
-                // Lanes past the share read a valid entry instead (lane 0's, or entry c)
-                // so every load is in bounds; es >= e1 on every lane.
-                const uint32_t e1 = e0 < eb ? e0 : c;
-                const uint32_t es = ok ? e : e1;
-                // segment of e1 (wave-uniform), then step each lane forward to the segment
-                // of es; the loop is wave-uniform so every lane takes part in each shuffle
+                kn += e < eb ? 1u : 0u;
+                const uint32_t e1 = e0 < eb ? e0 : ea;
+                const uint32_t es = e < eb ? e : e1;
                 int sj = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
                 for (;;) {
                     const uint32_t nx = __shfl(excl, sj < 63 ? sj + 1 : 63);
@@ -610,90 +686,226 @@ __global__ __launch_bounds__(NT) void k_sp_count(
                 }
                 const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
                                       (uint32_t)__shfl((int)sb_lo, sj);
-                const E v = split[base + es];
-                r[u] = ok ? v : (E)0;
-                cnt += ok ? 1 : 0;   // valid entries of a lane are a prefix of r
+                kr[u] = split[base + es];
             }
-            // calls of 8 keys (a lane's valid keys are a prefix of r)
-            E a8[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) a8[u] = r[u];
-            insert_keys(a8, cnt < 8 ? cnt : 8);
-            if constexpr (KB == 16) {
-                E b8[8];
+            for (int u = 0; u < KPL; ++u)
+                if ((uint32_t)u < kn) atomicAdd(&hist[bin_of(kr[u])], 1u);
+        }
+    } else {
+        ntot = walk([&](E r) { atomicAdd(&hist[bin_of(r)], 1u); });
+    }
+    KMH_PT(0)
+    lds_barrier();
+    KMH_PT(1)
+    if (ntot > (uint32_t)C) {   // more keys than the staging holds: fallback (uniform)
+        zero_bins();
+        if (tid == 0) {
+            const uint32_t at = atomicAdd(&failed[0], 1u);
+            failed[1 + at] = item;
+        }
+        lds_barrier();
+        continue;
+    }
+
+    // 2. exclusive scan: thread t owns bins 8t .. 8t + 7; bins of more than kBig keys are listed
+    uint32_t v[BPT];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) b8[u] = r[u + 8];
-                if (__ballot(cnt > 8)) insert_keys(b8, cnt > 8 ? cnt - 8 : 0);
-            }
+    for (int q = 0; q < BQ; ++q) {
+        const uint4 a = h4[BQ * tid + q];
+        v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+    }
+    uint32_t tsum = 0u;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) tsum += v[i];
+    uint32_t incl = tsum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(incl, d);
+        if (lane >= d) incl += x;
+    }
+    if (lane == 63) wtot[wave] = incl;
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+        if (v[i] > (uint32_t)kBig) {
+            const uint32_t at = atomicAdd(&nbig, 1u);
+            if (at < (uint32_t)kMaxBig) bigl[at] = (uint32_t)(BPT * tid + i);
         }
     }
     lds_barrier();
-    const unsigned long long c1 = prof ? clock64() : 0ull;
-
-    // Emission.  Each thread reads its kRows slots (rows q * NT + 64 * wave + lane,
-    // conflict-free) into registers once, clears them for the next item, and the wave
-    // counts its occupied slots; after the output base is known the registers are stored
-    // (occupied slots compacted with ballot + mbcnt, so the stores are coalesced).
-    unsigned long long x[kRows];
-    uint32_t mine = 0u;
+    uint32_t st = incl - tsum;
+    for (int w = 0; w < wave; ++w) st += wtot[w];
+    {
+        uint32_t o[BPT];
 #pragma unroll
-    for (int q = 0; q < kRows; ++q) {
-        x[q] = tbl[q * NT + tid];
-        mine += (uint32_t)__builtin_popcountll(__ballot((x[q] & CM) != 0ull));
+        for (int i = 0; i < BPT; ++i) {
+            o[i] = st;
+            st += v[i];
+        }
+#pragma unroll
+        for (int q = 0; q < BQ; ++q) h4[BQ * tid + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
     }
+    lds_barrier();
+    KMH_PT(2)
+
+    // 3. scatter: hist[b] ends as the end of bin b
+    if (single) {
 #pragma unroll
-    for (int q = 0; q < kRows; ++q) tbl[q * NT + tid] = 0ull;
-    if (lane == 0) wtot[wave] = mine;
-    if (tid == 0) fail[par ^ 1u] = 0u;   // read by the previous item before this one began
+        for (int u = 0; u < KPL; ++u)
+            if ((uint32_t)u < kn) sorted[atomicAdd(&hist[bin_of(kr[u])], 1u)] = kr[u];
+    } else {
+        walk([&](E r) { sorted[atomicAdd(&hist[bin_of(r)], 1u)] = r; });
+    }
+    lds_barrier();
+    KMH_PT(3)
+    const uint32_t nb = nbig;
+
+    // 4. big bins: their keys into the hash table (linear probing, CAS(empty -> key|1), +1 on
+    //    a slot holding the key)
+    if (nb) {
+        if (nb > (uint32_t)kMaxBig) {
+            if (tid == 0) bad = 1u;
+        } else {
+            for (uint32_t x = 0; x < nb; ++x) {
+                const uint32_t b = bigl[x];
+                const uint32_t s = b ? hist[b - 1] : 0u, e = hist[b];
+                for (uint32_t i = s + (uint32_t)tid; i < e; i += NT) {
+                    const E key = sorted[i];
+                    uint32_t h = (uint32_t)key ^ (uint32_t)((uint64_t)key >> 29) * 0x9E3779B1u;
+                    h = (uint32_t)__umul24(h ^ (h >> 15), 0x9E3779u) >> (32 - 10);
+                    for (uint32_t probe = 0;; ++probe) {
+                        if (probe == (uint32_t)kHSlots) {
+                            bad = 1u;
+                            break;
+                        }
+                        unsigned long long* slot = &htab[h];
+                        const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)key << CB) | 1ull);
+                        if (old == 0ull) break;
+                        if ((E)(old >> CB) == key) {
+                            const unsigned long long prev = atomicAdd(slot, 1ull);
+                            if (WIDE && (prev & CM) == CM) bad = 1u;   // count field full
+                            break;
+                        }
+                        h = (h + 1u) & (uint32_t)(kHSlots - 1);
+                    }
+                }
+            }
+        }
+        lds_barrier();
+    }
+
+    // 5. emission, position-parallel: the key at sorted position i (i = j * NT + tid, so a wave
+    //    reads 64 consecutive keys) is emitted if no earlier key of its bin equals it, with the
+    //    number of equal keys of the bin as its count (bins hold about one key: the loops run
+    //    zero or one times); keys of big bins are emitted from the hash table instead.  First
+    //    the flags and counts (kept in registers), then the item's output base, then the
+    //    stores, compacted per wave with ballot + mbcnt so that they are coalesced.
+    E ek[KPL];
+    uint32_t ec[KPL];
+    uint32_t fm = 0u;   // bit j: position j * NT + tid is emitted
+#pragma unroll
+    for (int jj = 0; jj < KPL; ++jj) {
+        const uint32_t i = (uint32_t)(jj * NT + tid);
+        const uint32_t ic = i < ntot ? i : 0u;
+        const E key = sorted[ic];
+        const uint32_t b = bin_of(key);
+        const uint32_t bs = b ? hist[b - 1] : 0u, be = hist[b];
+        bool first = i < ntot && be - bs <= (uint32_t)kBig;
+        uint32_t c = 1u;
+        // bins of up to 4 keys (all but a fraction of a percent): four independent reads, so
+        // the twelve positions of a thread overlap their LDS round trips; larger bins loop
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t y = bs + (uint32_t)t;
+            const E o = sorted[y < be ? y : bs];
+            first = first && !(y < i && o == key);
+            c += (y > i && y < be && o == key) ? 1u : 0u;
+        }
+        if (first && be - bs > 4u) {
+            for (uint32_t y = bs + 4u; y < be; ++y) {
+                const E o = sorted[y];
+                first = first && !(y < i && o == key);
+                c += (y > i && o == key) ? 1u : 0u;
+            }
+        }
+        ek[jj] = key;
+        ec[jj] = c;
+        fm |= first ? (1u << jj) : 0u;
+    }
+    unsigned long long hs[HPT];
+#pragma unroll
+    for (int q = 0; q < HPT; ++q) hs[q] = nb ? htab[q * NT + tid] : 0ull;
+    uint32_t wmine = 0u;   // the wave's emitted keys
+#pragma unroll
+    for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
+#pragma unroll
+    for (int q = 0; q < HPT; ++q) wmine += (uint32_t)__popcll(__ballot((hs[q] & CM) != 0ull));
+    KMH_PT(4)
+    lds_barrier();   // everybody has read hist / htab / nbig of this item
+    if (lane == 0) wtot[wave] = wmine;
     lds_barrier();
     uint32_t before = 0u, used = 0u;
 #pragma unroll
     for (int w = 0; w < kNW; ++w) {
-        const uint32_t v = wtot[w];
-        before += w < wave ? v : 0u;
-        used += v;
+        const uint32_t x = wtot[w];
+        before += w < wave ? x : 0u;
+        used += x;
     }
-    const bool bad = fail[par] || used > cap;
+    KMH_PT(5)
+    const bool fail_item = bad != 0u || used > cap;
     if (tid == 0) {
-        if (bad) {
+        if (fail_item) {
             const uint32_t at = atomicAdd(&failed[0], 1u);
             failed[1 + at] = item;
         } else {
             obase = atomicAdd(&nk[it.g], (unsigned long long)used);
         }
     }
+    // clear this item's state for the next one (every read of it happened before the barrier above)
+    zero_bins();
+    if (nb) {
+#pragma unroll
+        for (int q = 0; q < HPT; ++q) htab[q * NT + tid] = 0ull;
+    }
     lds_barrier();
-    if (!bad) {
+    if (!fail_item) {
         const uint64_t at = out_off[it.g] + obase + before;
         const uint64_t hib = (uint64_t)it.b << R;
+        const uint64_t below = (1ull << lane) - 1ull;
         uint32_t run = 0u;
 #pragma unroll
-        for (int q = 0; q < kRows; ++q) {
-            const bool occ = (x[q] & CM) != 0ull;
-            const uint64_t m = __ballot(occ);
-            if (occ) {
-                const uint64_t i = at + run + (uint32_t)__builtin_popcountll(m & below);
-                // plain stores: the wave's rows form one contiguous run, and write-back
-                // stores merge the partial lines at row boundaries in L2 (exactly 12 B per
-                // distinct k-mer reach HBM); non-temporal stores wrote 32 % more bytes
-                codes[i] = hib | (x[q] >> CB);
-                counts[i] = (uint32_t)(x[q] & CM);
+        for (int jj = 0; jj < KPL; ++jj) {
+            const bool f = (fm >> jj) & 1u;
+            const uint64_t m = __ballot(f);
+            if (f) {
+                const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                codes[o] = hib | (uint64_t)ek[jj];
+                counts[o] = ec[jj];
             }
-            run += (uint32_t)__builtin_popcountll(m);
+            run += (uint32_t)__popcll(m);
+        }
+#pragma unroll
+        for (int q = 0; q < HPT; ++q) {
+            const bool f = (hs[q] & CM) != 0ull;
+            const uint64_t m = __ballot(f);
+            if (f) {
+                const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                codes[o] = hib | (hs[q] >> CB);
+                counts[o] = (uint32_t)(hs[q] & CM);
+            }
+            run += (uint32_t)__popcll(m);
         }
     }
-    par ^= 1u;
-    if (prof && tid == 0) {
-        const unsigned long long c2 = clock64();
-        atomicAdd(&prof[0], c1 - c0);
-        atomicAdd(&prof[1], c2 - c1);
-        atomicAdd(&prof[5], 1ull);
+    KMH_PT(6)
+    if (tid == 0) nbig = bad = 0u;
+    lds_barrier();   // sorted / nbig are reused by the next item
+    KMH_PT(7)
     }
-    }
-    if (prof && lane == 0) {
-        atomicAdd(&prof[3], iters);
-        atomicAdd(&prof[4], calls);
-    }
+#ifdef KMH_EXPERIMENTS
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_sp_prof[i], pt[i]);
+    if (tid == 0) atomicAdd(&g_sp_prof[8], 1ull);
+#endif
 }
 
 // Fallback, step 1: the residues of bucket b, pass p of genome g, in any order.
@@ -843,20 +1055,14 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
 
     const size_t tile_bytes = (size_t)kSpTile * sizeof(E);
     const size_t budget = env_mb("KMH_SP_BUDGET_MB", 16384) << 20;
-    // LDS hash table of the count kernel: 2^14 slots.  Experiment builds (-DKMH_EXPERIMENTS)
-    // also take KMH_SP_TABLE_BITS 12..13: smaller tables, several count workgroups per CU
-    // (measured slower).
-#ifdef KMH_EXPERIMENTS
-    const int table_bits = (int)std::min<long>(14, std::max<long>(12, env_long("KMH_SP_TABLE_BITS", 14)));
-#else
-    const int table_bits = 14;
-#endif
-    const unsigned wg_per_cu = 1u << (14 - table_bits);   // LDS-limited residency
-    const uint32_t target = (uint32_t)std::max<long>(1, env_long("KMH_SP_TARGET", 1l << (table_bits - 1)));
+    // Keys per count item (one pass of a bucket): the bin sort of k_sp_count stages at most
+    // Cnt<E>::CAP keys (8192 u32 / 4096 u64); the pass target leaves room for the spread of
+    // the pass sizes around it.
+    const uint32_t target = (uint32_t)std::max<long>(1, env_long("KMH_SP_TARGET", sizeof(E) == 4 ? 7680 : 3840));
     const uint32_t split_target = (uint32_t)std::max<long>(1, std::min<long>(env_long("KMH_SP_SPLIT", 12288), kCaps));
-    // KMH_SP_LIMIT caps the distinct keys of one table (tests force the fallback with it)
-    const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", 1l << table_bits)),
-                                                    1l << table_bits);
+    // KMH_SP_LIMIT caps the distinct keys of one item (tests force the fallback with it)
+    const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", Cnt<E>::CAP)),
+                                                    Cnt<E>::CAP);
     // batches of whole genomes whose step-1 entries fit the budget (at most 2^18 tiles)
     std::vector<std::pair<int, int>> batches;
     uint64_t max_tiles = 0;
@@ -954,41 +1160,26 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
         time_begin(ctx, s, "k_sp_count");
-        const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * wg_per_cu);
-        // KMH_SP_PROF=1 (experiment builds): per-phase cycle counters of k_sp_count on stderr
-        unsigned long long* d_prof = nullptr;
-#ifdef KMH_EXPERIMENTS
-        const bool prof = env_long("KMH_SP_PROF", 0) == 1;
-#else
-        const bool prof = false;
-#endif
-        if (prof) {
-            rc = ensure(ctx, ctx->sparse[7], 256);
-            if (rc) return rc;
-            d_prof = static_cast<unsigned long long*>(ctx->sparse[7].ptr);
-            KMH_HIP(ctx, hipMemsetAsync(d_prof, 0, 256, s));
-        }
-#define KMH_SP_COUNT(SB, NT)                                                                         \
-    hipLaunchKernelGGL((k_sp_count<SB, NT, E>), dim3(cgrid), dim3(NT), 0, s, d_split, d_toff2, d_citems, \
-                       (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts,                               \
-                       reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed, d_prof)
-#ifdef KMH_EXPERIMENTS
-        if (table_bits == 13) KMH_SP_COUNT(13, 1024);
-        else if (table_bits == 12) KMH_SP_COUNT(12, 512);
-        else
-#endif
-            KMH_SP_COUNT(14, 1024);
-#undef KMH_SP_COUNT
+        const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
+        hipLaunchKernelGGL(k_sp_count<E>, dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_toff2, d_citems, (uint32_t)nci,
+                           R, limit, d_out_off, d_codes, d_counts, reinterpret_cast<unsigned long long*>(d_nkmers),
+                           d_gbfail, d_failed);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
-        if (prof) {
-            unsigned long long h[8];
-            KMH_HIP(ctx, hipMemcpyAsync(h, d_prof, 64, hipMemcpyDeviceToHost, s));
+#ifdef KMH_EXPERIMENTS
+        if (env_long("KMH_SP_PROF", 0) == 1) {
+            unsigned long long h[16];
             KMH_HIP(ctx, hipStreamSynchronize(s));
-            std::fprintf(stderr, "k_sp_count prof: items %llu insert-phase cyc/item %.0f emit cyc/item %.0f "
-                         "iterations/call %.2f calls/item %.1f\n", h[5], (double)h[0] / h[5],
-                         (double)h[1] / h[5], (double)h[3] / (h[4] ? h[4] : 1), (double)h[4] / h[5]);
+            KMH_HIP(ctx, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sp_prof), sizeof(h)));
+            const double w = (double)h[8] * kNW;   // waves
+            std::fprintf(stderr, "k_sp_count per wave over %zu items on %u WGs: load+hist %.0f | bar %.0f | scan %.0f | "
+                         "scatter %.0f | big %.0f | count %.0f | write %.0f | bar %.0f Mcyc\n", nci, (unsigned)h[8],
+                         h[0] / w / 1e6, h[1] / w / 1e6, h[2] / w / 1e6, h[3] / w / 1e6, h[4] / w / 1e6,
+                         h[5] / w / 1e6, h[6] / w / 1e6, h[7] / w / 1e6);
+            const unsigned long long z[16] = {};
+            KMH_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_sp_prof), z, sizeof(z)));
         }
+#endif
         const double h3 = hprof ? now_ms() : 0.0;
         // passes left to the fallback: count items whose table overflowed, and every pass of
         // a bucket whose split overflowed

@@ -608,6 +608,32 @@ def test_sparse_dev_low_complexity(ctx, dev, oracle_lib, k):
             assert np.array_equal(got[g][1], wn)
 
 
+@pytest.mark.parametrize("k,canonical", [(21, 1), (19, 0), (27, 1)])
+def test_sparse_dev_repeats(ctx, dev, oracle_lib, k, canonical):
+    """Random genomes carrying repeats: 60 copies of a 2 kbp segment and 3000 of a 37 bp unit
+    (k-mers counted 60 to ~6000 times).  Their bins hold more keys than a thread compares, so
+    they go through the count kernel's LDS hash table beside ordinary keys of the same bins;
+    a 9-copy segment stays on the comparison path."""
+    rng = np.random.default_rng(500 + k)
+    seg = osynth.synth_bases(2000, osynth.genome_seed(71))
+    unit = osynth.synth_bases(37, osynth.genome_seed(72))
+    small = osynth.synth_bases(900, osynth.genome_seed(73))
+    parts = []
+    for i in range(60):
+        parts.append(osynth.synth_bases(int(rng.integers(500, 20_000)), osynth.genome_seed(1000 + i)))
+        parts.append(seg)
+        if i % 6 == 0:
+            parts.append(small)
+    a = np.concatenate(parts + [np.tile(unit, 3000)])
+    b = np.concatenate([osynth.synth_bases(700_000, osynth.genome_seed(74)), np.tile(seg, 5), a[:50_000]])
+    got = _sparse_dev(ctx, dev, [a, b], k, canonical)
+    for g, seq in enumerate((a, b)):
+        wc, wn, _ = oracle_lib.count_sparse(seq, k, canonical=bool(canonical))
+        assert wn.max() >= (60 if g == 0 else 5)
+        assert got[g][0].size == wc.size
+        assert np.array_equal(got[g][0], wc) and np.array_equal(got[g][1], wn)
+
+
 def test_sparse_dev_config5_genome(ctx, dev, oracle_lib):
     """One 25 Mbp synthetic genome (a tenth of a config-5 genome) at k = 21 canonical."""
     seq = osynth.synth_bases(25_000_000, osynth.genome_seed(0))
