@@ -62,6 +62,14 @@ template <> struct Sp<uint64_t> {
     static constexpr int CAPS = 10240;             // 80 KiB
 };
 template <typename E> constexpr int epc() { return 16 / (int)sizeof(E); }   // entries per chunk
+
+// Tiles a wave of the split kernel takes per queue step, for segments of about `per` entries
+// of `epc` per 16-byte chunk: a step fills at most half of the kQueue-chunk queue.
+__host__ __device__ __forceinline__ uint32_t split_bt(uint32_t per, uint32_t epc) {
+    uint32_t bt = (uint32_t)kQueue / 2u / (per / epc + 2u);
+    return bt < 1u ? 1u : (bt > 64u ? 64u : bt);
+}
+
 constexpr int kMaxPasses = 256;
 constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
@@ -354,8 +362,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid < kMaxPasses) hist[tid] = 0u;
     __syncthreads();
-    uint32_t bt = (uint32_t)kQueue / 2u / (it.per / (uint32_t)EPC + 2u);
-    bt = bt < 1u ? 1u : (bt > 64u ? 64u : bt);
+    const uint32_t bt = split_bt(it.per, (uint32_t)EPC);
     const uint32_t np = it.np;
     // Branch-free LDS atomics: an entry outside its segment counts into one of 32 dummy
     // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
@@ -418,12 +425,16 @@ struct CountItem {
 // passes (at most kMaxPasses), split items of ts tiles each (about split_target entries).
 struct GbRule {
     uint32_t np, per, ts, nsplit;
-    __device__ GbRule(uint32_t n, uint32_t nt, uint32_t target, uint32_t split_target) {
+    // ts is also capped at one queue step per wave of the split kernel, so that each wave
+    // reads its chunks once (k_sp_split keeps them in registers between its two walks)
+    __device__ GbRule(uint32_t n, uint32_t nt, uint32_t target, uint32_t split_target, uint32_t epc) {
         np = (n + target - 1u) / target;
         np = np < (uint32_t)kMaxPasses ? np : (uint32_t)kMaxPasses;
         per = nt ? (n + nt - 1u) / nt : 0u;
         ts = split_target / (per + 1u);
         ts = ts < 1u ? 1u : ts;
+        const uint32_t one_step = (uint32_t)kNW * split_bt(per, epc);
+        ts = ts < one_step ? ts : one_step;
         nsplit = n ? (nt + ts - 1u) / ts : 0u;
         if (!n) np = 0u;
     }
@@ -438,7 +449,7 @@ __device__ __forceinline__ uint32_t gb_tiles(const uint64_t* tbase, int g0, int 
 // (genome, bucket) pair, exclusive offsets of both in pair order, and the two totals.
 __global__ __launch_bounds__(1024) void k_sp_plan(const uint32_t* __restrict__ nb, int ngb,
                                                   const uint64_t* __restrict__ tbase, int g0,
-                                                  uint32_t target, uint32_t split_target,
+                                                  uint32_t target, uint32_t split_target, uint32_t epc,
                                                   uint32_t* __restrict__ sofs, uint32_t* __restrict__ cofs,
                                                   uint32_t* __restrict__ totals) {
     __shared__ uint32_t ws[16], wc[16];
@@ -447,7 +458,7 @@ __global__ __launch_bounds__(1024) void k_sp_plan(const uint32_t* __restrict__ n
     const int a = tid * per_t, e = min(ngb, a + per_t);
     uint32_t ns = 0u, nc = 0u;
     for (int gb = a; gb < e; ++gb) {
-        const GbRule r(nb[gb], gb_tiles(tbase, g0, gb), target, split_target);
+        const GbRule r(nb[gb], gb_tiles(tbase, g0, gb), target, split_target, epc);
         ns += r.nsplit;
         nc += r.np;
     }
@@ -472,7 +483,7 @@ __global__ __launch_bounds__(1024) void k_sp_plan(const uint32_t* __restrict__ n
     }
     uint32_t os = bs + is - ns, oc = bc + ic - nc;
     for (int gb = a; gb < e; ++gb) {
-        const GbRule r(nb[gb], gb_tiles(tbase, g0, gb), target, split_target);
+        const GbRule r(nb[gb], gb_tiles(tbase, g0, gb), target, split_target, epc);
         sofs[gb] = os;
         cofs[gb] = oc;
         os += r.nsplit;
@@ -488,6 +499,7 @@ __global__ __launch_bounds__(1024) void k_sp_plan(const uint32_t* __restrict__ n
 __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
                                                 const uint64_t* __restrict__ tbase, int g0,
                                                 uint64_t tile_lo, uint32_t target, uint32_t split_target,
+                                                uint32_t epc,
                                                 const uint32_t* __restrict__ sofs,
                                                 const uint32_t* __restrict__ cofs,
                                                 SplitItem* __restrict__ sitems, CountItem* __restrict__ citems) {
@@ -497,7 +509,7 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
     const int g = g0 + gb / kSpBuckets;
     const uint32_t b = (uint32_t)(gb % kSpBuckets);
     const uint32_t ta = (uint32_t)(tbase[g] - tile_lo), tb = (uint32_t)(tbase[g + 1] - tile_lo);
-    const GbRule r(n, tb - ta, target, split_target);
+    const GbRule r(n, tb - ta, target, split_target, epc);
     const uint32_t s0 = sofs[gb], s1 = s0 + r.nsplit;
     for (uint32_t i = threadIdx.x; i < r.nsplit; i += 64u) {
         const uint32_t t = ta + i * r.ts;
@@ -1122,7 +1134,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
                            L.tbase[g0], d_nb);
         KMH_HIP(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_sp_plan, dim3(1), dim3(1024), 0, s, d_nb, (int)ngb, d_tbase, g0, target,
-                           split_target, d_sofs, d_cofs, d_totals);
+                           split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_totals);
         KMH_HIP(ctx, hipGetLastError());
         uint32_t totals[2] = {0u, 0u};
         KMH_HIP(ctx, hipMemcpyAsync(totals, d_totals, 8, hipMemcpyDeviceToHost, s));
@@ -1150,7 +1162,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         uint64_t* d_out_off = reinterpret_cast<uint64_t*>(base + sib + cib);
         uint32_t* d_failed = reinterpret_cast<uint32_t*>(base + sib + cib + ob);
         hipLaunchKernelGGL(k_sp_fill, dim3((unsigned)ngb), dim3(64), 0, s, d_nb, d_tbase, g0, L.tbase[g0],
-                           target, split_target, d_sofs, d_cofs, d_sitems, d_citems);
+                           target, split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_sitems, d_citems);
         KMH_HIP(ctx, hipGetLastError());
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
