@@ -1,9 +1,9 @@
 // kmh_hash.hip -- device-resident sparse k-mer counting (13 <= k <= 32, forward or
 // canonical) for BASELINE config 5: 250 Mbp genomes at k = 21, where 4^k bins cannot be
 // tabulated and almost every k-mer is distinct.  The reference counts into a Python dict
-// (a hash table, /root/reference/kmerml/kmers/generate.py:36,58); here the counting is done
-// by LDS hash tables after two partition passes, so every hash insert is an LDS operation
-// and every kernel streams whole 16-byte chunks:
+// (a hash table, /root/reference/kmerml/kmers/generate.py:36,58); here the keys are
+// partitioned twice until one pass of a bucket fits a workgroup's LDS, and then deduplicated
+// there by a counting sort; every kernel streams whole 16-byte chunks:
 //
 //  1. k_sp_partition  one workgroup per 32768-window tile: forward (and reverse-complement)
 //                     codes from 2-bit packed registers, bucket = top 10 bits of the code
@@ -12,20 +12,20 @@
 //                     one coalesced store of the tile's entries and an exact
 //                     bucket-major offset table toff[bucket][tile] (u16 entry indices).
 //  2. k_sp_sizes      entries per (genome, bucket).  The host splits every bucket into
-//                     P = ceil(entries / 8192) passes over equal residue ranges (one LDS hash
-//                     table each) and into split items of ~12K entries (ranges of tiles).
+//                     P = ceil(entries / 7680) passes over equal residue ranges (one count
+//                     item each) and into split items of ~12K entries (ranges of tiles).
 //  3. k_sp_split      one workgroup per split item: gathers the bucket's segments of its
 //                     tiles (16-byte chunk loads, entries outside the segment masked by
 //                     position), partitions them by pass (LDS histogram, scan, scatter) and
 //                     stores them contiguously with per-pass offsets toff2[item][pass].
-//  4. k_sp_count      one workgroup per (genome, bucket, pass): reads that pass's segment of
-//                     every split item of the bucket, inserts it into a 16384-slot LDS hash
-//                     table (linear probing, 64-bit key|count slots; for u64 residues the count
-//                     takes the 64 - (2k - 10) bits the key leaves, and an item whose count
-//                     would overflow them goes to the fallback), then scans the table and
-//                     appends the distinct k-mers to the genome's output (one atomic cursor).
-//  5. fallback        a split item whose entries exceed its staging, or a pass whose distinct
-//                     keys exceed the table limit, emits nothing; those passes are counted by
+//  4. k_sp_count      one item per (genome, bucket, pass), two persistent workgroups per CU:
+//                     reads that pass's segment of every split item of the bucket into
+//                     registers and deduplicates it by an LDS counting sort on the key's
+//                     position inside the pass (8192 bins of about one key; equal keys share
+//                     a bin), then emits each distinct key with its count, position-parallel;
+//                     bins of repeated keys go through a small LDS hash table.
+//  5. fallback        a split item whose entries exceed its staging, or an item the count
+//                     kernel cannot hold, emits nothing; those passes are counted by
 //                     gather + hipCUB radix sort + run-length encode from the step-1 entries
 //                     (keys of different passes are disjoint, so nothing is counted twice).
 #include <hipcub/hipcub.hpp>
