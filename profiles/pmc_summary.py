@@ -1,6 +1,8 @@
 """Merge rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_traffic.json.
 
-    python profiles/pmc_summary.py FETCH_CSV WRITE_CSV KEY_SUFFIX [NOTE]
+    python profiles/pmc_summary.py FETCH_CSV WRITE_CSV KEY_SUFFIX [NOTE] [KERNELS]
+
+KERNELS (comma-separated short names) keeps only those kernels' entries.
 
 For each kernel: mean FETCH_SIZE and WRITE_SIZE (KB) per dispatch and
 hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (FETCH_SIZE doubled: gfx950
@@ -37,11 +39,14 @@ def main():
 
     fetch_csv, write_csv, suffix = sys.argv[1:4]
     note = sys.argv[4] if len(sys.argv) > 4 else ""
+    keep = set(sys.argv[5].split(",")) if len(sys.argv) > 5 and sys.argv[5] else None
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     d = json.load(open(OUT)) if os.path.exists(OUT) else {}
     bid = _native.build_id()
     for k in sorted(set(f) & set(w)):
+        if keep is not None and k not in keep:
+            continue
         fk, n = f[k]
         wk, _ = w[k]
         entry = {"FETCH_SIZE_KB": round(fk, 1), "WRITE_SIZE_KB": round(wk, 1), "dispatches": n,
