@@ -415,9 +415,12 @@ struct U4Out {
 __device__ __forceinline__ uint32_t sat4(uint32_t x) { return x < 15u ? x : 15u; }
 
 // The first nv entries of one 16-byte chunk (8 suffixes) into the table; the other slots add 0
-// (branch-free).  The eight returning adds go out back to back; a wrap (an added-to half that
-// held 0xFFFF) is looked for once per chunk through the maximum of the returned halves (an
-// add-0 slot at 0xFFFF is a false alarm that the rare path sorts out).
+// (branch-free).  EXACT = false (the first pass over a bucket): plain adds, whose returned
+// values nobody waits for.  EXACT = true (the recount of a bucket in which some bin passed
+// 65535): the eight returning adds go out back to back; a wrap (an added-to half that held
+// 0xFFFF) is looked for once per chunk through the maximum of the returned halves (an add-0
+// slot at 0xFFFF is a false alarm that the rare path sorts out).
+template <bool EXACT>
 __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv, const FixLog& L,
                                             uint64_t row0, uint32_t* wrapped) {
     const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
@@ -432,6 +435,7 @@ __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv,
         old[i] = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tbl) + addr),
                                         add << off[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    if constexpr (!EXACT) return;
     uint32_t mx = 0u;
 #pragma unroll
     for (int i = 0; i < 8; i += 2)
@@ -480,7 +484,8 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     constexpr int WORDS = (int)kCBins / 2;
     __shared__ __attribute__((aligned(16))) uint32_t tbl[WORDS];
     __shared__ uint32_t queue[NW][QMAX];     // chunk queues; escape staging of the epilogue
-    __shared__ uint32_t wrapped, ecnt, ebase;
+    __shared__ uint32_t wrapped, ecnt, ebase, nent;
+    __shared__ unsigned long long hsum;
 
     const uint32_t w = xcd_work_id();
     const int s = (int)(w % (uint32_t)S);
@@ -498,6 +503,8 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     if (threadIdx.x == 0) {
         wrapped = 0u;
         ecnt = 0u;
+        nent = 0u;
+        hsum = 0ull;
     }
     __syncthreads();
 
@@ -510,101 +517,168 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
         hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
     };
-    uint32_t lo_n = 0, hi_n = 0;
-    uint64_t tw = ta + (uint64_t)wave * BT;
-    if (tw < tb) bounds(tw, lo_n, hi_n);
-    for (; tw < tb; tw += (uint64_t)NW * BT) {
-        const uint32_t c0 = lo_n & 0xFFFu, nc = (hi_n & 0xFFFu) - c0;
-        const uint32_t nlast = 8u - (lo_n >> 12);
-        const uint32_t incl = scan64(nc);
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint64_t cbat = tw * (uint64_t)CPT;                  // the batch's first chunk
-        const uint32_t crel = (uint32_t)lane * CPT + c0;           // this segment's, relative
-        if (total <= (uint32_t)QMAX) {
-            const uint32_t ex = incl - nc;
-            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = (crel + j) | ((j + 1 == nc ? nlast - 1u : 7u) << 20);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t qe[U];
+    // One pass over the bucket's segments into the table; returns this lane's share of the
+    // bucket's entries.
+    auto walk = [&](auto exact) -> uint32_t {
+        constexpr bool EX = decltype(exact)::value;
+        uint32_t ent = 0u;
+        uint32_t lo_n = 0, hi_n = 0;
+        uint64_t tw = ta + (uint64_t)wave * BT;
+        if (tw < tb) bounds(tw, lo_n, hi_n);
+        for (; tw < tb; tw += (uint64_t)NW * BT) {
+            const uint32_t c0 = lo_n & 0xFFFu, nc = (hi_n & 0xFFFu) - c0;
+            const uint32_t nlast = 8u - (lo_n >> 12);
+            ent += nc ? 8u * nc - (lo_n >> 12) : 0u;
+            const uint32_t incl = scan64(nc);
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            const uint64_t cbat = tw * (uint64_t)CPT;                  // the batch's first chunk
+            const uint32_t crel = (uint32_t)lane * CPT + c0;           // this segment's, relative
+            if (total <= (uint32_t)QMAX) {
+                const uint32_t ex = incl - nc;
+                for (uint32_t j = 0; j < nc; ++j) q[ex + j] = (crel + j) | ((j + 1 == nc ? nlast - 1u : 7u) << 20);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint32_t qe[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t e = (uint32_t)(u * 64 + lane);
-                qe[u] = e < total ? q[e] : 0u;                       // idle lanes re-read chunk 0
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t e = (uint32_t)(u * 64 + lane);
+                    qe[u] = e < total ? q[e] : 0u;                       // idle lanes re-read chunk 0
+                }
+                uint4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = chunks[cbat + (qe[u] & 0xFFFFFu)];
+                // next batch's bounds load behind this batch's data loads
+                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if ((uint32_t)(u * 64 + lane) < total)
+                        count_chunk<EX>(tbl, v[u], (qe[u] >> 20) + 1u, L, row0, &wrapped);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else {
+                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+                for (uint32_t j = 0; j < nc; ++j)
+                    count_chunk<EX>(tbl, chunks[cbat + crel + j], j + 1 == nc ? nlast : 8u, L, row0, &wrapped);
             }
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = chunks[cbat + (qe[u] & 0xFFFFFu)];
-            // next batch's bounds load behind this batch's data loads
-            if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if ((uint32_t)(u * 64 + lane) < total) count_chunk(tbl, v[u], (qe[u] >> 20) + 1u, L, row0, &wrapped);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else {
-            if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
-            for (uint32_t j = 0; j < nc; ++j)
-                count_chunk(tbl, chunks[cbat + crel + j], j + 1 == nc ? nlast : 8u, L, row0, &wrapped);
         }
+        return ent;
+    };
+    // First pass with plain adds.  A bin that passes 65535 wraps its u16 half (a low half also
+    // carries into its partner), and every such event lowers the sum of the table's halves
+    // (by 65536, or 65535 for a low half), so the table is exact iff that sum equals the
+    // bucket's entries; otherwise the bucket is counted again with returning adds, which log
+    // every wrap (skewed genomes only: uniform 100 Mbp genomes stay below 65536 per bin).
+    const uint32_t ent = walk(std::false_type{});
+    {
+        uint32_t e = ent;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) e += __shfl_xor(e, d);
+        if (lane == 0) atomicAdd(&nent, e);
     }
-    __syncthreads();
-
-    // Widen the u16 pairs into the u32 row slice (plain stores, or adds when split).  ENC (S = 1
-    // only): also the slice's u4 nibbles (one u32 of 8 counts per thread and step) and its
-    // escapes, staged in the LDS of the queues and appended behind one global atomic.
+    // the halves' sum of this thread's table words (64 halves of at most 65535: fits 32 bits),
+    // added into hsum
+    auto add_hsum = [&](uint32_t hs) {
+        unsigned long long h = hs;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d);
+        if (lane == 0) atomicAdd(&hsum, h);
+    };
+    auto halves = [](uint4 x) {
+        return (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) +
+               (x.z & 0xFFFFu) + (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
+    };
+    // Plain row stores (no u4 epilogue, one workgroup per bucket) can be redone, so there the
+    // check rides on the widening's own read of the table; otherwise it reads the table first.
+    // A failed check clears the table and counts the bucket again exactly (one call site of
+    // each walk: a third inlined copy made the compiler spill to scratch).
+    const bool post = !ENC && S == 1;   // uniform
+    bool exact = false, enc = false;
     constexpr uint32_t kStage = (uint32_t)(NW * QMAX) / 2;   // (index, value) pairs
     uint32_t* stage = &queue[0][0];
-    const bool enc = ENC && wrapped == 0u;                     // uniform
-    if (ENC && wrapped != 0u && threadIdx.x == 0) {            // k_reencode redoes this bucket
-        const uint32_t at = atomicAdd(E.redo, 1u);
-        E.redo[1 + at] = (uint32_t)g * NBK + b;
-    }
-    uint32_t* orow = out + row0;
-    for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
-        const uint4 x = tbl4[i];
-        const uint4 lo4 = make_uint4(x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16);
-        const uint4 hi4 = make_uint4(x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16);
-        if (S == 1) {
-            store_nt(reinterpret_cast<uint4*>(orow) + 2 * i, lo4);
-            store_nt(reinterpret_cast<uint4*>(orow) + 2 * i + 1, hi4);
-            if (enc) {
-                const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-                uint32_t w = 0u, ne = 0u;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    w |= sat4(e[j]) << (4 * j);
-                    ne += e[j] >= 15u ? 1u : 0u;
-                }
-                E.nib[row0 / 8 + (uint64_t)i] = w;
-                if (ne) {   // ~1 in 100 threads for uniform 100 Mbp genomes at k = 12
-                    uint32_t at = atomicAdd(&ecnt, ne);
+    for (;;) {
+        if (exact) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
+            __syncthreads();
+            walk(std::true_type{});
+        }
+        __syncthreads();
+        if (!post && !exact) {
+            uint32_t hs0 = 0u;
+            for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) hs0 += halves(tbl4[i]);
+            add_hsum(hs0);
+            __syncthreads();
+            if (hsum != (unsigned long long)nent) {   // uniform
+                exact = true;
+                continue;
+            }
+        }
+        // Widen the u16 pairs into the u32 row slice (plain stores, or adds when split).  ENC (S = 1
+        // only): also the slice's u4 nibbles (one u32 of 8 counts per thread and step) and its
+        // escapes, staged in the LDS of the queues and appended behind one global atomic.
+        enc = ENC && wrapped == 0u;                                // uniform
+        if (ENC && wrapped != 0u && threadIdx.x == 0) {            // k_reencode redoes this bucket
+            const uint32_t at = atomicAdd(E.redo, 1u);
+            E.redo[1 + at] = (uint32_t)g * NBK + b;
+        }
+        uint32_t* orow = out + row0;
+        uint32_t hs = 0u;
+        for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
+            const uint4 x = tbl4[i];
+            const uint4 lo4 = make_uint4(x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16);
+            const uint4 hi4 = make_uint4(x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16);
+            if (S == 1) {
+                store_nt(reinterpret_cast<uint4*>(orow) + 2 * i, lo4);
+                store_nt(reinterpret_cast<uint4*>(orow) + 2 * i + 1, hi4);
+                if (post && !exact) hs += halves(x);
+                if (enc) {
+                    const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+                    uint32_t w = 0u, ne = 0u;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        if (e[j] >= 15u) {
-                            const uint32_t idx = (uint32_t)(row0 + 8 * (uint64_t)i + j);
-                            if (at < kStage) {
-                                stage[2 * at] = idx;
-                                stage[2 * at + 1] = e[j];
-                            } else {   // a skewed bucket: past the staging, one global atomic each
-                                const uint32_t gat = atomicAdd(E.esc_n, 1u);
-                                if (gat < E.cap) {
-                                    E.esc[2 * (uint64_t)gat] = idx;
-                                    E.esc[2 * (uint64_t)gat + 1] = e[j];
+                        w |= sat4(e[j]) << (4 * j);
+                        ne += e[j] >= 15u ? 1u : 0u;
+                    }
+                    E.nib[row0 / 8 + (uint64_t)i] = w;
+                    if (ne) {   // ~1 in 100 threads for uniform 100 Mbp genomes at k = 12
+                        uint32_t at = atomicAdd(&ecnt, ne);
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            if (e[j] >= 15u) {
+                                const uint32_t idx = (uint32_t)(row0 + 8 * (uint64_t)i + j);
+                                if (at < kStage) {
+                                    stage[2 * at] = idx;
+                                    stage[2 * at + 1] = e[j];
+                                } else {   // a skewed bucket: past the staging, one global atomic each
+                                    const uint32_t gat = atomicAdd(E.esc_n, 1u);
+                                    if (gat < E.cap) {
+                                        E.esc[2 * (uint64_t)gat] = idx;
+                                        E.esc[2 * (uint64_t)gat + 1] = e[j];
+                                    }
                                 }
+                                ++at;
                             }
-                            ++at;
                         }
                     }
                 }
-            }
-        } else if (ta < tb) {
-            const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+            } else if (ta < tb) {
+                const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (e[j]) atomicAdd(&orow[8 * i + j], e[j]);
+                for (int j = 0; j < 8; ++j)
+                    if (e[j]) atomicAdd(&orow[8 * i + j], e[j]);
+            }
         }
+        if (post && !exact) {   // uniform
+            add_hsum(hs);
+            lds_barrier();   // not __syncthreads(): the slice's stores drain behind it
+            if (hsum != (unsigned long long)nent) {
+                exact = true;
+                continue;
+            }
+        }
+        break;
     }
     if (ENC) {
         __syncthreads();
