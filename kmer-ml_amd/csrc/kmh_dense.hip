@@ -589,17 +589,21 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         return (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) +
                (x.z & 0xFFFFu) + (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
     };
-    // Plain row stores (no u4 epilogue, one workgroup per bucket) can be redone, so there the
-    // check rides on the widening's own read of the table; otherwise it reads the table first.
-    // A failed check clears the table and counts the bucket again exactly (one call site of
-    // each walk: a third inlined copy made the compiler spill to scratch).
-    const bool post = !ENC && S == 1;   // uniform
+    // With one workgroup per bucket (S = 1) the row slice and its nibbles can be rewritten, so
+    // the check rides on the widening's own read of the table: the first widening keeps its
+    // escapes in LDS (a bucket past the staging is left to k_reencode, which encodes it from
+    // the rows), and a failed check drops them, counts the bucket again exactly (the wraps
+    // make it a k_reencode bucket) and widens again.  With split rows (S > 1, added with
+    // atomics) the table is checked before it is widened.  One call site of each walk (a
+    // third inlined copy made the compiler spill to scratch).
+    const bool post = S == 1;   // uniform
     bool exact = false, enc = false;
     constexpr uint32_t kStage = (uint32_t)(NW * QMAX) / 2;   // (index, value) pairs
     uint32_t* stage = &queue[0][0];
     for (;;) {
         if (exact) {
             __syncthreads();
+            if (threadIdx.x == 0) ecnt = 0u;   // the first widening's staged escapes are dropped
             for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
             __syncthreads();
             walk(std::true_type{});
@@ -619,10 +623,6 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         // only): also the slice's u4 nibbles (one u32 of 8 counts per thread and step) and its
         // escapes, staged in the LDS of the queues and appended behind one global atomic.
         enc = ENC && wrapped == 0u;                                // uniform
-        if (ENC && wrapped != 0u && threadIdx.x == 0) {            // k_reencode redoes this bucket
-            const uint32_t at = atomicAdd(E.redo, 1u);
-            E.redo[1 + at] = (uint32_t)g * NBK + b;
-        }
         uint32_t* orow = out + row0;
         uint32_t hs = 0u;
         for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
@@ -651,13 +651,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
                                 if (at < kStage) {
                                     stage[2 * at] = idx;
                                     stage[2 * at + 1] = e[j];
-                                } else {   // a skewed bucket: past the staging, one global atomic each
-                                    const uint32_t gat = atomicAdd(E.esc_n, 1u);
-                                    if (gat < E.cap) {
-                                        E.esc[2 * (uint64_t)gat] = idx;
-                                        E.esc[2 * (uint64_t)gat + 1] = e[j];
-                                    }
-                                }
+                                }   // past the staging: k_reencode encodes this bucket
                                 ++at;
                             }
                         }
@@ -682,6 +676,11 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     }
     if (ENC) {
         __syncthreads();
+        if (ecnt > kStage) enc = false;                            // uniform
+        if (!enc && threadIdx.x == 0) {                            // k_reencode redoes this bucket
+            const uint32_t at = atomicAdd(E.redo, 1u);
+            E.redo[1 + at] = (uint32_t)g * NBK + b;
+        }
         const uint32_t n = min(ecnt, kStage);
         if (enc && threadIdx.x == 0) ebase = n ? atomicAdd(E.esc_n, n) : 0u;
         __syncthreads();
