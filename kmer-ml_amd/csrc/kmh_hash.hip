@@ -89,6 +89,7 @@ __device__ __forceinline__ uint64_t window(uint64_t hi, uint64_t lo, int j) {
     constexpr uint64_t M = K == 32 ? ~0ull : (1ull << (2 * K)) - 1ull;
     const int e = 2 * (j + K);  // bit end (MSB-first) of the window
     if (e <= 64) return (hi >> (64 - e)) & M;
+    if (e == 128) return lo & M;  // (a 64-bit shift by 64 is undefined)
     return ((hi << (e - 64)) | (lo >> (128 - e))) & M;
 }
 
@@ -123,14 +124,26 @@ __device__ __forceinline__ Bases load_bases(const uint8_t* __restrict__ seq, uin
 }
 
 // f(code) for every valid window of this thread (canonical: min(forward, reverse complement)).
+// The reverse complements come from the reverse complement of the whole 64-base block, taken
+// once per thread: window j's is the K bases of that block starting at base 64 - j - K, so it
+// costs a constant-shift extract like the forward code instead of a bit reversal per window.
 template <int K, int CANON, int WPT, typename F>
 __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
+    // laundered: each call recomputes its codes rather than keeping the 2 x 32 of the first
+    // call alive across the caller's barrier and scan (that spilled)
+    uint64_t hi = b.hi, lo = b.lo;
+    asm volatile("" : "+v"(hi), "+v"(lo));
+    uint64_t rhi = 0ull, rlo = 0ull;
+    if constexpr (CANON != 0) {
+        rhi = revcomp<32>(lo);
+        rlo = revcomp<32>(hi);
+    }
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
         if (((b.inv << j) >> (64 - K)) == 0ull) {
-            uint64_t c = window<K>(b.hi, b.lo, j);
-            if (CANON) {
-                const uint64_t r = revcomp<K>(c);
+            uint64_t c = window<K>(hi, lo, j);
+            if constexpr (CANON != 0) {
+                const uint64_t r = window<K>(rhi, rlo, 64 - j - K);
                 c = r < c ? r : c;
             }
             f(c);
