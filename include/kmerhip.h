@@ -149,16 +149,16 @@ int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, i
 
 /* ---- sparse counting, device-resident batch (BASELINE config 5) --------------- */
 /* The reference counts every k in a Python dict, a hash table (generate.py:36,58); for
- * 13 <= k <= 32 this counts G device-resident genomes (layout as kmh_count_dense_dev)
- * with partitioned LDS hash tables (u32 residues up to k = 21, u64 beyond; a count too large
- * for the bits a u64 residue leaves in its table slot sends that pass to the exact
- * sort-based fallback).  canonical != 0 counts min(forward, reverse
+ * 13 <= k <= 32 this counts G device-resident genomes (layout as kmh_count_dense_dev):
+ * two partition passes bring one pass of a bucket into a workgroup's LDS, where a counting
+ * sort deduplicates it (u32 residues up to k = 21, u64 beyond; what the LDS cannot hold
+ * goes to the exact sort-based fallback).  canonical != 0 counts min(forward, reverse
  * complement) codes.  Genome g's distinct k-mers (2-bit codes, A0 C1 G2 T3, first base
  * most significant) and their exact counts are written to d_codes / d_counts starting at
  * entry out_off[g] (kmh_sparse_out_offsets: the number of windows of the genomes before
  * g, so a genome never needs more room than its windows); d_nkmers[g] (device) receives
- * the number of distinct k-mers.  Order within a genome is unspecified (grouped by the
- * top 11 bits of the code).  Synchronises `stream` (the work list depends on the bucket
+ * the number of distinct k-mers.  Order within a genome is unspecified (grouped by bucket,
+ * the top 10 bits of the code, and pass).  Synchronises `stream` (the work list depends on the bucket
  * sizes). */
 int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
                          int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
