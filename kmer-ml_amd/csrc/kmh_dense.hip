@@ -7,11 +7,11 @@
 //   k <= 9   k_direct:     each workgroup counts a span of one genome into an LDS table
 //                          (4^k bins, or 32768-bin slices in 4^k/32768 passes for k = 8, 9)
 //                          and adds it into the genome's row.
-//   k >= 10  k_partition:  one 32768-window tile per workgroup; k-mers are bucketed by
-//                          their top 2k-15 bits with an LDS counting sort and each tile
-//                          writes its bucket-ordered 15-bit suffixes + bucket offsets.
+//   k >= 10  k_partition:  one 16384-window tile per workgroup (three per CU); k-mers are
+//                          bucketed by their top 2k-16 bits with an LDS counting sort and
+//                          each tile writes its bucket-ordered 16-bit suffixes + offsets.
 //            k_bucket_count: one workgroup per (genome, bucket) gathers that bucket's
-//                          segments from every tile of the genome into a 32768-bin LDS
+//                          segments from every tile of the genome into a 65536-bin u16 LDS
 //                          histogram and stores the row slice once.
 //
 // Bases: A/C/G/T in either case (generate.py:41 upper()s the record; :55 keeps windows of
@@ -176,13 +176,15 @@ __global__ __launch_bounds__(kDirectThreads) void k_direct(const uint8_t* __rest
 // Buckets are the top 2k - 16 bits of the code (256 at k = 12); a bucket's 65536 bins are
 // counted by one k_bucket_count workgroup in a u16 LDS table (128 KiB).  Tiles of kPTile
 // window starts (512 threads x 32) are partitioned by bucket with an LDS counting sort whose
-// rank counters are replicated per LDS bank:
+// counters are replicated per LDS bank:
 //
-//   rep word b * 32 + (lane & 31) counts the k-mers of bucket b seen by replica lane & 31,
-//   so the 32 lanes of a lane group always hit 32 different banks.  One returning add per
-//   k-mer gives its rank inside (bucket, replica); a scan turns the counters into segment
-//   starts (bucket start + replica prefix) in place; the scatter reads its start (the same
-//   conflict-free word) and stores the 16-bit suffix: the one random LDS access of a k-mer.
+//   the u16 half b & 1 of rep word (b >> 1) * 32 + (lane & 31) counts the k-mers of bucket b
+//   seen by replica lane & 31, so the 32 lanes of a lane group always hit 32 different banks.
+//   A histogram pass adds 1 per k-mer (no returned value), a scan turns the counters into
+//   segment starts (bucket start + replica prefix) in place, and the scatter's returning add
+//   on the same conflict-free word hands each k-mer its slot, where it stores the 16-bit
+//   suffix: the one random LDS access of a k-mer.  No per-k-mer rank is kept in registers and
+//   the counters take half the LDS, so three workgroups fit a CU (52.5 KiB, 68 VGPRs).
 //   Windows with a non-base byte count in an extra row that the scan places after every
 //   bucket, so they need no branch and are never copied out.
 //
@@ -229,8 +231,9 @@ __device__ __forceinline__ uint32_t scan64(uint32_t s) {
     return s;
 }
 
-// The 32 window codes of this thread from its 48 loaded bytes (invalid windows: ~0u).
-template <int K>
+// The 32 window codes of this thread from its 48 loaded bytes (invalid windows: INV, which
+// k_partition makes bucket NBK, suffix 0).
+template <int K, uint32_t INV>
 __device__ __forceinline__ void visit_raw(uint4 a, uint4 b, uint4 n, uint32_t tm_a, uint32_t tm_b,
                                           uint32_t tm_n, uint32_t (&km)[kTileBpt]) {
     uint32_t cA, iA, cB, iB, cN, iN;
@@ -247,42 +250,51 @@ __device__ __forceinline__ void visit_raw(uint4 a, uint4 b, uint4 n, uint32_t tm
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t code = (uint32_t)(wAB >> (64 - 2 * (j + K))) & KM;
-        km[j] = (((vAB >> (32 - (j + K))) & VM) == 0u) ? code : 0xFFFFFFFFu;
+        km[j] = (((vAB >> (32 - (j + K))) & VM) == 0u) ? code : INV;
     }
     const uint64_t wBN = ((uint64_t)cB << 32) | cN;
     const uint32_t vBN = (iB << 16) | iN;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint32_t code = (uint32_t)(wBN >> (64 - 2 * (j + K))) & KM;
-        km[16 + j] = (((vBN >> (32 - (j + K))) & VM) == 0u) ? code : 0xFFFFFFFFu;
+        km[16 + j] = (((vBN >> (32 - (j + K))) & VM) == 0u) ? code : INV;
     }
 }
 
 template <int K>
-__global__ __launch_bounds__(kPThreads, 2) void k_partition(const uint8_t* __restrict__ seq,
+__global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __restrict__ seq,
                                                             GenomeMap m, uint16_t* __restrict__ suf,
                                                             uint16_t* __restrict__ toff, uint32_t ldt) {
     constexpr int NBK = num_buckets<K>();
-    constexpr int NROW = NBK + 8;                  // + invalid-window row, padded to 8 rows
+    constexpr int NROW = NBK + 16;                 // + invalid-window row, padded to 16 rows
     constexpr int NW = kPThreads / 64;
     constexpr int CAP = tile_cap<K>();
     static_assert(NBK + 1 <= kPThreads && CAP / 8 < 4096, "scan layout / 12-bit chunk offsets");
-    __shared__ __attribute__((aligned(16))) uint32_t rep[NROW * kRep];
+    static_assert(NROW + NW <= CAP / 2 && CAP <= 65535 - kPTile, "starts alias the stage; u16 counters");
+    constexpr uint32_t kInv = (uint32_t)NBK << kCBits;   // invalid windows: bucket NBK, suffix 0
+    static_assert(kCBits == 16, "counter word = code >> 17, half = bit 16 of the code");
+    // counters as u16 halves: bucket b, replica r in half b & 1 of word (b >> 1) * 32 + r
+    // (52 KiB of LDS per workgroup: three workgroups per CU)
+    __shared__ __attribute__((aligned(16))) uint32_t rep[NROW / 2 * kRep];
     __shared__ __attribute__((aligned(16))) uint16_t stage[CAP];
-    __shared__ uint32_t start[NROW];
-    __shared__ uint32_t wsum[NW];
+    uint32_t* start = reinterpret_cast<uint32_t*>(stage);   // bucket starts until the scatter
+    uint32_t* wsum = start + NROW;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t r = (uint32_t)lane & 31u;
+    const uint32_t r4 = ((uint32_t)lane & 31u) << 2;   // byte offset of this lane's replica
     const uint64_t lt = xcd_work_id();
     const uint64_t gt = m.tile_lo + lt;
     const int g = find_genome(m, gt);
     const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)kPTile;
     const uint64_t ge = m.goff[g + 1];
     const uint64_t base = tstart + (uint64_t)tid * kTileBpt;
+    // counter of code c (bucket c >> 16 <= NBK): byte (c >> 17) * 128 + r4 of rep, half c bit 16
+    char* repb = reinterpret_cast<char*>(rep);
+    auto ctr = [&](uint32_t c) { return reinterpret_cast<uint32_t*>(repb + (((c >> 17) << 7) | r4)); };
+    auto half = [](uint32_t c) { return (c >> 12) & 16u; };
 
     uint4* rep4 = reinterpret_cast<uint4*>(rep);
-    for (int i = tid; i < NROW * kRep / 4; i += kPThreads) rep4[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < NROW / 2 * kRep / 4; i += kPThreads) rep4[i] = make_uint4(0u, 0u, 0u, 0u);
 
     uint32_t km[kTileBpt];
     {
@@ -298,30 +310,29 @@ __global__ __launch_bounds__(kPThreads, 2) void k_partition(const uint8_t* __res
         }
         // tiles whose bytes all lie inside the genome (all but its last) need no tail masks
         if (tstart + (uint64_t)kPTile + 16 <= ge)   // uniform per workgroup
-            visit_raw<K>(ra, rb, rn, 0u, 0u, 0u, km);
+            visit_raw<K, kInv>(ra, rb, rn, 0u, 0u, 0u, km);
         else
-            visit_raw<K>(ra, rb, rn, tail_mask(base, ge), tail_mask(base + 16, ge), tail_mask(base + 32, ge), km);
+            visit_raw<K, kInv>(ra, rb, rn, tail_mask(base, ge), tail_mask(base + 16, ge), tail_mask(base + 32, ge), km);
     }
     lds_barrier();
 
-    // 1. rank of every k-mer inside (bucket, replica); ranks < 512, two per register
-    uint32_t rk[kTileBpt / 2];
+    // 1. histogram of (bucket, replica): adds whose results nobody waits for
 #pragma unroll
-    for (int j = 0; j < kTileBpt; j += 2) {
-        const uint32_t b0 = min(km[j] >> kCBits, (uint32_t)NBK);
-        const uint32_t b1 = min(km[j + 1] >> kCBits, (uint32_t)NBK);
-        const uint32_t x0 = atomicAdd(&rep[(b0 << 5) | r], 1u);
-        const uint32_t x1 = atomicAdd(&rep[(b1 << 5) | r], 1u);
-        rk[j >> 1] = x0 | (x1 << 16);
+    for (int j = 0; j < kTileBpt; ++j) {
+        __hip_atomic_fetch_add(ctr(km[j]), 1u << half(km[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     lds_barrier();
 
-    // 2a. row totals: one 16-byte read per lane, 8 lanes per row, 8 rows per wave instruction
-    for (int i = wave; i < NROW / 8; i += NW) {
-        const int row = i * 8 + (lane >> 3);
-        const uint4 v = rep4[row * (kRep / 4) + (lane & 7)];
+    // 2a. row totals: one 16-byte read per lane, 8 lanes per word row (two buckets, summed as
+    //     packed halves: a bucket holds at most kPTile < 65536), 8 word rows per wave instruction
+    for (int i = wave; i < NROW / 16; i += NW) {
+        const int wr = i * 8 + (lane >> 3);
+        const uint4 v = rep4[wr * (kRep / 4) + (lane & 7)];
         const uint32_t sm = scan8(v.x + v.y + v.z + v.w, lane);
-        if ((lane & 7) == 7) start[row] = sm;
+        if ((lane & 7) == 7) {
+            start[2 * wr] = sm & 0xFFFFu;
+            start[2 * wr + 1] = sm >> 16;
+        }
     }
     lds_barrier();
 
@@ -345,25 +356,34 @@ __global__ __launch_bounds__(kPThreads, 2) void k_partition(const uint8_t* __res
     const uint32_t total = start[NBK];   // entries to write: the padded buckets
 
     // 2c. segment start of every (bucket, replica), in place
-    for (int i = wave; i < NROW / 8; i += NW) {
-        const int row = i * 8 + (lane >> 3);
-        uint4* pr = &rep4[row * (kRep / 4) + (lane & 7)];
+    //     (packed halves: every start stays below CAP + kPTile < 65536)
+    for (int i = wave; i < NROW / 16; i += NW) {
+        const int wr = i * 8 + (lane >> 3);
+        uint4* pr = &rep4[wr * (kRep / 4) + (lane & 7)];
         const uint4 v = *pr;
         const uint32_t sm = v.x + v.y + v.z + v.w;
-        const uint32_t st = start[row] + scan8(sm, lane) - sm;
+        const uint32_t ex = scan8(sm, lane) - sm;
+        const uint32_t st = (start[2 * wr] + (ex & 0xFFFFu)) | ((start[2 * wr + 1] + (ex >> 16)) << 16);
         *pr = make_uint4(st, st + v.x, st + v.x + v.y, st + v.x + v.y + v.z);
     }
     lds_barrier();
 
-    // 3. scatter the suffixes (groups of 8: eight start reads in flight, then eight stores)
+    // 3. scatter the suffixes: a returning add on the (bucket, replica) start gives each k-mer
+    //    its slot (groups of 8: eight adds in flight, then eight stores); the order inside a
+    //    segment is arbitrary, the count kernel only adds.  The codes are laundered so that the
+    //    compiler derives the counter addresses again instead of keeping step 1's 64 live.
+#pragma unroll
+    for (int j = 0; j < kTileBpt; ++j) __asm__ volatile("" : "+v"(km[j]));
 #pragma unroll
     for (int j0 = 0; j0 < kTileBpt; j0 += 8) {
         uint32_t pos[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pos[j] = rep[(min(km[j0 + j] >> kCBits, (uint32_t)NBK) << 5) | r];
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t h = half(km[j0 + j]);
+            pos[j] = __builtin_amdgcn_ubfe(atomicAdd(ctr(km[j0 + j]), 1u << h), h, 16);
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            stage[pos[j] + ((rk[(j0 + j) >> 1] >> (16 * (j & 1))) & 0xFFFFu)] = (uint16_t)km[j0 + j];
+        for (int j = 0; j < 8; ++j) stage[pos[j]] = (uint16_t)km[j0 + j];
     }
     lds_barrier();
 
