@@ -82,8 +82,12 @@ def test_dense_all_k_vs_oracle(ctx, dev, oracle_lib, k):
 
 @pytest.mark.parametrize("k", [4, 8, 10, 12])
 def test_dense_low_complexity(ctx, dev, oracle_lib, k):
+    # every window of a tile in one bucket: A (bucket 0, even: low counter half), T (the last
+    # bucket, odd: high half, next to the invalid-window row), C / G (odd / even), AT / TA
     genomes = [np.full(1_000_000, ord("A"), np.uint8),
-               np.frombuffer(b"AT" * 300_000 + b"a" * 5000, np.uint8).copy()]
+               np.frombuffer(b"AT" * 300_000 + b"a" * 5000, np.uint8).copy(),
+               np.full(700_001, ord("T"), np.uint8),
+               np.frombuffer(b"c" * 300_000 + b"N" * 17 + b"G" * 300_000, np.uint8).copy()]
     rows, _, _ = _dense_rows(ctx, dev, genomes, k)
     for g, seq in enumerate(genomes):
         assert np.array_equal(rows[g], oracle_lib.count_dense(seq, k)), (k, g)
