@@ -37,6 +37,7 @@ from kmerml import _native  # noqa: E402
 
 METRIC = "bases/s counted into k-mer feature matrix (1/2/4/8 GPU) + % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0          # one xGMI link per direction; 7 links per MI355X
 SEED_BASE = 0x6B6D65724D4C0000
 
 
@@ -96,7 +97,10 @@ def parse():
     return a
 
 
-def cpu_baseline(sample, k):
+CONFIG5_CPU_SAMPLE = 3_000_000
+
+
+def cpu_baseline(sample, k, strand=None):
     """Time the reference's per-window loop (oracle restatement, forward strand: the
     reference has no canonical mode) on one core."""
     sys.path.insert(0, HERE)
@@ -107,10 +111,12 @@ def cpu_baseline(sample, k):
     table = okmers.count_sequence(seq, k)
     dt = time.perf_counter() - t0
     assert sum(table.values()) == sample - k + 1
+    note = (" (forward strand: the reference counts no canonical k-mers, so this is its loop on "
+            "the config's genomes, not a canonical count)") if strand == "forward" else ""
     return {"value": sample / dt, "unit": "bases/s", "cores": 1, "kind": "port",
             "sample": f"first {sample} bases of synthetic genome 0, k={k}: the count loop of "
                       f"generate.py:49-58 restated in pure Python (oracle/kmers.py), "
-                      f"{dt:.2f} s on one core",
+                      f"{dt:.2f} s on one core{note}",
             "seconds": dt, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
 
 
@@ -243,6 +249,26 @@ def check_assembly(full, own, B, G, world, rank, k, check_dir):
     return bool(ok)
 
 
+def allgather_report(mode, world, B, bins, gather_ms, gloo, scope):
+    """the matrix assembly's all-gather on its own -- time per step (mean over the
+    timed steps, max over ranks; RCCL: HIP events on the comm stream, which include waiting for
+    the slowest peer), bytes each rank receives, and that rate against the xGMI links: all 7 of
+    an MI355X (7 x 153 GB/s, SURVEY's figure) and the N - 1 links that reach the other ranks."""
+    if mode == "none" or gather_ms is None:
+        return None
+    per_rank = {"u32": B * bins * 4}.get(mode, scope.get("P"))
+    recv_bytes = (world - 1) * per_rank
+    gbs = recv_bytes / (gather_ms * 1e-3) / 1e9 if gather_ms > 0 else None
+    return {"allgather_ms": round(gather_ms, 4), "wire": mode, "slot_bytes": per_rank,
+            "received_bytes_per_rank": recv_bytes,
+            "received_GBs_per_gpu": round(gbs, 1) if gbs is not None else None,
+            "frac_of_7_links": round(gbs / (7 * XGMI_LINK_GBS), 4) if gbs is not None else None,
+            "frac_of_peer_links": (round(gbs / ((world - 1) * XGMI_LINK_GBS), 4)
+                                   if gbs is not None and world > 1 else None),
+            "timing": "gloo host-staged, wall clock (validation only)" if gloo else
+                      "HIP events around the RCCL all-gather on its own stream (includes peer skew)"}
+
+
 def workload_name(G, L, k, world, single_device, backend):
     """BASELINE.json config label -- only for the configs' own sizes on real devices; anything
     else (smaller genomes, ranks sharing one GPU) is labelled a rehearsal."""
@@ -267,11 +293,13 @@ def main():
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     # CPU baselines first (rank 0, N = 1 only), before the GPU is touched (the process pool
     # forks) and so that they never overlap GPU timing.
-    cpu = cpu_mt = cpu_p = None
+    cpu = cpu_mt = cpu_p = cpu5 = None
     if a.workload == "dense" and rank == 0 and world == 1 and a.cpu_sample > 0:
         cpu = cpu_baseline(a.cpu_sample, a.k)
         cpu_p = cpu_procs_baseline(a.k)
         cpu_mt = cpu_threads_baseline(a.k)
+        if not a.no_config5:
+            cpu5 = cpu_baseline(CONFIG5_CPU_SAMPLE, 21, strand="forward")
     dev_index = 0 if a.single_device else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -310,6 +338,34 @@ def main():
     gloo = a.backend == "gloo"
     full = torch.empty((world * B, bins), dtype=torch.int32, device=dev) if mode == "u32" else None
     t_count = []
+    t_gather = []          # per timed step: (start, end) events on the comm stream, or gloo wall ms
+    comm = torch.cuda.Stream(dev) if use_dist and not gloo else None
+
+    def gather(recv_t, send_t, record):
+        """All-gather send_t of every rank into recv_t (SURVEY 8(e)'s one exchange step).  RCCL:
+        issued from the `comm` stream after the count that wrote send_t, with a HIP event pair
+        around it on that stream (the time includes waiting for the slowest peer); returns the
+        event the consumer waits for, so step i+1's count overlaps it.  gloo: host-staged and
+        synchronous (validation only), timed by the wall clock."""
+        if gloo:
+            t0 = time.perf_counter()
+            host = torch.empty(tuple(recv_t.shape), dtype=recv_t.dtype)
+            dist.all_gather_into_tensor(host, send_t.cpu())
+            recv_t.copy_(host)
+            if record:
+                t_gather.append((time.perf_counter() - t0) * 1e3)
+            return None
+        comm.wait_stream(stream)
+        with torch.cuda.stream(comm):
+            e0 = torch.cuda.Event(enable_timing=True) if record else None
+            if record:
+                e0.record(comm)
+            dist.all_gather_into_tensor(recv_t, send_t)
+            done = torch.cuda.Event(enable_timing=record)
+            done.record(comm)
+        if record:
+            t_gather.append((e0, done))
+        return done
 
     def count_into(buf, record, u4=None):
         e0 = torch.cuda.Event(enable_timing=True) if record else None
@@ -362,12 +418,8 @@ def main():
                     ev = torch.cuda.Event()
                     ev.record(side)
                 inflight[b] = ev
-            elif not gloo:
-                inflight[b] = dist.all_gather_into_tensor(recv[b], sb, async_op=True)
-            else:  # gloo validation path: host staging, synchronous
-                host = torch.empty(world * P, dtype=torch.uint8)
-                dist.all_gather_into_tensor(host, sb.cpu())
-                recv[b].copy_(host)
+            else:
+                inflight[b] = gather(recv[b], sb, record)
 
         def drain():
             for b in range(2):
@@ -382,12 +434,9 @@ def main():
         def step(i, record=False):
             count_into(local, record)
             if mode == "u32":
-                if not gloo:
-                    dist.all_gather_into_tensor(full, local)
-                else:  # gloo validation path: host staging
-                    host = torch.empty((world * B, bins), dtype=torch.int32)
-                    dist.all_gather_into_tensor(host, local.cpu())
-                    full.copy_(host)
+                done = gather(full, local, record)
+                if done is not None:     # the next count rewrites `local`
+                    stream.wait_event(done)
 
         def drain():
             pass
@@ -421,7 +470,7 @@ def main():
                 side.wait_stream(stream)
             with torch.cuda.stream(side):
                 if work is not None:
-                    work.wait()
+                    side.wait_event(work)
                 r = recv[j % 2]
                 base = r.data_ptr()
                 dst = fulls[j % 2]
@@ -453,13 +502,7 @@ def main():
             else:
                 ctx.rows_encode_u8(locals_[b].data_ptr(), B, bins, sb.data_ptr(), sb[payload + 16:].data_ptr(),
                                    cap, sb[payload:].data_ptr(), s)
-            if not gloo:
-                work = dist.all_gather_into_tensor(recv[b], sb, async_op=True)
-            else:  # gloo validation path: host staging, synchronous
-                host = torch.empty(world * P, dtype=torch.uint8)
-                dist.all_gather_into_tensor(host, sb.cpu())
-                recv[b].copy_(host)
-                work = None
+            work = gather(recv[b], sb, record)
             if pending:
                 finish(*pending.pop())
             pending.append((i, work))
@@ -490,11 +533,15 @@ def main():
     kernels = ctx.timing_report()
     ctx.timing(False)
     count_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in t_count]))
+    gather_ms = None
+    if t_gather:
+        gather_ms = float(np.mean([x if isinstance(x, float) else x[0].elapsed_time(x[1]) for x in t_gather]))
     if world > 1:
-        t = torch.tensor([elapsed, count_ms], dtype=torch.float64,
+        t = torch.tensor([elapsed, count_ms, gather_ms or 0.0], dtype=torch.float64,
                          device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, count_ms = float(t[0]), float(t[1])
+        gather_ms = float(t[2]) if gather_ms is not None else None
 
     # sanity: every row sums to the number of valid windows (all-ACGT genomes)
     last = locals_[(a.steps - 1) % len(locals_)]
@@ -588,6 +635,7 @@ def main():
                               # bases read once vs the HBM-read peak, per GPU
                               "reads_only_frac": round(g_local * L / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "count_ms_per_step_rank_max": round(count_ms, 4),
+            "allgather": allgather_report(mode, world, B, bins, gather_ms, gloo, locals()),
             "count_only_bases_per_s_per_gpu": count_rate,
             "kernels": {n: {"launches": l, "total_ms": round(t, 4), "mean_ms": round(t / l, 4)}
                         for n, (l, t) in kernels.items()},
@@ -601,7 +649,8 @@ def main():
             # BASELINE config 5 measured in the same run (its own line: bench.py --workload sparse)
             torch.cuda.empty_cache()
             sa = argparse.Namespace(k=21, genomes=16, genome_len=250_000_000, steps=3, warmup=1,
-                                    cpu_sample=0, forward=False, backend=a.backend, pmc_summary=a.pmc_summary)
+                                    cpu_sample=0, forward=False, backend=a.backend, pmc_summary=a.pmc_summary,
+                                    cpu=cpu5)
             try:
                 out["config5"] = run_sparse(sa, 1, 0, dev, dev_index, emit=False)
             except Exception as e:   # never lose the config-3 line over the extra measurement
@@ -629,9 +678,9 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
     k, G, L = a.k, a.genomes, a.genome_len
     lo, hi = (G * rank) // world, (G * (rank + 1)) // world
     g_local = hi - lo
-    cpu = None
-    if rank == 0 and world == 1 and a.cpu_sample > 0:
-        cpu = cpu_baseline(min(a.cpu_sample, 4_000_000), k)
+    cpu = getattr(a, "cpu", None)
+    if cpu is None and rank == 0 and world == 1 and a.cpu_sample > 0:
+        cpu = cpu_baseline(min(a.cpu_sample, CONFIG5_CPU_SAMPLE), k, strand="forward" if not a.forward else None)
     ctx = _native.context(dev_index)
     stream = torch.cuda.current_stream(dev)
     s = stream.cuda_stream

@@ -886,7 +886,8 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
         // (the fused u4 encoding needs each bucket in one workgroup: S = 1)
         int S = enc ? 1 : (int)std::max<uint64_t>(1, std::min<uint64_t>(want, std::max<uint64_t>(maxt, 1)));
 #ifdef KMH_EXPERIMENTS
-        if (env_long("KMH_COUNT_S", 0) > 0) S = (int)env_long("KMH_COUNT_S", 1);   // A/B only
+        // A/B only; the fused u4 encode needs one workgroup per bucket, so never with enc
+        if (!enc && env_long("KMH_COUNT_S", 0) > 0) S = (int)env_long("KMH_COUNT_S", 1);
 #endif
         if (S > 1) KMH_HIP(ctx, hipMemsetAsync(d_out + (size_t)g * row, 0, (size_t)nG * row * sizeof(uint32_t), s));
         if (tiles) {

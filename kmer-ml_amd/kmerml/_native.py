@@ -9,8 +9,10 @@ import threading
 
 import numpy as np
 
-# KMH_LIB_PATH: A/B profiling of another build of the same ABI (profiles/); default: the in-tree build
-LIB_PATH = os.environ.get("KMH_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkmerhip.so")
+DEFAULT_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkmerhip.so")
+# KMH_LIB_PATH: A/B profiling of another build of the same ABI (profiles/); every symbol of
+# SIGNATURES must resolve, and a warning names the build id of the library loaded instead
+LIB_PATH = os.environ.get("KMH_LIB_PATH") or DEFAULT_LIB_PATH
 
 KMH_OK = 0
 KMH_ERR_INVALID = -1
@@ -95,6 +97,10 @@ def lib():
                     fn = getattr(L, name)
                     fn.restype = res
                     fn.argtypes = args
+                if LIB_PATH != DEFAULT_LIB_PATH:
+                    import warnings
+                    warnings.warn(f"KMH_LIB_PATH: using {LIB_PATH} (build {L.kmh_build_id().decode()}, "
+                                  f"{L.kmh_version().decode()}) instead of the in-tree library")
                 _lib = L
     return _lib
 

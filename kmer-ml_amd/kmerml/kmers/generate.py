@@ -18,8 +18,16 @@ the reference itself, tests/golden/):
   distinct k-mer, digits A=0 T=1 C=2 G=3, lines in first-occurrence order (:68-91); an
   empty result still creates the file.
 
-Differences: 1 <= k <= 1024 is supported (k > 1024 raises NotImplementedError,
-k <= 0 raises ValueError; k >= 33 is counted by sorting ceil(k / 32) code words per window
+* k <= 0 and bool k behave as in the reference's loop (tests/golden: k = 0 counts the empty
+  k-mer len + 1 times per record and writes ``"\t{count}"``; a negative k counts the slices
+  ``seq[i:i + k]``; True / False are k = 1 / 0 under the key True / False, file
+  ``kTrue.txt``); these degenerate k are counted on the host (they are no hot path).  A
+  non-integer k raises the reference's TypeError from ``range()`` at the first kept record,
+  after the "Skipping" lines of the records before it, and leaves no file; with no kept
+  record it writes an empty ``k{k}.txt`` as the reference does.
+
+Differences (DESIGN.md): k <= 1024 is supported (k > 1024 raises NotImplementedError;
+k >= 33 is counted by sorting ceil(k / 32) code words per window
 and its lines are written from the sequence); counting never falls back to the CPU --
 without the HIP library or a device it raises.  Size limits per organism (its kept records
 joined): below 2^32 - 1 bytes for every k, and fewer than 2^31 windows for k >= 13 (a
@@ -28,6 +36,7 @@ k >= 13, which extract_from_genome_list reports as "Error processing <id>" like 
 failure).  The reference's dict has no such limit but needs tens of bytes per distinct
 k-mer of host memory.
 """
+import operator
 import os
 from pathlib import Path
 
@@ -62,17 +71,22 @@ class KmerExtractor:
         results = {}
         packed = np.zeros(0, np.uint8)
         if len(fasta):
-            longest = max(k_values)
+            longest = max(k_values)                   # generate.py:44 (same error for odd k)
+            if not all(_is_index(k) for k in k_values):
+                _raise_like_reference(fasta, k_values, longest)
+                longest = float("inf")                # no record is kept: nothing to count
+            packed, kept = fasta.pack(_min_len(longest))
+            ctx = None
             for k in k_order:
-                if not isinstance(k, (int, np.integer)) or isinstance(k, bool):
-                    raise TypeError(f"k values must be integers, got {k!r}")
-                if k < 1:
-                    raise ValueError(f"k must be >= 1 (got {k})")
-            packed, kept = fasta.pack(longest)
-            ctx = _native.context(_device())
-            for k in k_order:
-                if kept.any():
-                    results[k] = ctx.count(packed, k)
+                if not kept.any():
+                    break
+                kv = operator.index(k)                # True / False count as k = 1 / 0
+                if kv >= 1:
+                    ctx = ctx or _native.context(_device())
+                    results[k] = ctx.count(packed, kv)
+                else:
+                    bodies = bytes(packed).split(b"\n")[:int(kept.sum())]
+                    results[k] = _count_degenerate(bodies, kv)
             for rid, keep in zip(fasta.ids, kept):
                 if keep:
                     print(f"Processed chromosome/contig: {rid}")
@@ -80,14 +94,21 @@ class KmerExtractor:
                     print(f"Skipping {rid}: too short for k-mer extraction")
         fasta.close()
         for k in k_order:
-            codes, counts, first = results.get(k, (np.empty(0, np.uint64), np.empty(0, np.uint32),
-                                                   np.empty(0, np.uint64)))
+            path = self._kmer_path(organism_id, k)
+            res = results.get(k)
+            if isinstance(res, dict):                 # k <= 0
+                self._write_bytes(path, _degenerate_text(res, multiplicity[k]))
+                continue
+            if res is None or not _is_index(k) or operator.index(k) < 1:
+                self._write_bytes(path, b"")          # no kept record: an empty file (:87-91)
+                continue
+            codes, counts, first = res
+            kv = operator.index(k)
             counts = np.multiply(counts, np.uint64(multiplicity[k]), dtype=np.uint64)
-            if k > 32:   # a code holds 32 bases: the line digits come from the sequence
-                self._write_bytes(self._kmer_path(organism_id, k),
-                                  _native.format_lines_seq(k, packed, first, counts))
+            if kv > 32:   # a code holds 32 bases: the line digits come from the sequence
+                self._write_bytes(path, _native.format_lines_seq(kv, packed, first, counts))
             else:
-                self._write_kmer_file(organism_id, k, codes, counts)
+                self._write_bytes(path, _native.format_lines_array(kv, codes, counts))
         return organism_id
 
     def _kmer_path(self, organism_id, k):
@@ -97,9 +118,6 @@ class KmerExtractor:
     def _write_bytes(self, path, data):
         # gzip.open's default level 9 (generate.py:82-85), deflated on several host threads
         _native.write_file(path, data, gzip_level=9 if self.compress else -1)
-
-    def _write_kmer_file(self, organism_id, k, codes, counts):
-        self._write_bytes(self._kmer_path(organism_id, k), _native.format_lines_array(k, codes, counts))
 
     # generate.py:68-91 -- kept for callers that hand in a {kmer: count} dict.
     def _save_kmers_to_file(self, kmers, organism_id, k):
@@ -125,3 +143,70 @@ class KmerExtractor:
                 print(f"Error processing {org_id}: {str(e)}")
         print(f"Completed processing {len(processed_ids)} out of {total} genomes")
         return processed_ids
+
+
+def _is_index(k):
+    """True for the k values range() accepts (int, bool, numpy integers)."""
+    try:
+        operator.index(k)
+        return True
+    except TypeError:
+        return False
+
+
+def _min_len(longest):
+    """The record filter of generate.py:44 as a minimum character length."""
+    if longest == float("inf"):
+        return 1 << 62
+    return max(0, -(-longest // 1)) if not _is_index(longest) else max(0, operator.index(longest))
+
+
+def _raise_like_reference(fasta, k_values, longest):
+    """A k that is no integer: the reference prints its "Skipping" lines up to the first record
+    that passes the length rule and raises from ``range(len(sequence) - k + 1)`` there
+    (generate.py:44-51).  Returns only if no record passes the rule."""
+    skipped = []
+    for i, rid in enumerate(fasta.ids):
+        n = _upper_len(fasta, i)
+        if n < longest:                     # may itself raise (e.g. a str k), as :44 does
+            skipped.append(f"Skipping {rid}: too short for k-mer extraction")
+            continue
+        for line in skipped:
+            print(line)
+        for k in k_values:
+            range(n - k + 1)                # the reference's TypeError
+        return
+
+
+def _upper_len(fasta, i):
+    if fasta.char_lens[i] == fasta.seq_lens[i]:
+        return fasta.char_lens[i]
+    return len(fasta.sequence(i).decode("utf-8", errors="surrogateescape").upper())
+
+
+def _count_degenerate(bodies, k):
+    """generate.py:49-58 for k <= 0 over the kept records (upper-cased bytes, one per record).
+    Windows i >= -k are empty slices (the empty k-mer, which passes the ACGT test of :55); the
+    first -k windows are ``seq[i:i + k]``, counted when every character is a base.  Returns the
+    dict in the reference's insertion order."""
+    table = {}
+    m = -k
+    for body in bodies:
+        s = body.upper()
+        n = len(s) - k + 1                  # range(len(sequence) - k + 1)
+        for i in range(min(m, n)):
+            t = s[i:i + k]
+            if not t.translate(None, b"ACGT"):
+                table[t] = table.get(t, 0) + 1
+        if n > m:
+            table[b""] = table.get(b"", 0) + (n - m)
+    return table
+
+
+_DIGIT_TABLE = bytes.maketrans(b"ACGT", b"0231")
+
+
+def _degenerate_text(table, mult):
+    """_save_kmers_to_file's lines (generate.py:86-91) for the dict of _count_degenerate."""
+    return b"".join(t.translate(_DIGIT_TABLE) + b"\t" + str(c * mult).encode() + b"\n"
+                    for t, c in table.items())

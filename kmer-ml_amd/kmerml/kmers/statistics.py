@@ -124,9 +124,8 @@ class KmerFeatureExtractor:
         if len(labels) == 0:
             return pd.DataFrame(cols)
         codes = label_codes(df['kmer'].to_numpy(), k_val)
-        if codes is not None:   # every label is a k-mer: rows of the per-k table (feature_table)
-            t = feature_table(k_val)
-            f = {name: col[codes] for name, col in t.items()}
+        if codes is not None:   # every label is a k-mer: features computed per code
+            f = code_features_of(k_val, codes)
         else:
             f = label_features([str(x) for x in labels])
         if 'gc_content' in required_features:
@@ -233,23 +232,51 @@ def label_codes(values, k):
     return codes if not v.any() else None
 
 
-_TABLES = {}
+_TABLES = {}          # k -> the table of feature_table(k); only the last k is kept
+_TABLE_MAX_K = 12     # a full table is 4^k rows (k = 12: 16.7 M rows, ~30 temporaries of 134 MB)
+
+
+def code_features_of(k, codes):
+    """Feature columns for the integer-label codes of one k{k}.txt file.  A dense file (k <=
+    12 and at least 1/8 of the 4^k codes present) takes rows of the per-k table; any other
+    file (sparse k = 13..19 files: a few distinct k-mers out of 4^k) computes the features of
+    its distinct codes only, so memory follows the file, not 4^k."""
+    if k <= _TABLE_MAX_K and (1 << (2 * k)) <= 8 * len(codes):
+        t = feature_table(k)
+        return {name: col[codes] for name, col in t.items()}
+    uniq, inv = np.unique(codes, return_inverse=True)
+    t = _code_features(k, uniq)
+    return {name: col[inv] for name, col in t.items()}
 
 
 def feature_table(k):
     """The statistics.py:188-238 features of every label of a dense k (the compat label of each
     of the 4^k codes: the k-mer with its leading A's stripped, one kept for A...A), computed
-    once per k on the GPU (torch on cuda; on the CPU without one) and indexed by code.  Same
+    once per k on the GPU (torch on cuda; on the CPU without one) and indexed by code (k <= 12;
+    the last table is cached)."""
+    if k in _TABLES:
+        return _TABLES[k]
+    if not 1 <= k <= _TABLE_MAX_K:
+        raise ValueError(f"feature_table: 1 <= k <= {_TABLE_MAX_K} (got {k}); use code_features_of")
+    table = _code_features(k, None)
+    _TABLES.clear()
+    _TABLES[k] = table
+    return table
+
+
+def _code_features(k, codes):
+    """statistics.py:188-238 for the compat labels of `codes` (None: all 4^k codes).  Same
     IEEE operations as the reference, per value: gc = (g + c) / L * 100; expected =
     c / L * (g / L) * (L - 1); entropy summed in set(kmer) order (_entropy_order per
     first-appearance pattern) with math.log2 of the same quotients."""
-    if k in _TABLES:
-        return _TABLES[k]
     import torch
 
     dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
     i64 = torch.int64
-    c = torch.arange(1 << (2 * k), dtype=i64, device=dev)
+    if codes is None:
+        c = torch.arange(1 << (2 * k), dtype=i64, device=dev)
+    else:
+        c = torch.as_tensor(np.ascontiguousarray(codes, dtype=np.int64)).to(dev)
     # stripped length m: significant base-4 digits (at least 1)
     m = torch.ones_like(c)
     for j in range(1, k):
@@ -311,9 +338,7 @@ def feature_table(k):
         term = p * lg[n, m]                       # one rounding, as prob * math.log2(prob)
         ent = torch.where(has, ent - term, ent)
     out['shannon_entropy'] = ent
-    table = {name: v.cpu().numpy() for name, v in out.items()}
-    _TABLES[k] = table
-    return table
+    return {name: v.cpu().numpy() for name, v in out.items()}
 
 
 def _entropy_order(pattern):

@@ -157,24 +157,44 @@ class KmerFeatureBuilder:
         order[rank] = np.arange(rank.size, dtype=np.int64)
         return order
 
+    @staticmethod
+    def _from_assembled(mat, order, block=8):
+        """from_count_matrix on an AssembledMatrix without widening it whole: rows are widened
+        `block` at a time on the device, once for the presence test and once for the values."""
+        import torch
+
+        G = mat.shape[0]
+        dev = mat.recv.device if mat.recv is not None else mat._dense.device
+        dev_order = torch.from_numpy(order).to(dev)
+        present = torch.zeros(mat.shape[1], dtype=torch.bool, device=dev)
+        for lo in range(0, G, block):
+            present |= (mat.rows(lo, min(G, lo + block)) != 0).any(dim=0)
+        cols_t = dev_order[present[dev_order]]
+        values = np.empty((G, cols_t.numel()), np.int64)
+        for lo in range(0, G, block):
+            hi = min(G, lo + block)
+            values[lo:hi] = (mat.rows(lo, hi)[:, cols_t].to(torch.int64) & 0xFFFFFFFF).cpu().numpy()
+        return values, cols_t.cpu().numpy()
+
     def from_count_matrix(self, counts, k: int, organisms) -> pd.DataFrame:
         """Count matrix DataFrame for organisms with one k-mer file each, from the dense
         [G, 4^k] count rows (numpy or torch, u32 stored as int32 is fine; or a
         kmerml.kmers.matrix.AssembledMatrix).  Equal to build_from_statistics_files(
         metric="count") on the files the extractor writes (statistics.py:95-147 ->
         features.py:85-117): columns = labels present in any organism, in label order."""
-        if hasattr(counts, "dense") and hasattr(counts, "rows"):     # AssembledMatrix
-            counts = counts.dense()
         order = self.compat_label_order(k)
-        if hasattr(counts, "is_cuda") and counts.is_cuda:
-            # device counts: presence test and the column permutation on the GPU, then one copy
+        if hasattr(counts, "dense") and hasattr(counts, "rows"):     # AssembledMatrix
+            values, cols = self._from_assembled(counts, order)
+        elif hasattr(counts, "is_cuda") and counts.is_cuda:
+            # device counts: presence test and the column permutation on the GPU, then one copy;
+            # an int32 cell holding a u32 is non-zero iff the count is, so only the gathered
+            # columns are widened
             import torch
 
             dev_order = torch.from_numpy(order).to(counts.device)
-            wide = counts.to(torch.int64) & 0xFFFFFFFF                  # u32 stored as int32
-            keep = (wide != 0).any(dim=0)[dev_order] if wide.shape[0] else torch.zeros(0, dtype=torch.bool)
+            keep = (counts != 0).any(dim=0)[dev_order] if counts.shape[0] else torch.zeros(0, dtype=torch.bool)
             cols_t = dev_order[keep]
-            values = wide[:, cols_t].cpu().numpy()
+            values = (counts[:, cols_t].to(torch.int64) & 0xFFFFFFFF).cpu().numpy()
             cols = cols_t.cpu().numpy()
         else:
             rows = counts.cpu().numpy() if hasattr(counts, "cpu") else np.asarray(counts)

@@ -63,14 +63,41 @@ EDGE_CASES = [
     ("e8_unicode.fa", [4]),
     ("e8_unicode.fa", [6]),
     ("e8_unicode.fa", [2, 3]),
+    # k <= 0, bool and non-integer k (scripts/extract_kmers.py:34 accepts any int): the window
+    # loop of generate.py:51-58 still runs -- k = 0 counts the empty k-mer len + 1 times per
+    # record, a negative k counts the slices seq[i:i + k] -- and _save_kmers_to_file writes
+    # "\t{count}" for the empty k-mer (:90-91); True / False are k = 1 / 0 under the dict key
+    # True / False (file kTrue.txt); a float k raises TypeError from range() at the first kept
+    # record (after the "Skipping" lines before it) and writes nothing, but an empty file
+    # writes an empty k2.5.txt
+    ("e1_mixed.fa", [0]),
+    ("e1_mixed.fa", [0, 3]),
+    ("e1_mixed.fa", [-1]),
+    ("e1_mixed.fa", [True]),
+    ("e1_mixed.fa", [1, True]),
+    ("e4_short.fa", [True, 2, False]),
+    ("e4_short.fa", [-2, 2]),
+    ("e4_short.fa", [-7]),
+    ("e6_lowcomplex.fa", [-3, 0, -3]),
+    ("e7_headers.fa", [0, 5]),
+    ("e8_unicode.fa", [-2]),
+    ("e3_empty.fa", [0, -1]),
+    ("e4_short.fa", [6, 2.5]),
+    ("e3_empty.fa", [2.5]),
 ]
 
 
-def run_reference(fasta, k_values, organism_id, outdir, compress=False):
+def run_reference(fasta, k_values, organism_id, outdir, compress=False, errors=None):
     buf = io.StringIO()
+    ret = None
     with contextlib.redirect_stdout(buf):
         ext = KmerExtractor(output_dir=outdir, compress=compress)
-        ret = ext.extract_kmers_from_fasta(fasta, k_values, organism_id=organism_id)
+        try:
+            ret = ext.extract_kmers_from_fasta(fasta, k_values, organism_id=organism_id)
+        except Exception as e:   # recorded for the error cases, re-raised for every other call
+            if errors is None:
+                raise
+            errors.append({"type": type(e).__name__, "message": str(e)})
     files = {}
     odir = os.path.join(outdir, organism_id)
     if os.path.isdir(odir):
@@ -90,10 +117,13 @@ def main():
     try:
         for name, ks in EDGE_CASES:
             odir = os.path.join(tmp, f"edge_{len(out['cases'])}")
+            errors = []
             ret, lines, files = run_reference(os.path.join(HERE, "inputs", name), ks,
-                                              "org", odir)
-            out["cases"].append({"input": name, "k_values": ks, "returned": ret,
-                                 "stdout": lines, "files": files})
+                                              "org", odir, errors=errors)
+            case = {"input": name, "k_values": ks, "returned": ret, "stdout": lines, "files": files}
+            if errors:
+                case["error"] = errors[0]
+            out["cases"].append(case)
             print(name, ks, {k: len(v) for k, v in files.items()})
         with open(os.path.join(HERE, "edge_cases.json"), "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)

@@ -237,3 +237,23 @@ def test_feature_frame_table_path_equals_label_path(monkeypatch):
     assert st.label_codes(np.array([104], np.int64), 3) is None          # digit 4
     assert st.label_codes(np.array([1233], np.int64), 3) is None         # 4 digits at k = 3
     assert st.label_codes(np.array(["12"], dtype=object), 2) is None     # text labels
+
+
+@pytest.mark.parametrize("k", [15, 16, 19])
+def test_feature_frame_sparse_large_k(monkeypatch, k):
+    """Integer labels of a sparse k = 15..19 file: features of the distinct codes
+    only -- never a 4^k table -- equal to the per-label path, bit for bit."""
+    import kmerml.kmers.statistics as st
+    rng = np.random.default_rng(k)
+    codes = rng.integers(0, 4 ** k, 4000, dtype=np.int64)
+    codes[:4] = [0, 1, 4 ** k - 1, codes[5]]           # A...A, leading A's, a repeat
+    dig = np.array([0, 2, 3, 1])
+    lab = np.zeros(codes.size, np.int64)
+    for i in range(k):
+        lab = lab * 10 + dig[(codes >> (2 * (k - 1 - i))) & 3]
+    df = pd.DataFrame({'kmer': lab, 'count': rng.integers(1, 50, codes.size)})
+    monkeypatch.setattr(st, "feature_table", lambda kk: pytest.fail("4^k table built"))
+    fast = st.KmerFeatureExtractor.feature_frame(df, k, st.DEFAULT_FEATURES)
+    monkeypatch.setattr(st, "label_codes", lambda v, kk: None)
+    slow = st.KmerFeatureExtractor.feature_frame(df, k, st.DEFAULT_FEATURES)
+    assert fast.to_csv() == slow.to_csv()

@@ -19,6 +19,7 @@ from kmerml.kmers.generate import KmerExtractor  # noqa: E402
 from kmerml.kmers import matrix as kmatrix  # noqa: E402
 from kmerml.utils.path_utils import find_files  # noqa: E402
 from oracle import synth as osynth  # noqa: E402
+from _dropin import run_extractor  # noqa: E402
 
 
 @pytest.fixture(scope="module")
@@ -315,28 +316,13 @@ def test_count_host_dense_first_order(ctx, oracle_lib, k):
 
 
 # ---------------------------------------------------------------- the drop-in API
-def _run_extractor(tmp_path, fasta, ks, compress=False, org="org"):
-    buf = io.StringIO()
-    with contextlib.redirect_stdout(buf):
-        ext = KmerExtractor(output_dir=str(tmp_path), compress=compress)
-        ret = ext.extract_kmers_from_fasta(fasta, ks, organism_id=org)
-    odir = tmp_path / org
-    files = {}
-    if odir.is_dir():
-        for p in sorted(odir.iterdir()):
-            data = p.read_bytes()
-            if p.suffix == ".gz":
-                data = gzip.decompress(data)
-            files[p.name.replace(".gz", "")] = data.decode()
-    return ret, buf.getvalue().splitlines(), files
-
-
 def test_dropin_edge_cases_byte_identical(tmp_path, golden_dir, edge_cases):
     # every case, k = 33 and k = 40 included (long k-mers: word-sorted on the GPU, lines
-    # written from the sequence)
+    # written from the sequence); k <= 0 / bool / float cases too (tests/test_dropin_degenerate.py
+    # runs the ones that need no device on the CPU)
     for i, case in enumerate(edge_cases):
-        ret, out, files = _run_extractor(tmp_path / f"c{i}", os.path.join(golden_dir, "inputs", case["input"]),
-                                         case["k_values"])
+        ret, out, files = run_extractor(tmp_path / f"c{i}", os.path.join(golden_dir, "inputs", case["input"]),
+                                         case["k_values"], expect_error=case.get("error"))
         assert ret == case["returned"]
         assert out == case["stdout"], case["input"]
         assert files == case["files"], (case["input"], case["k_values"])
@@ -344,7 +330,7 @@ def test_dropin_edge_cases_byte_identical(tmp_path, golden_dir, edge_cases):
 
 def test_dropin_compressed(tmp_path, golden_dir, edge_cases):
     case = edge_cases[3]
-    _, _, files = _run_extractor(tmp_path, os.path.join(golden_dir, "inputs", case["input"]),
+    _, _, files = run_extractor(tmp_path, os.path.join(golden_dir, "inputs", case["input"]),
                                  case["k_values"], compress=True)
     assert files == case["files"]
     assert all(p.name.endswith(".txt.gz") for p in (tmp_path / "org").iterdir())
@@ -356,7 +342,7 @@ def test_dropin_synthetic_hashes(tmp_path, synthetic_cases):
             recs = osynth.yeast_standin_records()
             fa = tmp_path / "yeast_standin.fa"
             osynth.write_fasta(fa, recs)
-            _, out, files = _run_extractor(tmp_path / "ys", fa, [4], org="yeast_standin")
+            _, out, files = run_extractor(tmp_path / "ys", fa, [4], org="yeast_standin")
             assert files["k4.txt"] == case["text"]["k4.txt"]
             assert out == case["stdout"]
             continue
@@ -364,7 +350,7 @@ def test_dropin_synthetic_hashes(tmp_path, synthetic_cases):
         fa = tmp_path / f"{case['name']}.fa"
         osynth.write_fasta(fa, [(g["id"], osynth.synth_bases(g["length"], g["seed"], g["start"]).tobytes())])
         (k,) = case["k_values"]
-        _, out, files = _run_extractor(tmp_path / case["name"], fa, [k])
+        _, out, files = run_extractor(tmp_path / case["name"], fa, [k])
         assert out == case["stdout"]
         assert hashlib.sha256(files[f"k{k}.txt"].encode()).hexdigest() == case["sha256"][f"k{k}.txt"], case["name"]
 
@@ -782,6 +768,7 @@ def test_bench_pipelined_u4_assembly_rccl():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["config"]["assembly"] == "u4"
+    assert d["allgather"]["allgather_ms"] > 0 and d["allgather"]["received_bytes_per_rank"] == 0
 
 
 @pytest.mark.parametrize("wire", ["u4", "u4-dense", "u8"])
@@ -796,6 +783,10 @@ def test_bench_pipelined_assembly_two_ranks(wire):
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["n_gpus"] == 2 and d["config"]["assembly"] == wire
+    ag = d["allgather"]                 # the assembly's all-gather reported on its own
+    assert ag["allgather_ms"] > 0 and ag["received_bytes_per_rank"] == ag["slot_bytes"] > 0
+    for key in ("received_GBs_per_gpu", "frac_of_7_links", "frac_of_peer_links"):
+        assert ag[key] > 0, key
 
 
 def test_rows_decode_u4_range(ctx, dev):
@@ -962,6 +953,44 @@ def test_sparse_dev_config5_full_genome(ctx, dev, oracle_lib):
     wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
     assert got[0].size == wc.size
     assert np.array_equal(got[0], wc) and np.array_equal(got[1], wn)
+
+
+def test_sparse_dev_config5_batched_plan(ctx, dev, oracle_lib):
+    """The bench's per-GPU config-5 plan (bench.py --workload sparse): 16 synthetic 250 Mbp
+    genomes generated on the device and counted at k = 21 canonical in ONE batch (the default
+    16 GiB entry budget: one multi-genome item plan, output offsets of 16 genomes).  Every
+    genome's distinct k-mers must sum to its windows; genomes 0 and 15 (first and last
+    output ranges) are compared k-mer by k-mer with the C oracle.  Reference anchor: the dict
+    of /root/reference/kmerml/kmers/generate.py:36,58."""
+    L, G, k = 250_000_000, 16, 21
+    s = torch.cuda.current_stream().cuda_stream
+    d = torch.empty(G * L, dtype=torch.uint8, device=dev)
+    ctx.synth_dev(d.data_ptr(), L, L, G, osynth.SEED_BASE, s)
+    offs = np.arange(G + 1, dtype=np.uint64) * np.uint64(L)
+    out_off = _native.sparse_out_offsets(offs, k)
+    cap = int(out_off[-1])
+    d_codes = torch.empty(cap, dtype=torch.int64, device=dev)
+    d_counts = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_nk = torch.full((G,), -1, dtype=torch.int64, device=dev)
+    ctx.count_sparse_dev(d.data_ptr(), offs, k, 1, d_codes.data_ptr(), d_counts.data_ptr(), d_nk.data_ptr(), s)
+    torch.cuda.synchronize()
+    del d
+    nk = d_nk.cpu().numpy()
+    for g in range(G):
+        a, n = int(out_off[g]), int(nk[g])
+        assert 0 < n <= int(out_off[g + 1]) - a, g
+        assert int(d_counts[a:a + n].to(torch.int64).sum()) == L - k + 1, g
+    for g in (0, G - 1):
+        a, n = int(out_off[g]), int(nk[g])
+        codes, order = torch.sort(d_codes[a:a + n])      # codes < 2^42: int64 order = u64 order
+        counts = d_counts[a:a + n][order]
+        got_c = codes.cpu().numpy().view(np.uint64)
+        got_n = counts.cpu().numpy().view(np.uint32)
+        del codes, order, counts
+        wc, wn, _ = oracle_lib.count_sparse(oracle_lib.synth(L, osynth.genome_seed(g)), k, canonical=True)
+        assert got_c.size == wc.size, g
+        assert np.array_equal(got_c, wc) and np.array_equal(got_n, wn), g
+        del wc, wn, got_c, got_n
 
 
 @pytest.mark.parametrize("k,canonical", [(21, True), (9, False), (25, True), (32, False)])

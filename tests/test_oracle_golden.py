@@ -23,6 +23,12 @@ def test_python_oracle_reproduces_edge_cases(golden_dir, edge_cases):
     for case in edge_cases:
         recs = [(rid, seq) for rid, _, seq in ofasta.parse_fasta(_inputs(golden_dir, case["input"]))]
         msgs = []
+        if "error" in case:   # a non-integer k: the reference raised from range() (generate.py:51)
+            with pytest.raises(Exception) as e:
+                okmers.count_records(recs, case["k_values"], msgs)
+            assert (type(e.value).__name__, str(e.value)) == (case["error"]["type"], case["error"]["message"])
+            assert msgs == case["stdout"] and case["files"] == {}
+            continue
         if recs:
             res = okmers.count_records(recs, case["k_values"], msgs)
         else:
@@ -30,6 +36,11 @@ def test_python_oracle_reproduces_edge_cases(golden_dir, edge_cases):
         assert msgs == case["stdout"], case["input"]
         files = {f"k{k}.txt": okmers.kmer_text(v) for k, v in res.items()}
         assert files == case["files"], (case["input"], case["k_values"])
+
+
+def _plain_k(ks):
+    """k lists the C restatement covers: integers 1 <= k <= 32 (no bool, no k <= 0)."""
+    return all(type(k) is int and 1 <= k <= 32 for k in ks)
 
 
 def _text_from_sparse(k, codes, counts, first, mult=1):
@@ -50,8 +61,8 @@ def _pack(golden_dir, name, longest):
 def test_c_oracle_reproduces_edge_cases(golden_dir, edge_cases, oracle_lib):
     for case in edge_cases:
         ks = case["k_values"]
-        if max(ks) > 32:
-            continue  # the C restatement stops at k = 32 (so does the product)
+        if not _plain_k(ks):
+            continue  # the C restatement covers 1 <= k <= 32 (k > 32, k <= 0: Python oracle above)
         packed = _pack(golden_dir, case["input"], max(ks))
         for k in dict.fromkeys(ks):
             codes, counts, first = oracle_lib.count_sparse(packed, k)
