@@ -97,7 +97,7 @@ def parse():
     return a
 
 
-CONFIG5_CPU_SAMPLE = 3_000_000
+CONFIG5_CPU_SAMPLE = 12_000_000   # ~10 s of the k = 21 loop on one EPYC 9575F core
 
 
 def cpu_baseline(sample, k, strand=None):

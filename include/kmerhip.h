@@ -239,6 +239,35 @@ int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, u
 int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const uint64_t* first,
                              const uint64_t* counts, uint64_t n, char* out, uint64_t cap);
 
+/* ---- feature CSV text (host) --------------------------------------------------- */
+/* Replaces pandas' DataFrame.to_csv(index=False) of the per-organism feature table
+ * (/root/reference/kmerml/kmers/statistics.py:136-144): the rows of a block of columns as CSV
+ * text, no header, '\n' after every row, exactly as pandas writes them -- int64 / uint64 as
+ * decimal integers, float64 as Python's float repr (shortest round trip; fixed notation for
+ * decimal exponents -4 < e <= 16, else d.ddde+XX).  Column j has kinds[j] and data[j] / aux[j]:
+ *   KMH_CSV_I64   data: const int64_t[nrows]                       aux: unused
+ *   KMH_CSV_F64   data: const double[nrows]                        aux: unused
+ *   KMH_CSV_STR   data: UTF-8 bytes of every field back to back    aux: const uint64_t[nrows + 1]
+ *                 field offsets
+ *   KMH_CSV_LABEL data: const uint64_t[nrows] k-mer codes (A0 C1 G2 T3) aux: const int64_t* k
+ *                 (1..32): the reference's label of an integer-parsed k-mer file line, the k-mer
+ *                 with its leading A's stripped ("A" for A...A; statistics.py:157, 248-273)
+ *   KMH_CSV_U64   data: const uint64_t[nrows]                      aux: unused
+ * Formatted on up to `threads` host threads (0 = all cores, at most 16).  KMH_ERR_UNSUPPORTED
+ * when pandas would write a value differently (NaN or inf, an empty text field, a field with
+ * ',', '"', '\n' or '\r': pandas quotes it): the caller then writes that block with pandas. */
+#define KMH_CSV_I64   0
+#define KMH_CSV_F64   1
+#define KMH_CSV_STR   2
+#define KMH_CSV_LABEL 3
+#define KMH_CSV_U64   4
+typedef struct kmh_text kmh_text;
+int kmh_csv_format(int ncols, const int32_t* kinds, const void* const* data, const void* const* aux,
+                   uint64_t nrows, int threads, kmh_text** out);
+/* Borrow the text (valid until kmh_text_free). */
+int kmh_text_data(const kmh_text* t, const char** data, uint64_t* len);
+void kmh_text_free(kmh_text* t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,7 +67,12 @@ SIGNATURES = [
                                                 _vp, _vp]),
     ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
                                           _u64, _vp, _vp]),
+    ("kmh_csv_format", _c.c_int, [_c.c_int, _vp, _vp, _vp, _u64, _c.c_int, _c.POINTER(_vp)]),
+    ("kmh_text_data", _c.c_int, [_vp, _c.POINTER(_vp), _u64p]),
+    ("kmh_text_free", None, [_vp]),
 ]
+
+CSV_I64, CSV_F64, CSV_STR, CSV_LABEL, CSV_U64 = 0, 1, 2, 3, 4
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -413,3 +418,58 @@ def sparse_out_offsets(offsets, k):
     out = np.zeros(off.size, dtype=np.uint64)
     lib().kmh_sparse_out_offsets(_ptr(off), off.size - 1, int(k), _ptr(out))
     return out
+
+
+class _Text:
+    """Owns a kmh_text; the numpy view of its bytes keeps it alive."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def __del__(self):
+        if self._h:
+            lib().kmh_text_free(self._h)
+            self._h = None
+
+
+def csv_format(columns, nrows, threads=0):
+    """CSV rows of a column block (kmh_csv_format: pandas' to_csv text without the header).
+
+    columns: list of (kind, data, aux) with kind one of CSV_*: CSV_I64 / CSV_U64 / CSV_F64 take a
+    numpy array; CSV_STR a (utf-8 bytes, uint64 offsets[nrows + 1]) pair as (data, aux); CSV_LABEL
+    uint64 codes and aux = k.  Returns a uint8 numpy view of the text (no copy), or None when
+    pandas would write some value differently (NaN / inf, text needing quotes)."""
+    keep = []
+    kinds = np.array([c[0] for c in columns], dtype=np.int32)
+    data = (ctypes.c_void_p * max(len(columns), 1))()
+    aux = (ctypes.c_void_p * max(len(columns), 1))()
+    for j, (kind, d, x) in enumerate(columns):
+        if kind in (CSV_I64, CSV_U64, CSV_F64):
+            arr = np.ascontiguousarray(d, dtype={CSV_I64: np.int64, CSV_U64: np.uint64, CSV_F64: np.float64}[kind])
+            keep.append(arr)
+            data[j] = arr.ctypes.data if arr.size else None
+        elif kind == CSV_STR:
+            buf = np.frombuffer(d, np.uint8) if len(d) else np.zeros(1, np.uint8)
+            off = np.ascontiguousarray(x, dtype=np.uint64)
+            keep += [buf, off]
+            data[j], aux[j] = buf.ctypes.data, off.ctypes.data
+        elif kind == CSV_LABEL:
+            arr = np.ascontiguousarray(d, dtype=np.uint64)
+            kk = np.array([int(x)], dtype=np.int64)
+            keep += [arr, kk]
+            data[j], aux[j] = (arr.ctypes.data if arr.size else None), kk.ctypes.data
+        else:
+            raise ValueError(f"csv_format: unknown column kind {kind}")
+    h = ctypes.c_void_p()
+    rc = lib().kmh_csv_format(len(columns), _ptr(kinds), data, aux, int(nrows), int(threads), ctypes.byref(h))
+    if rc == KMH_ERR_UNSUPPORTED:
+        return None
+    _check(rc)
+    owner = _Text(h)
+    p, n = ctypes.c_void_p(), ctypes.c_uint64()
+    _check(lib().kmh_text_data(h, ctypes.byref(p), ctypes.byref(n)))
+    if n.value == 0:
+        return np.zeros(0, np.uint8)
+    buf = (ctypes.c_uint8 * n.value).from_address(p.value)
+    buf._owner = owner
+    return np.frombuffer(buf, dtype=np.uint8)

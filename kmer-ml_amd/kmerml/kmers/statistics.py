@@ -79,7 +79,7 @@ class KmerFeatureExtractor:
         genome_size = None
         if hasattr(self, 'metadata_manager'):
             genome_size = self.metadata_manager.get_genome_size(organism)
-        frames = []
+        blocks = []
         total = len(kmer_files)
         start = time.time()
         for i, kmer_file in enumerate(kmer_files, 1):
@@ -88,17 +88,17 @@ class KmerFeatureExtractor:
                 print(f"Warning: Could not extract k value from {kmer_file}")
                 continue
             df = self._load_kmer_file(kmer_file)
-            frames.append(self.feature_frame(df, k_val, required_features))
+            blocks.append(self.feature_block(df, k_val, required_features))
             start = progress_bar(i, total, start_time=start, title="K values processed")
-        frames = [f for f in frames if len(f)]
-        if not frames:
+        blocks = [b for b in blocks if b.nrows]
+        if not blocks:
             print(f"No features extracted for {organism}")
             return None
-        result = pd.concat(frames, ignore_index=True) if len(frames) > 1 else frames[0]
         if genome_size:
-            result['genome_size'] = genome_size
+            for b in blocks:
+                b.cols['genome_size'] = np.full(b.nrows, genome_size)
         output_file = self.output_dir / f"{organism}_kmer_features.csv"
-        write_csv(result, output_file)
+        write_feature_csv(blocks, output_file)
         print(f"Created feature CSV for {organism}: {output_file}")
         return output_file
 
@@ -119,15 +119,22 @@ class KmerFeatureExtractor:
     @classmethod
     def feature_frame(cls, df, k_val, required_features):
         """The rows statistics.py:149-186 would produce for one k-mer file, as a DataFrame."""
-        labels = cls.decode_labels(df['kmer'])
-        cols = {'kmer': labels, 'count': df['count'].to_numpy(), 'k': np.full(len(labels), k_val, dtype=np.int64)}
-        if len(labels) == 0:
-            return pd.DataFrame(cols)
-        codes = label_codes(df['kmer'].to_numpy(), k_val)
+        return cls.feature_block(df, k_val, required_features).frame()
+
+    @classmethod
+    def feature_block(cls, df, k_val, required_features):
+        """feature_frame's columns without the DataFrame (a FeatureBlock): the label column stays
+        as codes when every label is an integer-parsed k-mer, for the native CSV writer."""
+        n = len(df)
+        codes = label_codes(df['kmer'].to_numpy(), k_val) if n else None
+        cols = {'kmer': None, 'count': df['count'].to_numpy(), 'k': np.full(n, k_val, dtype=np.int64)}
+        block = FeatureBlock(cols, n, df['kmer'], codes, k_val)
+        if n == 0:
+            return block
         if codes is not None:   # every label is a k-mer: features computed per code
             f = code_features_of(k_val, codes)
         else:
-            f = label_features([str(x) for x in labels])
+            f = label_features([str(x) for x in block.labels()])
         if 'gc_content' in required_features:
             cols['gc_percent'] = f['gc_percent']
         if 'base_counts' in required_features:
@@ -144,7 +151,7 @@ class KmerFeatureExtractor:
             cols['normalized_entropy'] = f['shannon_entropy'] / 2.0
         if 'repeats' in required_features:
             cols['has_repeat'] = f['has_repeat']
-        return pd.DataFrame(cols)
+        return block
 
     # ------------------------------------------------------------------ helpers
     def _extract_k_from_filename(self, filename):
@@ -165,6 +172,81 @@ class KmerFeatureExtractor:
         except Exception:
             df = pd.read_csv(filepath, sep='\t', header=None, names=['kmer', 'count'], compression=compression)
         return df
+
+
+class FeatureBlock:
+    """The feature rows of one k-mer file (statistics.py:149-186): column name -> numpy array,
+    in the reference's column order.  The 'kmer' column is kept as the file's label column and,
+    when every label is an integer-parsed k-mer, its codes (label_codes), so the native writer
+    prints the labels from the codes without building a Python string per row."""
+
+    def __init__(self, cols, nrows, raw_labels, codes, k):
+        self.cols, self.nrows, self.raw_labels, self.codes, self.k = cols, nrows, raw_labels, codes, k
+
+    def labels(self):
+        """The 'kmer' column as statistics.py:157 sees it (decode_labels)."""
+        return KmerFeatureExtractor.decode_labels(self.raw_labels)
+
+    def frame(self):
+        cols = dict(self.cols)
+        cols['kmer'] = self.labels() if self.nrows else np.empty(0, dtype=object)
+        return pd.DataFrame(cols)
+
+
+def _native_columns(block):
+    """(kind, data, aux) per column for _native.csv_format, or None if a column has a dtype the
+    native writer does not print the way pandas does."""
+    from kmerml import _native
+    out = []
+    for name, v in block.cols.items():
+        if name == 'kmer':
+            if block.codes is not None:
+                out.append((_native.CSV_LABEL, block.codes.astype(np.uint64), block.k))
+                continue
+            labels = block.labels()
+            if not all(type(x) is str for x in labels):
+                return None
+            enc = [x.encode('utf-8') for x in labels]
+            off = np.zeros(len(enc) + 1, dtype=np.uint64)
+            np.cumsum(np.fromiter(map(len, enc), dtype=np.uint64, count=len(enc)), out=off[1:])
+            out.append((_native.CSV_STR, b''.join(enc), off))
+            continue
+        v = np.asarray(v)
+        if v.dtype.kind == 'i':
+            out.append((_native.CSV_I64, v, None))
+        elif v.dtype.kind == 'u':
+            out.append((_native.CSV_U64, v, None))
+        elif v.dtype == np.float64:
+            out.append((_native.CSV_F64, v, None))
+        else:
+            return None
+    return out
+
+
+def _dtype_signature(block):
+    return tuple((name, 'O' if name == 'kmer' else np.asarray(v).dtype.str) for name, v in block.cols.items())
+
+
+def write_feature_csv(blocks, path):
+    """``pd.concat([b.frame() for b in blocks]).to_csv(path, index=False)``, with the rows of
+    each block formatted by the native writer (kmh_csv_format: Python's float repr, integer
+    str(), the k-mer labels printed from their codes).  A block holding a value pandas writes
+    differently (NaN, inf, text that needs quoting) is written by pandas itself; blocks whose
+    column dtypes differ (pandas would then upcast the concatenated column) are all written by
+    pandas."""
+    from kmerml import _native
+    if len({_dtype_signature(b) for b in blocks}) > 1 or any(q in name for name in blocks[0].cols for q in _NEEDS_QUOTES):
+        frames = [b.frame() for b in blocks]
+        (pd.concat(frames, ignore_index=True) if len(frames) > 1 else frames[0]).to_csv(path, index=False)
+        return
+    with open(path, 'wb') as f:
+        f.write((','.join(blocks[0].cols) + '\n').encode())
+        for b in blocks:
+            cols = _native_columns(b)
+            text = _native.csv_format(cols, b.nrows) if cols is not None else None
+            if text is None:
+                text = b.frame().to_csv(index=False, header=False).encode('utf-8')
+            f.write(text)
 
 
 _NEEDS_QUOTES = (',', '"', '\n', '\r')

@@ -257,3 +257,46 @@ def test_feature_frame_sparse_large_k(monkeypatch, k):
     monkeypatch.setattr(st, "label_codes", lambda v, kk: None)
     slow = st.KmerFeatureExtractor.feature_frame(df, k, st.DEFAULT_FEATURES)
     assert fast.to_csv() == slow.to_csv()
+
+
+def test_native_csv_equals_pandas(features2):
+    """kmh_csv_format (the native writer of the feature CSV rows) prints exactly the text of
+    pandas' to_csv(index=False): the reference-fixture frames, floats over every exponent, labels
+    printed from k-mer codes; NaN / inf and text that needs quotes are refused (pandas path)."""
+    from kmerml import _native
+    from kmerml.kmers.statistics import FeatureBlock, _native_columns
+
+    def native_text(df, codes=None, k=None):
+        cols = {c: df[c].to_numpy() for c in df.columns}
+        b = FeatureBlock(cols, len(df), df["kmer"] if "kmer" in df else None, codes, k)
+        nc = _native_columns(b)
+        t = _native.csv_format(nc, len(df)) if nc is not None else None
+        return None if t is None else ",".join(df.columns) + "\n" + t.tobytes().decode()
+
+    for org in ("orgC", "orgD"):
+        df = pd.read_csv(features2 / f"{org}_kmer_features.csv", keep_default_na=False)
+        assert native_text(df) == df.to_csv(index=False)
+    rng = np.random.default_rng(21)
+    bits = rng.integers(0, 2**63, 200_000, dtype=np.uint64) | (rng.integers(0, 2, 200_000, dtype=np.uint64) << np.uint64(63))
+    x = bits.view(np.float64)
+    x = x[np.isfinite(x)]
+    extra = np.array([0.0, -0.0, 1e16, 1e15, 9999999999999998.0, 1e-4, 1e-5, 0.1 + 0.2, 5e-324, 50.0,
+                      1.7976931348623157e308, 123456789012345678.0, 2 / 3, 100.0, 1e22, 1e-300])
+    x = np.concatenate([x, extra, rng.random(5000) * 100])
+    df = pd.DataFrame({"kmer": ["ACGT"] * x.size, "count": rng.integers(-5, 2**62, x.size), "x": x})
+    assert native_text(df) == df.to_csv(index=False)
+    # labels from codes = the integer-parsed labels decoded (k = 1, 12, 19; A...A, leading A's)
+    for k in (1, 12, 19):
+        codes = rng.integers(0, 4 ** k, 3000, dtype=np.int64)
+        codes[:2] = [0, 4 ** k - 1]
+        dig = np.array([0, 2, 3, 1])
+        lab = np.zeros(codes.size, np.int64)
+        for i in range(k):
+            lab = lab * 10 + dig[(codes >> (2 * (k - 1 - i))) & 3]
+        raw = pd.DataFrame({"kmer": lab, "count": np.ones(codes.size, np.int64)})
+        want = pd.DataFrame({"kmer": KmerFeatureExtractor.decode_labels(raw["kmer"]), "count": raw["count"]})
+        assert native_text(raw, codes=codes, k=k) == want.to_csv(index=False)
+    assert native_text(pd.DataFrame({"kmer": ["A"], "x": [float("nan")]})) is None
+    assert native_text(pd.DataFrame({"kmer": ["A"], "x": [float("inf")]})) is None
+    assert native_text(pd.DataFrame({"kmer": ["a,b"], "count": [1]})) is None
+    assert native_text(pd.DataFrame({"kmer": [""], "count": [1]})) is None
