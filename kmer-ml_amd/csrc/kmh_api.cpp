@@ -352,13 +352,10 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
         return fail(ctx, KMH_ERR_UNSUPPORTED, "k must be in [1, 1024] (k = " + std::to_string(k) + ")");
     if (canonical && k > KMH_MAX_SPARSE_K)
         return fail(ctx, KMH_ERR_UNSUPPORTED, "canonical counting needs k <= 32 (k = " + std::to_string(k) + ")");
-    // Size limits, checked before any byte is read or staged ("Limits"): the
-    // dense table path takes sequences below 2^32 - 1 bytes (u32 positions and counts); the
-    // sort paths (k >= 13, canonical) take fewer than 2^31 windows per call (hipCUB item counts).
+    // Size limit, checked before any byte is read or staged ("Limits"): every path
+    // takes sequences below 2^32 - 1 bytes (u32 positions and counts; item counts are 64-bit).
     if (n >= 0xFFFFFFFFull)
         return fail(ctx, KMH_ERR_UNSUPPORTED, "sequence must be shorter than 2^32 - 1 bytes (one call)");
-    if ((k > KMH_MAX_DENSE_K || canonical) && n >= (uint64_t)k && n - (uint64_t)k + 1 > 0x7FFFFFFFull)
-        return fail(ctx, KMH_ERR_UNSUPPORTED, "k >= 13 / canonical counting takes fewer than 2^31 windows per call");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     std::unique_ptr<kmh_kmers> r(new (std::nothrow) kmh_kmers);
     if (!r) return fail(ctx, KMH_ERR_NOMEM, "out of host memory");
@@ -379,9 +376,13 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
                                        ctx->stream)))
                 return rc;
 
-        } else if (k <= KMH_MAX_SPARSE_K) {
+        } else if (k <= KMH_MAX_DENSE_K) {   // canonical, k <= 12: sort path
             if ((rc = kmh::sparse_count(ctx, d_seq, n, k, canonical, r->codes, r->counts, r->first,
                                         ctx->stream)))
+                return rc;
+        } else if (k <= KMH_MAX_SPARSE_K) {  // 13 <= k <= 32: hash-table path with first positions
+            if ((rc = kmh::sparse_count_first(ctx, d_seq, n, k, canonical, r->codes, r->counts, r->first,
+                                              ctx->stream)))
                 return rc;
         } else {
             if ((rc = kmh::sparse_count_long(ctx, d_seq, n, k, r->codes, r->counts, r->first, ctx->stream)))

@@ -28,8 +28,6 @@
 //                     kernel cannot hold, emits nothing; those passes are counted by
 //                     gather + hipCUB radix sort + run-length encode from the step-1 entries
 //                     (keys of different passes are disjoint, so nothing is counted twice).
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -44,24 +42,42 @@ constexpr int kSpThreads = 1024;           // threads of every workgroup here
 constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
-constexpr int kTileChunks = 8192;          // 16-byte chunks of a tile's entries (both widths)
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
 constexpr int kQU = 4;                     // chunk loads in flight per lane
 
 // Entry width: u32 residues (k <= 21) or u64 (22 <= k <= 32).  A u64 tile holds half the windows,
 // so a tile's entries (128 KiB) and a split item's staging (80 KiB) keep their LDS size.
-template <typename E> struct Sp;
-template <> struct Sp<uint32_t> {
+// POS (the drop-in's first occurrences): every entry also carries its window position (u32,
+// relative to its genome) in a parallel array of the same layout; tiles and stagings are
+// halved again so that entries + positions keep the same LDS.
+template <typename E, bool POS> struct Sp;
+template <> struct Sp<uint32_t, false> {
     static constexpr int WPT = 32;                 // window starts per thread
     static constexpr int TILE = kSpThreads * WPT;  // 32768 window starts per tile (= kTile)
     static constexpr int CAPS = 20480;             // entries staged by one split item (80 KiB)
 };
-template <> struct Sp<uint64_t> {
+template <> struct Sp<uint64_t, false> {
     static constexpr int WPT = 16;
     static constexpr int TILE = kSpThreads * WPT;  // 16384
     static constexpr int CAPS = 10240;             // 80 KiB
 };
+template <> struct Sp<uint32_t, true> {
+    static constexpr int WPT = 16;
+    static constexpr int TILE = kSpThreads * WPT;  // 16384 (entries + positions: 128 KiB)
+    static constexpr int CAPS = 10240;             // 80 KiB with positions
+};
+template <> struct Sp<uint64_t, true> {
+    static constexpr int WPT = 8;
+    static constexpr int TILE = kSpThreads * WPT;  // 8192 (96 KiB)
+    static constexpr int CAPS = 5120;              // 60 KiB
+};
 template <typename E> constexpr int epc() { return 16 / (int)sizeof(E); }   // entries per chunk
+// 16-byte chunks of a tile's entries (8192, or 4096 with positions) and the bits of a queue
+// entry that hold the chunk (the rest hold the tile within the batch)
+template <typename E, bool POS> constexpr int tile_chunks() { return Sp<E, POS>::TILE * (int)sizeof(E) / 16; }
+template <typename E, bool POS> constexpr int chunk_bits() { return tile_chunks<E, POS>() == 8192 ? 13 : 12; }
+// positions of the entries of one chunk (4 u32 for u32 entries, 2 for u64)
+using PosChunk = uint4;
 
 // Tiles a wave of the split kernel takes per queue step, for segments of about `per` entries
 // of `epc` per 16-byte chunk: a step fills at most half of the kQueue-chunk queue.
@@ -70,7 +86,7 @@ __host__ __device__ __forceinline__ uint32_t split_bt(uint32_t per, uint32_t epc
     return bt < 1u ? 1u : (bt > 64u ? 64u : bt);
 }
 
-constexpr int kMaxPasses = 256;
+constexpr int kMaxPasses = 1024;           // passes of one bucket (a 2^32-window genome needs ~512)
 constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
 
@@ -146,23 +162,26 @@ __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
                 const uint64_t r = window<K>(rhi, rlo, 64 - j - K);
                 c = r < c ? r : c;
             }
-            f(c);
+            f(c, j);
         }
     }
 }
 
-template <int K, int CANON, typename E>
+template <int K, int CANON, typename E, bool POS>
 __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __restrict__ seq,
                                                              GenomeMap m,
                                                              E* __restrict__ ent,
+                                                             uint32_t* __restrict__ epos,
                                                              uint16_t* __restrict__ toff,
                                                              uint32_t ldt) {
     constexpr int R = 2 * K - kSpBucketBits;
     constexpr uint64_t RM = (1ull << R) - 1ull;
-    constexpr int WPT = Sp<E>::WPT, kSpTile = Sp<E>::TILE, EPC = epc<E>();
+    constexpr int WPT = Sp<E, POS>::WPT, kSpTile = Sp<E, POS>::TILE, EPC = epc<E>();
     static_assert(kSpBuckets == kSpThreads, "one bucket per thread in the scan");
+    static_assert(kMaxPasses <= kSpThreads, "one pass per thread in the split scan");
     static_assert(R <= 8 * (int)sizeof(E), "residues fit the entry");
     __shared__ __attribute__((aligned(16))) E sorted[kSpTile];
+    __shared__ __attribute__((aligned(16))) uint32_t spos[POS ? kSpTile : 4];
     __shared__ uint32_t cnt[kSpBuckets];
     __shared__ uint32_t wsum[kNW];
 
@@ -179,7 +198,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     const uint64_t base = tstart + (uint64_t)WPT * (uint64_t)tid;
     const Bases bs = (tstart + (uint64_t)kSpTile + 48 <= m.data_end) ? load_bases<true>(seq, base, ge)
                                                                      : load_bases<false>(seq, base, ge);
-    each_window<K, CANON, WPT>(bs, [&](uint64_t c) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
+    each_window<K, CANON, WPT>(bs, [&](uint64_t c, int) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
     __syncthreads();
 
     // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
@@ -204,9 +223,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     if (tid == 0) toff[(uint64_t)kSpBuckets * ldt + lt] = (uint16_t)total;
     __syncthreads();
 
-    each_window<K, CANON, WPT>(bs, [&](uint64_t c) {
+    // window position of this thread's window 0, relative to the genome (< 2^32 - 1)
+    const uint32_t p0 = (uint32_t)(base - m.goff[g]);
+    each_window<K, CANON, WPT>(bs, [&](uint64_t c, int j) {
         const uint32_t slot = atomicAdd(&cnt[(uint32_t)(c >> R)], 1u);
         sorted[slot] = (E)(c & RM);
+        if constexpr (POS) spos[slot] = p0 + (uint32_t)j;
     });
     __syncthreads();
 
@@ -215,6 +237,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     for (uint32_t i = tid; i < n4; i += kSpThreads)
         store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
     if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
+    if constexpr (POS) {
+        uint32_t* pdst = epos + lt * (uint64_t)kSpTile;
+        for (uint32_t i = tid; i < total / 4; i += kSpThreads)
+            store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
+        if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+    }
 }
 
 // Entries of every (genome, bucket) of a batch: one workgroup per pair.
@@ -264,31 +292,50 @@ struct SplitItem {
 // tiles form a single (first and last) queue step of at most 64 * kQU chunks -- the common case -- keeps them
 // in registers (kv, kq) on the first walk (REUSE = false sets kept) and the second walk
 // (REUSE = true) takes them from there instead of reading the entries again; the segment
-// bounds stay in the wave's LDS slo / shi, which nothing writes in between.
+// bounds stay in the wave's LDS slo / shi, which nothing writes in between.  POS: the
+// positions of the chunk's entries ride along (pv).
+template <bool POS>
 struct Kept {
     uint4 v[kQU];
+    PosChunk pv[POS ? kQU : 1];
     uint32_t q[kQU];
     bool kept;
 };
 
-template <bool REUSE, typename E, typename F>
-__device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
+// Positions of entries [4 c, 4 c + 4) (u32 entries) or [2 c, 2 c + 2) (u64) of a tile's layout.
+template <typename E>
+__device__ __forceinline__ PosChunk load_pos(const uint32_t* __restrict__ epos, uint64_t chunk) {
+    if constexpr (sizeof(E) == 4) return reinterpret_cast<const uint4*>(epos)[chunk];
+    const uint2 x = reinterpret_cast<const uint2*>(epos)[chunk];
+    return make_uint4(x.x, x.y, 0u, 0u);
+}
+
+__device__ __forceinline__ uint32_t pos_of(const PosChunk& v, int i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+template <bool REUSE, bool POS, typename E, typename F>
+__device__ __forceinline__ void walk_bucket(const E* __restrict__ ent, const uint32_t* __restrict__ epos,
                                             const uint16_t* __restrict__ toff, uint32_t ldt,
                                             uint32_t b, uint64_t ta, uint64_t tb, uint32_t bt,
-                                            uint32_t* q, uint32_t* slo, uint32_t* shi, Kept& kc, F&& f) {
+                                            uint32_t* q, uint32_t* slo, uint32_t* shi, Kept<POS>& kc, F&& f) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint4* chunks = reinterpret_cast<const uint4*>(ent);
     constexpr uint32_t EPC = (uint32_t)epc<E>();
+    constexpr int CB = chunk_bits<E, POS>();
+    constexpr uint32_t CM = (1u << CB) - 1u;
+    constexpr uint64_t TC = (uint64_t)tile_chunks<E, POS>();
     if constexpr (REUSE) {
         if (kc.kept) {   // wave-uniform
 #pragma unroll
             for (int u = 0; u < kQU; ++u) {
                 const bool live = kc.q[u] != kEmpty;
                 const uint32_t qv = live ? kc.q[u] : 0u;
-                const uint32_t tl = qv >> 13, p0 = (qv & 8191u) * EPC;
+                const uint32_t tl = qv >> CB, p0 = (qv & CM) * EPC;
                 const uint32_t l = slo[tl], h = live ? shi[tl] : 0u;
 #pragma unroll
-                for (int i = 0; i < (int)EPC; ++i) f(lane_of<E>(kc.v[u], i), p0 + i >= l && p0 + i < h);
+                for (int i = 0; i < (int)EPC; ++i)
+                    f(lane_of<E>(kc.v[u], i), POS ? pos_of(kc.pv[POS ? u : 0], i) : 0u, p0 + i >= l && p0 + i < h);
             }
             return;
         }
@@ -313,28 +360,32 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
             slo[lane] = lo;
             shi[lane] = hi;
             const uint32_t ex = incl - nc;
-            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = ((uint32_t)lane << 13) | (c0 + j);
+            for (uint32_t j = 0; j < nc; ++j) q[ex + j] = ((uint32_t)lane << CB) | (c0 + j);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             for (uint32_t r0 = 0; r0 < total; r0 += 64u * kQU) {
                 uint4 v[kQU];
+                PosChunk pv[POS ? kQU : 1];
                 uint32_t qe[kQU];
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
                     const uint32_t e = r0 + (uint32_t)(u * 64 + lane);
                     qe[u] = q[e < total ? e : 0u];  // idle lanes re-read entry 0 (valid)
-                    v[u] = chunks[(tw + (qe[u] >> 13)) * (uint64_t)kTileChunks + (qe[u] & 8191u)];
+                    const uint64_t ci = (tw + (qe[u] >> CB)) * TC + (qe[u] & CM);
+                    v[u] = chunks[ci];
+                    if constexpr (POS) pv[u] = load_pos<E>(epos, ci);
                     if (e >= total) qe[u] = kEmpty;
                 }
 #pragma unroll
                 for (int u = 0; u < kQU; ++u) {
                     const bool live = qe[u] != kEmpty;   // idle lanes: every entry invalid
                     const uint32_t qv = live ? qe[u] : 0u;
-                    const uint32_t tl = qv >> 13, p0 = (qv & 8191u) * EPC;
+                    const uint32_t tl = qv >> CB, p0 = (qv & CM) * EPC;
                     const uint32_t l = slo[tl], h = live ? shi[tl] : 0u;
 #pragma unroll
-                    for (int i = 0; i < (int)EPC; ++i) f(lane_of<E>(v[u], i), p0 + i >= l && p0 + i < h);
+                    for (int i = 0; i < (int)EPC; ++i)
+                        f(lane_of<E>(v[u], i), POS ? pos_of(pv[POS ? u : 0], i) : 0u, p0 + i >= l && p0 + i < h);
                 }
                 if constexpr (!REUSE) {
                     // the wave's only step, in one round: keep the chunks for the second walk
@@ -344,6 +395,7 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
 #pragma unroll
                         for (int u = 0; u < kQU; ++u) {
                             kc.v[u] = v[u];
+                            if constexpr (POS) kc.pv[u] = pv[u];
                             kc.q[u] = qe[u];
                         }
                     }
@@ -353,22 +405,26 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent,
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else {  // skewed batch: each lane walks its own segment
-            for (uint32_t j = lo; j < hi; ++j) f(ent[t * (uint64_t)Sp<E>::TILE + j], true);
+            for (uint32_t j = lo; j < hi; ++j) {
+                const uint64_t ix = t * (uint64_t)Sp<E, POS>::TILE + j;
+                f(ent[ix], POS ? epos[ix] : 0u, true);
+            }
         }
     }
 }
 
-template <typename E>
+template <typename E, bool POS>
 __global__ __launch_bounds__(kSpThreads) void k_sp_split(
-    const E* __restrict__ ent, const uint16_t* __restrict__ toff, uint32_t ldt,
-    const SplitItem* __restrict__ items, int R, E* __restrict__ out,
+    const E* __restrict__ ent, const uint32_t* __restrict__ epos, const uint16_t* __restrict__ toff, uint32_t ldt,
+    const SplitItem* __restrict__ items, int R, E* __restrict__ out, uint32_t* __restrict__ opos,
     uint16_t* __restrict__ toff2, uint32_t* __restrict__ gb_fail) {
-    constexpr int kCaps = Sp<E>::CAPS, EPC = epc<E>();
+    constexpr int kCaps = Sp<E, POS>::CAPS, EPC = epc<E>();
     __shared__ __attribute__((aligned(16))) E sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
+    __shared__ __attribute__((aligned(16))) uint32_t spos[POS ? kCaps + 64 : 4];
     __shared__ uint32_t hist[kMaxPasses + 32];   // + dummy passes
     __shared__ uint32_t q[kNW][kQueue];
     __shared__ uint32_t slo[kNW][64], shi[kNW][64];
-    __shared__ uint32_t wsum[4], total_sh;
+    __shared__ uint32_t wsum[kMaxPasses / 64], total_sh;
 
     const uint32_t item = xcd_work_id();
     const SplitItem it = items[item];
@@ -381,9 +437,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
     // tail of `sorted`, so no exec-mask branch surrounds an atomic.
     const uint32_t dpass = (uint32_t)kMaxPasses + (uint32_t)(lane & 31);
-    Kept kc;
-    walk_bucket<false>(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc,
-                       [&](E r, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
+    Kept<POS> kc;
+    walk_bucket<false, POS>(ent, epos, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc,
+                            [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
     __syncthreads();
     // exclusive scan of the pass histogram (threads 0..255)
     uint32_t n0 = 0u, incl = 0u;
@@ -405,7 +461,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         hist[tid] = st;
         if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)st;
         if (tid == 0) {
-            const uint32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            uint32_t tot = 0u;
+#pragma unroll
+            for (int w = 0; w < kMaxPasses / 64; ++w) tot += wsum[w];
             total_sh = tot;
             toff2[(uint64_t)item * kT2 + np] = (uint16_t)(tot <= (uint32_t)kCaps ? tot : 0u);
             if (tot > (uint32_t)kCaps) gb_fail[it.gb] = 1u;
@@ -414,9 +472,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     __syncthreads();
     const uint32_t total = total_sh;
     if (total > (uint32_t)kCaps) return;  // staging overflow: the bucket goes to the fallback
-    walk_bucket<true>(ent, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc, [&](E r, bool ok) {
+    walk_bucket<true, POS>(ent, epos, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc,
+                           [&](E r, uint32_t p, bool ok) {
         const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
-        sorted[ok ? slot : (uint32_t)kCaps + (uint32_t)lane] = r;
+        const uint32_t at = ok ? slot : (uint32_t)kCaps + (uint32_t)lane;
+        sorted[at] = r;
+        if constexpr (POS) spos[at] = p;
     });
     __syncthreads();
     E* dst = out + (uint64_t)item * kCaps;
@@ -424,6 +485,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     for (uint32_t i = tid; i < n4; i += kSpThreads)
         store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
     if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
+    if constexpr (POS) {
+        uint32_t* pdst = opos + (uint64_t)item * kCaps;
+        for (uint32_t i = tid; i < total / 4; i += kSpThreads)
+            store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
+        if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+    }
 }
 
 // Count work item: pass p of bucket b of genome g; its entries are segment p of split items
@@ -546,9 +613,11 @@ constexpr int kHSlots = 1024;    // hash table of the big bins
 constexpr int kMaxBig = 256;     // big bins of one item (more: the item goes to the fallback)
 constexpr int kCntThreads = 512; // two count workgroups per CU (74 KiB of LDS each) hide each
                                  // other's load latency
-template <typename E> struct Cnt;
-template <> struct Cnt<uint32_t> { static constexpr int CAP = 8192; };   // keys of one item
-template <> struct Cnt<uint64_t> { static constexpr int CAP = 4096; };
+template <typename E, bool POS> struct Cnt;
+template <> struct Cnt<uint32_t, false> { static constexpr int CAP = 8192; };   // keys of one item
+template <> struct Cnt<uint64_t, false> { static constexpr int CAP = 4096; };
+template <> struct Cnt<uint32_t, true> { static constexpr int CAP = 4096; };    // + positions
+template <> struct Cnt<uint64_t, true> { static constexpr int CAP = 2048; };
 
 #ifdef KMH_EXPERIMENTS
 __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks of k_sp_count
@@ -557,20 +626,22 @@ __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks 
 #define KMH_PT(i)
 #endif
 
-template <typename E>
+template <typename E, bool POS>
 __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_count(
-    const E* __restrict__ split, const uint16_t* __restrict__ toff2,
+    const E* __restrict__ split, const uint32_t* __restrict__ opos, const uint16_t* __restrict__ toff2,
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
     const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
-    uint32_t* __restrict__ counts, unsigned long long* __restrict__ nk,
+    uint32_t* __restrict__ counts, uint32_t* __restrict__ firsts, unsigned long long* __restrict__ nk,
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
-    constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
+    constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E, POS>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
     constexpr int BQ = BPT / 4;   // uint4 words of a thread's bins
-    constexpr int kCaps = Sp<E>::CAPS, U = 4;
+    constexpr int kCaps = Sp<E, POS>::CAPS, U = 4;
     constexpr bool WIDE = sizeof(E) == 8;
     static_assert(BPT % 4 == 0 && HPT >= 1 && C % NT == 0, "thread layout");
     __shared__ __attribute__((aligned(16))) uint32_t hist[kBins];
     __shared__ __attribute__((aligned(16))) E sorted[C];
+    __shared__ uint32_t spos[POS ? C : 1];          // positions of sorted[] (POS)
+    __shared__ uint32_t hmin[POS ? kHSlots : 1];    // first position of each big-bin slot (POS)
     __shared__ unsigned long long htab[kHSlots];
     __shared__ uint32_t bigl[kMaxBig];
     __shared__ uint32_t wtot[kNW];
@@ -594,6 +665,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     zero_bins();
 #pragma unroll
     for (int q = 0; q < HPT; ++q) htab[q * NT + tid] = 0ull;
+    if constexpr (POS) {
+#pragma unroll
+        for (int q = 0; q < HPT; ++q) hmin[q * NT + tid] = 0xFFFFFFFFu;
+    }
     if (tid == 0) nbig = bad = 0u;
     lds_barrier();
 #ifdef KMH_EXPERIMENTS
@@ -638,6 +713,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
             for (uint32_t c = ea; c < eb; c += 64u * U) {
                 E r[U];
+                uint32_t rp[U];
                 bool ok[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -657,10 +733,11 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
                                           (uint32_t)__shfl((int)sb_lo, sj);
                     r[u] = split[base + es];
+                    rp[u] = POS ? opos[base + es] : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    if (ok[u]) f(r[u]);
+                    if (ok[u]) f(r[u], rp[u]);
             }
         }
         return ntot;
@@ -672,6 +749,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     constexpr int KPL = C / NT;                 // keys per lane of a single-group share
     const bool single = it.s1 - it.s0 <= 64u;   // uniform
     E kr[KPL];
+    uint32_t kp[POS ? KPL : 1];                 // their positions (POS)
     uint32_t kn = 0u;                           // valid keys of this lane (a prefix of kr)
     uint32_t ntot;
     if (single) {
@@ -712,13 +790,14 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
                                       (uint32_t)__shfl((int)sb_lo, sj);
                 kr[u] = split[base + es];
+                if constexpr (POS) kp[u] = opos[base + es];
             }
 #pragma unroll
             for (int u = 0; u < KPL; ++u)
                 if ((uint32_t)u < kn) atomicAdd(&hist[bin_of(kr[u])], 1u);
         }
     } else {
-        ntot = walk([&](E r) { atomicAdd(&hist[bin_of(r)], 1u); });
+        ntot = walk([&](E r, uint32_t) { atomicAdd(&hist[bin_of(r)], 1u); });
     }
     KMH_PT(0)
     lds_barrier();
@@ -777,9 +856,17 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (single) {
 #pragma unroll
         for (int u = 0; u < KPL; ++u)
-            if ((uint32_t)u < kn) sorted[atomicAdd(&hist[bin_of(kr[u])], 1u)] = kr[u];
+            if ((uint32_t)u < kn) {
+                const uint32_t at = atomicAdd(&hist[bin_of(kr[u])], 1u);
+                sorted[at] = kr[u];
+                if constexpr (POS) spos[at] = kp[u];
+            }
     } else {
-        walk([&](E r) { sorted[atomicAdd(&hist[bin_of(r)], 1u)] = r; });
+        walk([&](E r, uint32_t p) {
+            const uint32_t at = atomicAdd(&hist[bin_of(r)], 1u);
+            sorted[at] = r;
+            if constexpr (POS) spos[at] = p;
+        });
     }
     lds_barrier();
     KMH_PT(3)
@@ -805,10 +892,14 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         }
                         unsigned long long* slot = &htab[h];
                         const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)key << CB) | 1ull);
-                        if (old == 0ull) break;
+                        if (old == 0ull) {
+                            if constexpr (POS) atomicMin(&hmin[h], spos[i]);
+                            break;
+                        }
                         if ((E)(old >> CB) == key) {
                             const unsigned long long prev = atomicAdd(slot, 1ull);
                             if (WIDE && (prev & CM) == CM) bad = 1u;   // count field full
+                            if constexpr (POS) atomicMin(&hmin[h], spos[i]);
                             break;
                         }
                         h = (h + 1u) & (uint32_t)(kHSlots - 1);
@@ -827,6 +918,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     //    stores, compacted per wave with ballot + mbcnt so that they are coalesced.
     E ek[KPL];
     uint32_t ec[KPL];
+    uint32_t ef[POS ? KPL : 1];   // first position of the key (POS): the minimum over its bin's copies
     uint32_t fm = 0u;   // bit j: position j * NT + tid is emitted
 #pragma unroll
     for (int jj = 0; jj < KPL; ++jj) {
@@ -837,29 +929,39 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         const uint32_t bs = b ? hist[b - 1] : 0u, be = hist[b];
         bool first = i < ntot && be - bs <= (uint32_t)kBig;
         uint32_t c = 1u;
+        uint32_t fp = POS ? spos[ic] : 0u;
         // bins of up to 4 keys (all but a fraction of a percent): four independent reads, so
         // the twelve positions of a thread overlap their LDS round trips; larger bins loop
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const uint32_t y = bs + (uint32_t)t;
-            const E o = sorted[y < be ? y : bs];
+            const uint32_t yc = y < be ? y : bs;
+            const E o = sorted[yc];
             first = first && !(y < i && o == key);
             c += (y > i && y < be && o == key) ? 1u : 0u;
+            if constexpr (POS) fp = (y > i && y < be && o == key) ? min(fp, spos[yc]) : fp;
         }
         if (first && be - bs > 4u) {
             for (uint32_t y = bs + 4u; y < be; ++y) {
                 const E o = sorted[y];
                 first = first && !(y < i && o == key);
                 c += (y > i && o == key) ? 1u : 0u;
+                if constexpr (POS) fp = (y > i && o == key) ? min(fp, spos[y]) : fp;
             }
         }
         ek[jj] = key;
         ec[jj] = c;
+        if constexpr (POS) ef[jj] = fp;
         fm |= first ? (1u << jj) : 0u;
     }
     unsigned long long hs[HPT];
+    uint32_t hf[POS ? HPT : 1];
 #pragma unroll
     for (int q = 0; q < HPT; ++q) hs[q] = nb ? htab[q * NT + tid] : 0ull;
+    if constexpr (POS) {
+#pragma unroll
+        for (int q = 0; q < HPT; ++q) hf[q] = hmin[q * NT + tid];
+    }
     uint32_t wmine = 0u;   // the wave's emitted keys
 #pragma unroll
     for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
@@ -891,6 +993,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (nb) {
 #pragma unroll
         for (int q = 0; q < HPT; ++q) htab[q * NT + tid] = 0ull;
+        if constexpr (POS) {
+#pragma unroll
+            for (int q = 0; q < HPT; ++q) hmin[q * NT + tid] = 0xFFFFFFFFu;
+        }
     }
     lds_barrier();
     if (!fail_item) {
@@ -906,6 +1012,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 const uint64_t o = at + run + (uint32_t)__popcll(m & below);
                 codes[o] = hib | (uint64_t)ek[jj];
                 counts[o] = ec[jj];
+                if constexpr (POS) firsts[o] = ef[jj];
             }
             run += (uint32_t)__popcll(m);
         }
@@ -917,6 +1024,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 const uint64_t o = at + run + (uint32_t)__popcll(m & below);
                 codes[o] = hib | (hs[q] >> CB);
                 counts[o] = (uint32_t)(hs[q] & CM);
+                if constexpr (POS) firsts[o] = hf[q];
             }
             run += (uint32_t)__popcll(m);
         }
@@ -933,37 +1041,57 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #endif
 }
 
-// Fallback, step 1: the residues of bucket b, pass p of genome g, in any order.
-template <typename E>
-__global__ __launch_bounds__(256) void k_sp_gather(const E* __restrict__ ent,
+// Fallback, step 1: the residues of bucket b, pass p of genome g (and their positions), in
+// any order.
+template <typename E, bool POS>
+__global__ __launch_bounds__(256) void k_sp_gather(const E* __restrict__ ent, const uint32_t* __restrict__ epos,
                                                    const uint16_t* __restrict__ toff, uint32_t ldt,
                                                    uint64_t ta, uint64_t tb, uint32_t b, uint32_t p,
                                                    uint32_t np, int R, E* __restrict__ out,
-                                                   uint32_t* __restrict__ n) {
+                                                   uint32_t* __restrict__ opos, uint32_t* __restrict__ n) {
     const uint64_t t = ta + (uint64_t)blockIdx.x;
     if (t >= tb) return;
     const uint32_t lo = toff[(uint64_t)b * ldt + t], hi = toff[(uint64_t)(b + 1) * ldt + t];
     for (uint32_t j = lo + threadIdx.x; j < hi; j += 256) {
-        const E r = ent[t * (uint64_t)Sp<E>::TILE + j];
-        if (pass_of(r, np, R) == p) out[atomicAdd(n, 1u)] = r;
+        const uint64_t ix = t * (uint64_t)Sp<E, POS>::TILE + j;
+        const E r = ent[ix];
+        if (pass_of(r, np, R) == p) {
+            const uint32_t at = atomicAdd(n, 1u);
+            out[at] = r;
+            opos[at] = POS ? epos[ix] : at;   // without positions: any value (the sort needs one)
+        }
     }
 }
 
-// Fallback, step 3: append the run-length encoded keys to genome g's output.
 template <typename E>
-__global__ __launch_bounds__(256) void k_sp_append(const E* __restrict__ keys,
-                                                   const uint32_t* __restrict__ runs,
-                                                   const uint32_t* __restrict__ nruns, uint64_t hib,
-                                                   uint64_t off, unsigned long long* __restrict__ nk,
-                                                   uint64_t* __restrict__ codes,
-                                                   uint32_t* __restrict__ counts) {
+__global__ __launch_bounds__(256) void k_sp_gather_by(const E* __restrict__ src, const uint32_t* __restrict__ idx,
+                                                      uint32_t m, E* __restrict__ dst) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < m) dst[i] = src[idx[i]];
+}
+
+__global__ __launch_bounds__(256) void k_sp_iota(uint32_t* __restrict__ out, uint32_t m) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < m) out[i] = i;
+}
+
+// Fallback, step 3: append the runs of the sorted keys (count = run length, first position =
+// the run's first value: keys were sorted stably after their positions) to genome g's output.
+template <typename E, bool POS>
+__global__ __launch_bounds__(256) void k_sp_append(const E* __restrict__ keys, const uint32_t* __restrict__ pos,
+                                                   uint32_t m, const uint32_t* __restrict__ starts,
+                                                   const uint32_t* __restrict__ nruns, uint64_t hib, uint64_t off,
+                                                   unsigned long long* __restrict__ nk, uint64_t* __restrict__ codes,
+                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ firsts) {
     __shared__ unsigned long long base;
     const uint32_t n = *nruns;
     if (threadIdx.x == 0) base = atomicAdd(nk, (unsigned long long)n);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += 256) {
-        codes[off + base + i] = hib | keys[i];
-        counts[off + base + i] = runs[i];
+    for (uint32_t r = threadIdx.x; r < n; r += 256) {
+        const uint32_t a = starts[r], e = r + 1 < n ? starts[r + 1] : m;
+        codes[off + base + r] = hib | (uint64_t)keys[a];
+        counts[off + base + r] = e - a;
+        if constexpr (POS) firsts[off + base + r] = pos[a];
     }
 }
 
@@ -973,73 +1101,97 @@ void* carve(char*& p, size_t bytes) {
     return r;
 }
 
-template <int K, int CANON, typename E>
+template <int K, int CANON, typename E, bool POS>
 void launch_partition(unsigned tiles, hipStream_t s, const uint8_t* seq, const GenomeMap& m,
-                      E* ent, uint16_t* toff, uint32_t ldt) {
-    hipLaunchKernelGGL((k_sp_partition<K, CANON, E>), dim3(tiles), dim3(kSpThreads), 0, s, seq, m, ent,
-                       toff, ldt);
+                      E* ent, uint32_t* epos, uint16_t* toff, uint32_t ldt) {
+    hipLaunchKernelGGL((k_sp_partition<K, CANON, E, POS>), dim3(tiles), dim3(kSpThreads), 0, s, seq, m, ent,
+                       epos, toff, ldt);
 }
 
-template <int K, typename E>
+template <int K, typename E, bool POS>
 void partition_k(int canonical, unsigned tiles, hipStream_t s, const uint8_t* seq,
-                 const GenomeMap& m, E* ent, uint16_t* toff, uint32_t ldt) {
-    if (canonical) launch_partition<K, 1, E>(tiles, s, seq, m, ent, toff, ldt);
-    else launch_partition<K, 0, E>(tiles, s, seq, m, ent, toff, ldt);
+                 const GenomeMap& m, E* ent, uint32_t* epos, uint16_t* toff, uint32_t ldt) {
+    if (canonical) launch_partition<K, 1, E, POS>(tiles, s, seq, m, ent, epos, toff, ldt);
+    else launch_partition<K, 0, E, POS>(tiles, s, seq, m, ent, epos, toff, ldt);
 }
 
-template <typename E>
+template <typename E, bool POS>
 void launch_partition_k(int k, int canonical, unsigned tiles, hipStream_t s, const uint8_t* seq,
-                        const GenomeMap& m, E* ent, uint16_t* toff, uint32_t ldt) {
-#define KMH_PK(KK) case KK: partition_k<KK, E>(canonical, tiles, s, seq, m, ent, toff, ldt); break;
+                        const GenomeMap& m, E* ent, uint32_t* epos, uint16_t* toff, uint32_t ldt) {
+#define KMH_PK(KK) case KK: partition_k<KK, E, POS>(canonical, tiles, s, seq, m, ent, epos, toff, ldt); break;
     if constexpr (sizeof(E) == 4) {
         switch (k) { KMH_PK(13) KMH_PK(14) KMH_PK(15) KMH_PK(16) KMH_PK(17) KMH_PK(18) KMH_PK(19) KMH_PK(20)
-                     default: partition_k<21, E>(canonical, tiles, s, seq, m, ent, toff, ldt); break; }
+                     default: partition_k<21, E, POS>(canonical, tiles, s, seq, m, ent, epos, toff, ldt); break; }
     } else {
         switch (k) { KMH_PK(22) KMH_PK(23) KMH_PK(24) KMH_PK(25) KMH_PK(26) KMH_PK(27) KMH_PK(28) KMH_PK(29)
                      KMH_PK(30) KMH_PK(31)
-                     default: partition_k<32, E>(canonical, tiles, s, seq, m, ent, toff, ldt); break; }
+                     default: partition_k<32, E, POS>(canonical, tiles, s, seq, m, ent, epos, toff, ldt); break; }
     }
 #undef KMH_PK
 }
 
-// Fallback for pass p of bucket b of genome g: gather, radix sort, run-length encode, append.
-template <typename E>
+// Fallback for pass p of bucket b of genome g: gather, sort (radix_sort_pairs: with positions,
+// first by position and then stably by key, so a run's first entry holds its first position),
+// runs, append.  Hand-written kernels throughout (kmh_sort.hip).
+template <typename E, bool POS>
 int fallback_pass(Ctx* ctx, uint32_t g, uint32_t b, uint32_t p, uint32_t np, uint32_t n,
-                  const E* ent, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
+                  const E* ent, const uint32_t* epos, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
                   int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
-                  hipStream_t s) {
-    size_t t_sort = 0, t_rle = 0;
-    E* nulk = nullptr;
-    uint32_t* nul = nullptr;
-    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, t_sort, nulk, nulk, (int)n, 0, R, s));
-    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(nullptr, t_rle, nulk, nulk, nul, nul, (int)n, s));
-    const size_t temp = std::max(t_sort, t_rle);
-    const size_t arr = ((size_t)n * sizeof(E) + 255) & ~(size_t)255;
-    int rc = ensure(ctx, ctx->sparse[5], 4 * arr + temp + 1024);
+                  uint32_t* firsts, hipStream_t s) {
+    const size_t ne = ((size_t)n * sizeof(E) + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
+    int rc = ensure(ctx, ctx->sparse[5], 2 * ne + 7 * n4 + 1024);
     if (rc) return rc;
     char* p8 = static_cast<char*>(ctx->sparse[5].ptr);
-    E* a = static_cast<E*>(carve(p8, (size_t)n * sizeof(E)));
-    E* bsorted = static_cast<E*>(carve(p8, (size_t)n * sizeof(E)));
-    E* ukeys = static_cast<E*>(carve(p8, (size_t)n * sizeof(E)));
-    uint32_t* runs = static_cast<uint32_t*>(carve(p8, (size_t)n * 4));
+    E* ka = static_cast<E*>(carve(p8, ne));
+    E* kb = static_cast<E*>(carve(p8, ne));
+    uint32_t* pa = static_cast<uint32_t*>(carve(p8, n4));
+    uint32_t* pb = static_cast<uint32_t*>(carve(p8, n4));
+    uint32_t* ia = static_cast<uint32_t*>(carve(p8, n4));
+    uint32_t* ib = static_cast<uint32_t*>(carve(p8, n4));
+    uint32_t* flags = static_cast<uint32_t*>(carve(p8, n4));
+    uint32_t* ex = static_cast<uint32_t*>(carve(p8, n4));
+    uint32_t* starts = static_cast<uint32_t*>(carve(p8, n4));
     uint32_t* small = static_cast<uint32_t*>(carve(p8, 256));
-    void* tmp = carve(p8, temp);
     KMH_HIP(ctx, hipMemsetAsync(small, 0, 256, s));
     if (tb > ta) {
-        hipLaunchKernelGGL(k_sp_gather<E>, dim3((unsigned)(tb - ta)), dim3(256), 0, s, ent, toff, ldt, ta, tb,
-                           b, p, np, R, a, small);
+        hipLaunchKernelGGL((k_sp_gather<E, POS>), dim3((unsigned)(tb - ta)), dim3(256), 0, s, ent, epos, toff, ldt,
+                           ta, tb, b, p, np, R, ka, pa, small);
         KMH_HIP(ctx, hipGetLastError());
     }
     uint32_t m = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&m, small, 4, hipMemcpyDeviceToHost, s));
     KMH_HIP(ctx, hipStreamSynchronize(s));
     if (m == 0) return KMH_OK;
-    size_t t = temp;
-    KMH_HIP(ctx, hipcub::DeviceRadixSort::SortKeys(tmp, t, a, bsorted, (int)m, 0, R, s));
-    t = temp;
-    KMH_HIP(ctx, hipcub::DeviceRunLengthEncode::Encode(tmp, t, bsorted, ukeys, runs, small + 1, (int)m, s));
-    hipLaunchKernelGGL(k_sp_append<E>, dim3(1), dim3(256), 0, s, ukeys, runs, small + 1,
-                       (uint64_t)b << R, out_off, nk + g, codes, counts);
+    const unsigned gm = (m + 255u) / 256u;
+    bool alt = false;
+    E* keys = ka;
+    uint32_t* pos = pa;
+    if constexpr (POS) {
+        // by position (32 bits, indices as values), then the keys gathered in that order and sorted
+        // stably by key with their positions
+        hipLaunchKernelGGL(k_sp_iota, dim3(gm), dim3(256), 0, s, ia, m);
+        KMH_HIP(ctx, hipGetLastError());
+        rc = radix_sort_pairs<uint32_t>(ctx, pa, pb, ia, ib, m, 0, 32, &alt, s);
+        if (rc) return rc;
+        uint32_t* psorted = alt ? pb : pa;
+        uint32_t* isorted = alt ? ib : ia;
+        hipLaunchKernelGGL(k_sp_gather_by<E>, dim3(gm), dim3(256), 0, s, ka, isorted, m, kb);
+        KMH_HIP(ctx, hipGetLastError());
+        uint32_t* pother = alt ? pa : pb;
+        rc = radix_sort_pairs<E>(ctx, kb, ka, psorted, pother, m, 0, R, &alt, s);
+        if (rc) return rc;
+        keys = alt ? ka : kb;
+        pos = alt ? pother : psorted;
+    } else {
+        rc = radix_sort_pairs<E>(ctx, ka, kb, pa, pb, m, 0, R, &alt, s);
+        if (rc) return rc;
+        keys = alt ? kb : ka;
+        pos = alt ? pb : pa;
+    }
+    rc = run_starts<E>(ctx, keys, m, flags, ex, starts, small + 1, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_sp_append<E, POS>), dim3(1), dim3(256), 0, s, keys, pos, m, starts, small + 1,
+                       (uint64_t)b << R, out_off, nk + g, codes, counts, firsts);
     KMH_HIP(ctx, hipGetLastError());
     KMH_HIP(ctx, hipStreamSynchronize(s));
     return KMH_OK;
@@ -1060,11 +1212,11 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 
 namespace {
 
-template <typename E>
+template <typename E, bool POS>
 int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
-                          int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
-                          hipStream_t s) {
-    constexpr int kSpTile = Sp<E>::TILE, kCaps = Sp<E>::CAPS;
+                          int canonical, uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts,
+                          uint64_t* d_nkmers, hipStream_t s) {
+    constexpr int kSpTile = Sp<E, POS>::TILE, kCaps = Sp<E, POS>::CAPS;
     Layout L;
     int rc = make_layout(ctx, offsets, G, k, (uint64_t)kSpTile, L);
     if (rc) return rc;
@@ -1081,14 +1233,16 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
     const size_t tile_bytes = (size_t)kSpTile * sizeof(E);
     const size_t budget = env_mb("KMH_SP_BUDGET_MB", 16384) << 20;
     // Keys per count item (one pass of a bucket): the bin sort of k_sp_count stages at most
-    // Cnt<E>::CAP keys (8192 u32 / 4096 u64); the pass target leaves room for the spread of
-    // the pass sizes around it.
-    const uint32_t target = (uint32_t)std::max<long>(1, env_long("KMH_SP_TARGET", sizeof(E) == 4 ? 7680 : 3840));
+    // Cnt<E, POS>::CAP keys (8192 u32 / 4096 u64; half with positions); the pass target leaves
+    // room for the spread of the pass sizes around it.
+    const uint32_t target = (uint32_t)std::max<long>(
+        1, env_long("KMH_SP_TARGET", (sizeof(E) == 4 ? 7680 : 3840) / (POS ? 2 : 1)));
     const uint32_t split_target = (uint32_t)std::max<long>(1, std::min<long>(env_long("KMH_SP_SPLIT", 12288), kCaps));
     // KMH_SP_LIMIT caps the distinct keys of one item (tests force the fallback with it)
-    const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", Cnt<E>::CAP)),
-                                                    Cnt<E>::CAP);
-    // batches of whole genomes whose step-1 entries fit the budget (at most 2^18 tiles)
+    const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", Cnt<E, POS>::CAP)),
+                                                    Cnt<E, POS>::CAP);
+    // batches of whole genomes whose step-1 entries fit the budget (at most 2^20 tiles: toff rows;
+    // a genome always forms a batch of its own if it alone passes the budget)
     std::vector<std::pair<int, int>> batches;
     uint64_t max_tiles = 0;
     for (int g = 0; g < G;) {
@@ -1098,17 +1252,19 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             tiles += L.tbase[h + 1] - L.tbase[h];
             ++h;
         } while (h < G && (tiles + (L.tbase[h + 1] - L.tbase[h])) * tile_bytes <= budget &&
-                 tiles + (L.tbase[h + 1] - L.tbase[h]) <= (1u << 18));
+                 tiles + (L.tbase[h + 1] - L.tbase[h]) <= (1u << 20));
         batches.emplace_back(g, h);
         max_tiles = std::max(max_tiles, tiles);
         g = h;
     }
-    if (max_tiles > (1u << 18)) return fail(ctx, KMH_ERR_UNSUPPORTED, "genome too large for the sparse path");
+    if (max_tiles > (1u << 20)) return fail(ctx, KMH_ERR_UNSUPPORTED, "genome too large for the sparse path");
     const uint32_t ldt = (uint32_t)((max_tiles + 63) / 64 * 64);
     rc = ensure(ctx, ctx->sparse[2], std::max<uint64_t>(max_tiles, 1) * tile_bytes);
     if (!rc) rc = ensure(ctx, ctx->sparse[3], (size_t)ldt * (kSpBuckets + 1) * sizeof(uint16_t));
+    if (!rc && POS) rc = ensure(ctx, ctx->sparse[7], std::max<uint64_t>(max_tiles, 1) * (size_t)kSpTile * 4);
     if (rc) return rc;
     E* ent = static_cast<E*>(ctx->sparse[2].ptr);
+    uint32_t* epos = POS ? static_cast<uint32_t*>(ctx->sparse[7].ptr) : nullptr;
     uint16_t* toff = static_cast<uint16_t*>(ctx->sparse[3].ptr);
 
     // Experiment builds: KMH_SP_PROF=1 or 2 prints the host phases of every batch (2: without
@@ -1128,7 +1284,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         if (tiles == 0) continue;
         GenomeMap m{d_goff, d_tbase, g0, g1, L.tbase[g0], L.goff[G]};
         time_begin(ctx, s, "k_sp_partition");
-        launch_partition_k(k, canonical, (unsigned)tiles, s, d_seq, m, ent, toff, ldt);
+        launch_partition_k<E, POS>(k, canonical, (unsigned)tiles, s, d_seq, m, ent, epos, toff, ldt);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 
@@ -1156,13 +1312,15 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const size_t nsi = totals[0], nci = totals[1];
         if (nci == 0) continue;
         const double h2 = hprof ? now_ms() : 0.0;
-        // split output + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
+        // split output (+ positions) + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
         const size_t sbytes = nsi * (size_t)kCaps * sizeof(E);
+        const size_t pbytes = POS ? nsi * (size_t)kCaps * 4 : 0;
         const size_t t2bytes = (nsi * kT2 * 2 + 255) & ~(size_t)255;
-        rc = ensure(ctx, ctx->sparse[6], sbytes + t2bytes);
+        rc = ensure(ctx, ctx->sparse[6], sbytes + pbytes + t2bytes);
         if (rc) return rc;
         E* d_split = static_cast<E*>(ctx->sparse[6].ptr);
-        uint16_t* d_toff2 = reinterpret_cast<uint16_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes);
+        uint32_t* d_spos = POS ? reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes) : nullptr;
+        uint16_t* d_toff2 = reinterpret_cast<uint16_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes + pbytes);
         const size_t sib = (nsi * sizeof(SplitItem) + 255) & ~(size_t)255;
         const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
@@ -1180,15 +1338,15 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         time_begin(ctx, s, "k_sp_split");
-        hipLaunchKernelGGL(k_sp_split<E>, dim3((unsigned)nsi), dim3(kSpThreads), 0, s, ent, toff, ldt, d_sitems, R,
-                           d_split, d_toff2, d_gbfail);
+        hipLaunchKernelGGL((k_sp_split<E, POS>), dim3((unsigned)nsi), dim3(kSpThreads), 0, s, ent, epos, toff, ldt,
+                           d_sitems, R, d_split, d_spos, d_toff2, d_gbfail);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
         time_begin(ctx, s, "k_sp_count");
         const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
-        hipLaunchKernelGGL(k_sp_count<E>, dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_toff2, d_citems, (uint32_t)nci,
-                           R, limit, d_out_off, d_codes, d_counts, reinterpret_cast<unsigned long long*>(d_nkmers),
-                           d_gbfail, d_failed);
+        hipLaunchKernelGGL((k_sp_count<E, POS>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_toff2,
+                           d_citems, (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts, d_firsts,
+                           reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 #ifdef KMH_EXPERIMENTS
@@ -1231,9 +1389,9 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const double h4 = hprof ? now_ms() : 0.0;
         for (uint32_t id : ids) {
             const CountItem& it = citems[id];
-            rc = fallback_pass(ctx, it.g, it.b, it.p, it.np, it.n, ent, toff, ldt, L.tbase[it.g] - L.tbase[g0],
-                               L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
-                               reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, s);
+            rc = fallback_pass<E, POS>(ctx, it.g, it.b, it.p, it.np, it.n, ent, epos, toff, ldt,
+                                       L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
+                                       reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts, s);
             if (rc) return rc;
         }
         if (hprof)
@@ -1252,8 +1410,23 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
     if (k < 13 || k > 32) return fail(ctx, KMH_ERR_UNSUPPORTED, "device sparse counting needs 13 <= k <= 32");
     if (!d_seq || !d_codes || !d_counts || !d_nkmers) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
     // residues of 2k - 10 bits: u32 entries up to k = 21, u64 beyond
-    if (k <= 21) return sparse_count_dev_impl<uint32_t>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers, s);
-    return sparse_count_dev_impl<uint64_t>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers, s);
+    if (k <= 21)
+        return sparse_count_dev_impl<uint32_t, false>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, nullptr,
+                                                      d_nkmers, s);
+    return sparse_count_dev_impl<uint64_t, false>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, nullptr,
+                                                  d_nkmers, s);
+}
+
+int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, int canonical,
+                           uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts, uint64_t* d_nkmers,
+                           hipStream_t s) {
+    if (k < 13 || k > 32) return fail(ctx, KMH_ERR_UNSUPPORTED, "device sparse counting needs 13 <= k <= 32");
+    if (!d_seq || !d_codes || !d_counts || !d_firsts || !d_nkmers) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    if (k <= 21)
+        return sparse_count_dev_impl<uint32_t, true>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_firsts,
+                                                     d_nkmers, s);
+    return sparse_count_dev_impl<uint64_t, true>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_firsts,
+                                                 d_nkmers, s);
 }
 
 }  // namespace kmh

@@ -39,7 +39,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // device workspace
-    DevBuf seq, suf, toff, meta, out, out2, fix, redo, sparse[8], order;
+    DevBuf seq, suf, toff, meta, out, out2, fix, redo, sparse[8], order, sort_tmp, scan_tmp, first;
     // pinned staging for small host->device tables
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
@@ -123,6 +123,10 @@ int rows_decode_u4_range(Ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t 
 int sparse_count(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
                  std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
                  std::vector<uint64_t>& first, hipStream_t s);
+// 13 <= k <= 32: the same result through the device hash pipeline with positions (kmh_hash.hip).
+int sparse_count_first(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int canonical,
+                       std::vector<uint64_t>& codes, std::vector<uint32_t>& counts,
+                       std::vector<uint64_t>& first, hipStream_t s);
 // 33 <= k <= KMH_MAX_LONG_K, forward strand: sort by ceil(k / 32) code words (kmh_sparse.hip).
 int sparse_count_long(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, std::vector<uint64_t>& codes,
                       std::vector<uint32_t>& counts, std::vector<uint64_t>& first, hipStream_t s);
@@ -139,5 +143,28 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                      int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
                      hipStream_t s);
+// The same pipeline with every entry's window position carried along: d_firsts[i] (u32, relative
+// to the genome) = the first window start of k-mer i (the drop-in's first-occurrence order).
+int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, int canonical,
+                           uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts, uint64_t* d_nkmers,
+                           hipStream_t s);
+
+// ---- sort / scan / runs (kmh_sort.hip), n < 2^32 - 1 items ----
+// Stable LSD radix sort of (key, value) pairs on key bits [bit_lo, bit_hi), 8 bits per pass;
+// *result_in_alt: the sorted pairs ended in keys_alt / vals_alt (odd number of passes).
+template <typename K>
+int radix_sort_pairs(Ctx* ctx, K* keys, K* keys_alt, uint32_t* vals, uint32_t* vals_alt, uint64_t n, int bit_lo,
+                     int bit_hi, bool* result_in_alt, hipStream_t s);
+// out[i] = sum of in[0 .. i); *d_total (device, nullable) = the sum of all n (must fit 32 bits).
+int scan_exclusive_u32(Ctx* ctx, const uint32_t* d_in, uint32_t* d_out, uint64_t n, uint32_t* d_total,
+                       hipStream_t s);
+// Start index of every run of equal keys of a sorted array, in order; *d_nruns (device).
+// d_flags / d_ex: scratch of n u32 each.
+template <typename K>
+int run_starts(Ctx* ctx, const K* d_keys, uint64_t n, uint32_t* d_flags, uint32_t* d_ex, uint32_t* d_starts,
+               uint32_t* d_nruns, hipStream_t s);
+// Indices i with d_flags[i] != 0 (flags are 0 / 1), in order; *d_count (device).  d_ex: n u32 scratch.
+int select_flagged(Ctx* ctx, const uint32_t* d_flags, uint64_t n, uint32_t* d_ex, uint32_t* d_idx, uint32_t* d_count,
+                   hipStream_t s);
 
 }  // namespace kmh

@@ -272,6 +272,68 @@ def test_sparse_vs_oracle(ctx, oracle_lib, k, canonical):
     assert np.array_equal(first, wf[order])
 
 
+@pytest.mark.parametrize("k,target,limit", [(21, "37", "12288"), (21, "61", "9"), (27, "100000", "40"),
+                                            (17, "5000", "3")])
+def test_sparse_host_fallback_first_positions(ctx, oracle_lib, monkeypatch, k, target, limit):
+    """The drop-in's 13 <= k <= 32 path is the hash pipeline with window positions carried along:
+    capped tables push most passes into the hand-written sort fallback (sort by position, then
+    stably by key), which must give the same counts and first positions -- hence the same
+    first-occurrence order of k{k}.txt (generate.py:36,58) -- as the oracle.  Repeats make counts
+    > 1 and big bins (the count kernel's LDS hash table with its minimum position per slot)."""
+    rng = np.random.default_rng(900 + k)
+    unit = _rand_seq(rng, 5000, b"ACGTACGTacgt")
+    seq = np.concatenate([_rand_seq(rng, 200_000), np.tile(unit, 40), _rand_seq(rng, 90_000),
+                          np.tile(np.frombuffer(b"ACGTTGCAT", np.uint8), 4000)])
+    monkeypatch.setenv("KMH_SP_TARGET", target)
+    monkeypatch.setenv("KMH_SP_LIMIT", limit)
+    codes, counts, first = ctx.count(seq, k)
+    wc, wn, wf = oracle_lib.count_sparse(seq, k)
+    order = np.argsort(wf, kind="stable")
+    assert counts.max() >= 40
+    assert np.array_equal(first, wf[order])
+    assert np.array_equal(codes, wc[order])
+    assert np.array_equal(counts, wn[order])
+
+
+@pytest.mark.parametrize("k", [13, 21, 22, 32])
+def test_sparse_host_low_complexity(ctx, oracle_lib, k):
+    """poly-A, dinucleotide and short-period repeats through the drop-in path: at k = 32 the
+    u64 table slots overflow their count field and the passes go to the fallback."""
+    seq = np.concatenate([np.full(300_000, ord("A"), np.uint8), np.frombuffer(b"N", np.uint8),
+                          np.frombuffer(b"AC" * 150_000, np.uint8), np.frombuffer(b"acgttgacc" * 20_000, np.uint8)])
+    codes, counts, first = ctx.count(seq, k)
+    wc, wn, wf = oracle_lib.count_sparse(seq, k)
+    order = np.argsort(wf, kind="stable")
+    assert np.array_equal(first, wf[order])
+    assert np.array_equal(codes, wc[order]) and np.array_equal(counts, wn[order])
+
+
+def test_count_host_past_2_31_windows(ctx, oracle_lib):
+    """An organism of more than 2^31 windows at k = 21 (the reference's dict takes any length,
+    generate.py:36,58): a random 1,000,003-base unit repeated 2200 times (2.2 Gbases).  Window p
+    holds the k-mer of the circular unit at offset p mod U, so every k-mer's count is R times
+    its count over the U circular offsets, less its count over the k - 1 offsets past U - k (they
+    fit one copy fewer), and its first start is its first circular offset -- all from the
+    oracle's counts of the unit alone."""
+    U, R, k = 1_000_003, 2200, 21
+    unit = oracle_lib.synth(U, osynth.genome_seed(77))
+    seq = np.tile(unit, R)
+    assert seq.size - k + 1 > 2**31
+    codes, counts, first = ctx.count(seq, k)
+    del seq
+    circ = np.concatenate([unit, unit[:k - 1]])
+    cc, cn, cf = oracle_lib.count_sparse(circ, k)                       # U windows, offsets 0..U-1
+    tail = np.concatenate([unit[U - k + 1:], unit[:k - 1]])              # offsets U-k+1 .. U-1
+    tc, tn, _ = oracle_lib.count_sparse(tail, k)
+    want = cn.astype(np.int64) * R
+    want[np.searchsorted(cc, tc)] -= tn
+    order = np.argsort(cf, kind="stable")
+    assert np.array_equal(codes, cc[order])
+    assert np.array_equal(first, cf[order])
+    assert np.array_equal(counts.astype(np.int64), want[order])
+    assert int(counts.astype(np.int64).sum()) == U * R - k + 1
+
+
 @pytest.mark.parametrize("k", [33, 40, 63, 64, 65, 100])
 def test_long_kmers_vs_python_oracle(ctx, k):
     """k > 32 (the reference's dict takes any k): word-sorted on the GPU, first-occurrence
@@ -725,13 +787,14 @@ def test_count_genome_split(tmp_path, oracle_lib, backend, nproc):
 
 
 def test_count_host_size_limits(ctx):
-    """kmh_count_host rejects an organism past its limits before reading a byte (DESIGN.md 1
-    "Limits"; generate.py's docstring): 2^31 windows at k >= 13, 2^32 - 1 bytes at any k."""
+    """kmh_count_host rejects an organism of 2^32 - 1 bytes or more at any k before reading a
+    byte (DESIGN.md 1 "Limits"; generate.py's docstring).  2^31 windows and more are counted
+    (test_count_host_past_2_31_windows)."""
     import ctypes
     buf = np.zeros(64, np.uint8)      # the sizes below are claimed, never read
     out = ctypes.c_void_p()
     lib = _native.lib()
-    for n, k in ((2**31 + 20, 21), (2**31 + 12, 13), (2**32 - 1, 12), (2**32, 4)):
+    for n, k in ((2**32 - 1, 21), (2**32 - 1, 12), (2**32, 4), (2**33, 40)):
         rc = lib.kmh_count_host(ctx._h, ctypes.c_void_p(buf.ctypes.data), n, k, 0, ctypes.byref(out))
         assert rc == _native.KMH_ERR_UNSUPPORTED, (n, k, rc)
         assert not out.value
