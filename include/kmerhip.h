@@ -239,6 +239,20 @@ int64_t kmh_format_lines(int k, const uint64_t* codes, const uint64_t* counts, u
 int64_t kmh_format_lines_seq(int k, const uint8_t* seq, uint64_t seq_len, const uint64_t* first,
                              const uint64_t* counts, uint64_t n, char* out, uint64_t cap);
 
+/* ---- feature columns (device) ------------------------------------------------- */
+/* Replaces the per-row feature functions of /root/reference/kmerml/kmers/statistics.py:188-238
+ * (base counts, GC percent, CpG count and observed/expected ratio, Shannon entropy, dinucleotide
+ * repeat) for the labels of integer-parsed k{k}.txt lines: code i's label is the k-mer with its
+ * leading A's stripped ("A" for A...A; statistics.py:157, 248-273).  n codes (d_codes, or NULL for
+ * all codes 0 .. n - 1); all arrays are DEVICE arrays of n entries except d_cnt (4 x n: the A, C,
+ * G, T counts, base-major), d_order (625 x 4 int32: for the first-appearance pattern key of a
+ * label, the bases in the order Python's set() iterates them, -1-padded; computed by the caller's
+ * interpreter) and d_lg ((k + 1) x (k + 1) doubles: math.log2(n / L) at [n][L]).  Every float64 is
+ * the reference's operation sequence, rounded once per operation (no fused multiply-add). */
+int kmh_feature_columns_dev(kmh_ctx* ctx, const uint64_t* d_codes, uint64_t n, int k, const int32_t* d_order,
+                            const double* d_lg, int64_t* d_cnt, int64_t* d_cpg, int64_t* d_rep, double* d_gc,
+                            double* d_oe, double* d_ent, void* stream);
+
 /* ---- feature CSV text (host) --------------------------------------------------- */
 /* Replaces pandas' DataFrame.to_csv(index=False) of the per-organism feature table
  * (/root/reference/kmerml/kmers/statistics.py:136-144): the rows of a block of columns as CSV

@@ -311,6 +311,16 @@ int kmh_rows_decode_u4_range_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t row
                                      pick_stream(ctx, stream));
 }
 
+int kmh_feature_columns_dev(kmh_ctx* ctx, const uint64_t* d_codes, uint64_t n, int k, const int32_t* d_order,
+                            const double* d_lg, int64_t* d_cnt, int64_t* d_cpg, int64_t* d_rep, double* d_gc,
+                            double* d_oe, double* d_ent, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return kmh::feature_columns(ctx, d_codes, n, k, d_order, d_lg, d_cnt, d_cpg, d_rep, d_gc, d_oe, d_ent,
+                                pick_stream(ctx, stream));
+}
+
 // Host sequence -> device (padded with one non-base byte so loads past the end are safe).
 static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t** d_seq) {
     int rc = kmh::ensure(ctx, ctx->seq, (size_t)n + 64);

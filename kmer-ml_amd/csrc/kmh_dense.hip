@@ -390,7 +390,14 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     // 4. write the tile out
     uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)CAP);
     const uint4* src = reinterpret_cast<const uint4*>(stage);
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
+    // A/B only (counts wrong): store all but every KMH_EXCH_CUT-th chunk, the bytes a denser
+    // exchange code would save, without its coding work
+    for (uint32_t c = tid; c < (total >> 3); c += kPThreads)
+        if (c % KMH_EXCH_CUT != KMH_EXCH_CUT - 1) store_nt(&dst[c], src[c]);
+#else
     for (uint32_t c = tid; c < (total >> 3); c += kPThreads) store_nt(&dst[c], src[c]);
+#endif
 }
 
 // ---------------------------------------------------------------- k >= 10: count
@@ -556,6 +563,12 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             if (total <= (uint32_t)QMAX) {
                 const uint32_t ex = incl - nc;
                 for (uint32_t j = 0; j < nc; ++j) q[ex + j] = (crel + j) | ((j + 1 == nc ? nlast - 1u : 7u) << 20);
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
+                // A/B only: the chunks k_partition skipped are queued as re-reads of the segment's
+                // first chunk (an L2 hit), so the count reads the fewer bytes with unchanged LDS work
+                for (uint32_t j = 0; j < nc; ++j)
+                    if ((c0 + j) % KMH_EXCH_CUT == KMH_EXCH_CUT - 1) q[ex + j] = (q[ex + j] & ~0xFFFFFu) | crel;
+#endif
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -599,6 +599,16 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
         citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, s0, s1, (uint32_t)gb, n};
 }
 
+// Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel).
+#ifndef KMH_SP_NT_OUT
+#define KMH_SP_NT_OUT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void out_store(T* p, T v) {
+    if constexpr (KMH_SP_NT_OUT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Count work item: deduplication by a counting sort on the key's position inside its pass.
 // The keys of pass p of a bucket are the residues r with floor(r * np / 2^R) = p, so
 // (r * np) mod 2^R is increasing in r and spread evenly over [0, 2^R): its top 13 bits give
@@ -1010,8 +1020,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint64_t m = __ballot(f);
             if (f) {
                 const uint64_t o = at + run + (uint32_t)__popcll(m & below);
-                codes[o] = hib | (uint64_t)ek[jj];
-                counts[o] = ec[jj];
+                out_store(codes + o, hib | (uint64_t)ek[jj]);
+                out_store(counts + o, ec[jj]);
                 if constexpr (POS) firsts[o] = ef[jj];
             }
             run += (uint32_t)__popcll(m);

@@ -149,6 +149,11 @@ int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offse
                            uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts, uint64_t* d_nkmers,
                            hipStream_t s);
 
+// ---- feature columns of the feature CSV (kmh_features.hip) ----
+int feature_columns(Ctx* ctx, const uint64_t* d_codes, uint64_t n, int k, const int32_t* d_order, const double* d_lg,
+                    int64_t* d_cnt, int64_t* d_cpg, int64_t* d_rep, double* d_gc, double* d_oe, double* d_ent,
+                    hipStream_t s);
+
 // ---- sort / scan / runs (kmh_sort.hip), n < 2^32 - 1 items ----
 // Stable LSD radix sort of (key, value) pairs on key bits [bit_lo, bit_hi), 8 bits per pass;
 // *result_in_alt: the sorted pairs ended in keys_alt / vals_alt (odd number of passes).

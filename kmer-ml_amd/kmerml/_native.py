@@ -67,6 +67,7 @@ SIGNATURES = [
                                                 _vp, _vp]),
     ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
                                           _u64, _vp, _vp]),
+    ("kmh_feature_columns_dev", _c.c_int, [_vp, _vp, _u64, _c.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("kmh_csv_format", _c.c_int, [_c.c_int, _vp, _vp, _vp, _u64, _c.c_int, _c.POINTER(_vp)]),
     ("kmh_text_data", _c.c_int, [_vp, _c.POINTER(_vp), _u64p]),
     ("kmh_text_free", None, [_vp]),
@@ -252,6 +253,14 @@ class Context:
                                                   ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
                                                   int(row0), int(nrows), ctypes.c_void_p(d_rows),
                                                   ctypes.c_void_p(stream) if stream else None), self._h)
+
+    # -- feature columns (device pointers; statistics.py:188-238) --
+    def feature_columns_dev(self, d_codes, n, k, d_order, d_lg, d_cnt, d_cpg, d_rep, d_gc, d_oe, d_ent, stream=None):
+        _check(lib().kmh_feature_columns_dev(self._h, ctypes.c_void_p(d_codes) if d_codes else None, int(n), int(k),
+                                             ctypes.c_void_p(d_order), ctypes.c_void_p(d_lg), ctypes.c_void_p(d_cnt),
+                                             ctypes.c_void_p(d_cpg), ctypes.c_void_p(d_rep), ctypes.c_void_p(d_gc),
+                                             ctypes.c_void_p(d_oe), ctypes.c_void_p(d_ent),
+                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- kernel timing --
     def timing(self, enable):

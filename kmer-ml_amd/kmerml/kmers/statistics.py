@@ -346,14 +346,71 @@ def feature_table(k):
     return table
 
 
+def _order_lut():
+    """625 x 4 int32: for the first-appearance pattern key of a label (present bases A0 C1 G2 T3
+    in order of first appearance, as base-5 digits b + 1, absent ones 0), the bases in the order
+    this interpreter's set() iterates them (-1-padded)."""
+    from itertools import permutations
+    lut = np.full((625, 4), -1, dtype=np.int32)
+    letters = 'ACGT'
+    for m in range(1, 5):
+        for pat in permutations(range(4), m):
+            key = 0
+            for r in range(4):
+                key = key * 5 + (pat[r] + 1 if r < m else 0)
+            seq = [letters.index(ch) for ch in _entropy_order(''.join(letters[b] for b in pat))]
+            lut[key, :len(seq)] = seq
+    return lut
+
+
+def _log2_table(k):
+    """(k + 1) x (k + 1) float64: math.log2(n / L) at [n][L] (the reference's log2 of each prob)."""
+    lg = np.zeros((k + 1, k + 1), dtype=np.float64)
+    for L in range(1, k + 1):
+        for n in range(1, L + 1):
+            lg[n, L] = math.log2(n / L)
+    return lg
+
+
+def _code_features_hip(k, codes):
+    """_code_features on the HIP device: one thread per code (kmh_feature_columns_dev,
+    csrc/kmh_features.hip), the same operations rounded once each."""
+    import torch
+
+    from kmerml import _native
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = (1 << (2 * k)) if codes is None else len(codes)
+    d_codes = None if codes is None else torch.from_numpy(np.ascontiguousarray(codes, dtype=np.int64)).to(dev)
+    d_order = torch.from_numpy(_order_lut()).to(dev)
+    d_lg = torch.from_numpy(_log2_table(k)).to(dev)
+    cnt = torch.empty((4, n), dtype=torch.int64, device=dev)
+    cpg = torch.empty(n, dtype=torch.int64, device=dev)
+    rep = torch.empty(n, dtype=torch.int64, device=dev)
+    gc = torch.empty(n, dtype=torch.float64, device=dev)
+    oe = torch.empty(n, dtype=torch.float64, device=dev)
+    ent = torch.empty(n, dtype=torch.float64, device=dev)
+    ctx = _native.context(dev.index)
+    ctx.feature_columns_dev(d_codes.data_ptr() if d_codes is not None else None, n, k, d_order.data_ptr(),
+                            d_lg.data_ptr(), cnt.data_ptr(), cpg.data_ptr(), rep.data_ptr(), gc.data_ptr(),
+                            oe.data_ptr(), ent.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    cnt = cnt.cpu().numpy()
+    return {'A_count': cnt[0], 'C_count': cnt[1], 'G_count': cnt[2], 'T_count': cnt[3],
+            'cpg_count': cpg.cpu().numpy(), 'has_repeat': rep.cpu().numpy(), 'gc_percent': gc.cpu().numpy(),
+            'cpg_obs_exp': oe.cpu().numpy(), 'shannon_entropy': ent.cpu().numpy()}
+
+
 def _code_features(k, codes):
     """statistics.py:188-238 for the compat labels of `codes` (None: all 4^k codes).  Same
     IEEE operations as the reference, per value: gc = (g + c) / L * 100; expected =
     c / L * (g / L) * (L - 1); entropy summed in set(kmer) order (_entropy_order per
-    first-appearance pattern) with math.log2 of the same quotients."""
+    first-appearance pattern) with math.log2 of the same quotients.  On a HIP device the
+    hand-written kernel computes them (_code_features_hip); on a host without one, torch on
+    the CPU (this consumer of the k-mer files is a CPU program in the reference)."""
     import torch
 
-    dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+    if torch.cuda.is_available():
+        return _code_features_hip(k, codes)
+    dev = torch.device("cpu")
     i64 = torch.int64
     if codes is None:
         c = torch.arange(1 << (2 * k), dtype=i64, device=dev)
@@ -388,28 +445,13 @@ def _code_features(k, codes):
     expected = torch.where(prod > 0, prod * (Lf - 1), torch.full_like(prod, 0.001))
     out['cpg_obs_exp'] = torch.where(expected > 0, cpg.to(torch.float64) / expected, torch.zeros_like(prod))
     # entropy: first-appearance pattern -> the set order of this interpreter
-    letters = 'ACGT'
     key = torch.zeros_like(c)
     order_rank = torch.stack(first).argsort(dim=0, stable=True)      # letters by first position
     present_sorted = torch.stack(first).gather(0, order_rank) < (1 << 20)
     for r in range(4):
         key = key * 5 + torch.where(present_sorted[r], order_rank[r] + 1, torch.zeros_like(c))
-    keys = torch.unique(key).tolist()
-    lut_order = torch.full((625, 4), -1, dtype=i64)
-    for kv in keys:
-        ds, x = [], kv
-        for _ in range(4):
-            ds.append(x % 5)
-            x //= 5
-        pat = ''.join(letters[d - 1] for d in reversed(ds) if d)
-        seq = [letters.index(ch) for ch in _entropy_order(pat)]
-        lut_order[kv, :len(seq)] = torch.tensor(seq, dtype=i64)
-    lut_order = lut_order.to(dev)
-    lg = torch.zeros((k + 1, k + 1), dtype=torch.float64)               # log2(n / L) as math.log2
-    for L in range(1, k + 1):
-        for n in range(1, L + 1):
-            lg[n, L] = math.log2(n / L)
-    lg = lg.to(dev)
+    lut_order = torch.from_numpy(_order_lut().astype(np.int64)).to(dev)
+    lg = torch.from_numpy(_log2_table(k)).to(dev)
     cnt_t = torch.stack(cnt)
     ent = torch.zeros_like(Lf)
     for r in range(4):

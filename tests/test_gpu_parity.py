@@ -955,6 +955,34 @@ def test_feature_table_on_gpu():
             assert np.array_equal(got, want), name
 
 
+@pytest.mark.parametrize("k", [1, 4, 12, 15, 19])
+def test_feature_columns_hip_kernel(k):
+    """kmh_feature_columns_dev (csrc/kmh_features.hip: one thread per code, the reference's
+    float64 operations rounded once each, the entropy in this interpreter's set() order) equals
+    label_features on the same compat labels bit for bit: every code for k <= 4, random codes
+    (with A...A, T...T and leading-A codes) at larger k.  Reference anchor: statistics.py:188-238."""
+    from kmerml.kmers import statistics as st
+    rng = np.random.default_rng(70 + k)
+    if k <= 4:
+        codes = np.arange(4 ** k, dtype=np.int64)
+    else:
+        codes = rng.integers(0, 4 ** k, 20_000, dtype=np.int64)
+        codes[:4] = [0, 4 ** k - 1, 1, 4 ** (k - 3) + 6]
+    got = st._code_features_hip(k, codes)
+    labels = []
+    for c in codes.tolist():
+        s = "".join("ACGT"[(c >> (2 * (k - 1 - i))) & 3] for i in range(k)).lstrip("A") or "A"
+        labels.append(s)
+    want = st.label_features(labels)
+    for name, w in want.items():
+        w = np.asarray(w)
+        g = got[name]
+        if w.dtype.kind == "f":
+            assert np.array_equal(g.view(np.int64), w.view(np.int64)), (k, name)
+        else:
+            assert np.array_equal(g, w), (k, name)
+
+
 def _synth_row(oracle_lib, g, L=100_000_000, k=12, repeat=None):
     seq = oracle_lib.synth(L, osynth.genome_seed(g))
     if repeat:
