@@ -395,6 +395,9 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     // exchange code would save, without its coding work
     for (uint32_t c = tid; c < (total >> 3); c += kPThreads)
         if (c % KMH_EXCH_CUT != KMH_EXCH_CUT - 1) store_nt(&dst[c], src[c]);
+#elif defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_PLAIN)
+    // A/B only: plain stores (the lines may stay in the Infinity Cache for the count kernel)
+    for (uint32_t c = tid; c < (total >> 3); c += kPThreads) dst[c] = src[c];
 #else
     for (uint32_t c = tid; c < (total >> 3); c += kPThreads) store_nt(&dst[c], src[c]);
 #endif

@@ -14,6 +14,8 @@
 namespace kmh {
 namespace {
 
+// Plain operators under this pragma (not the __d*_rn helpers of the HIP headers, whose
+// inlined multiply and subtract the default contraction may still fuse into one FMA).
 #pragma clang fp contract(off)
 
 __global__ __launch_bounds__(256) void k_features(const uint64_t* __restrict__ codes, uint64_t n, int k,
@@ -40,11 +42,11 @@ __global__ __launch_bounds__(256) void k_features(const uint64_t* __restrict__ c
     }
     const double L = (double)m;
     // statistics.py:196: (gc_count / len(kmer)) * 100
-    gc_out[i] = __dmul_rn(__ddiv_rn((double)(cnt[2] + cnt[1]), L), 100.0);
+    gc_out[i] = ((double)(cnt[2] + cnt[1]) / L) * 100.0;
     // statistics.py:205-212: c_freq * g_freq * (len - 1), 0.001 when the product is 0
-    const double prod = __dmul_rn(__ddiv_rn((double)cnt[1], L), __ddiv_rn((double)cnt[2], L));
-    const double expected = prod > 0.0 ? __dmul_rn(prod, L - 1.0) : 0.001;
-    oe_out[i] = expected > 0.0 ? __ddiv_rn((double)cpg, expected) : 0.0;
+    const double prod = ((double)cnt[1] / L) * ((double)cnt[2] / L);
+    const double expected = prod > 0.0 ? prod * (L - 1.0) : 0.001;
+    oe_out[i] = expected > 0.0 ? (double)cpg / expected : 0.0;
     // first-appearance pattern of the present bases -> set() iteration order (table row)
     int rank[4] = {0, 1, 2, 3};
     for (int a = 1; a < 4; ++a)   // stable sort of the bases by first position
@@ -60,8 +62,9 @@ __global__ __launch_bounds__(256) void k_features(const uint64_t* __restrict__ c
         const int b = order[key * 4 + r];
         if (b < 0) break;
         const int nb = cnt[b];
-        const double p = __ddiv_rn((double)nb, L);
-        ent = __dsub_rn(ent, __dmul_rn(p, lg[nb * (k + 1) + m]));   // entropy -= prob * log2(prob)
+        const double p = (double)nb / L;
+        const double term = p * lg[nb * (k + 1) + m];
+        ent = ent - term;                                             // entropy -= prob * log2(prob)
     }
     ent_out[i] = ent;
     for (int b = 0; b < 4; ++b) cnt_out[(uint64_t)b * n + i] = cnt[b];
