@@ -390,12 +390,7 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     // 4. write the tile out
     uint4* dst = reinterpret_cast<uint4*>(suf + lt * (uint64_t)CAP);
     const uint4* src = reinterpret_cast<const uint4*>(stage);
-#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
-    // A/B only (counts wrong): store all but every KMH_EXCH_CUT-th chunk, the bytes a denser
-    // exchange code would save, without its coding work
-    for (uint32_t c = tid; c < (total >> 3); c += kPThreads)
-        if (c % KMH_EXCH_CUT != KMH_EXCH_CUT - 1) store_nt(&dst[c], src[c]);
-#elif defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_PLAIN)
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_PLAIN)
     // A/B only: plain stores (the lines may stay in the Infinity Cache for the count kernel)
     for (uint32_t c = tid; c < (total >> 3); c += kPThreads) dst[c] = src[c];
 #else
@@ -556,7 +551,14 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         uint64_t tw = ta + (uint64_t)wave * BT;
         if (tw < tb) bounds(tw, lo_n, hi_n);
         for (; tw < tb; tw += (uint64_t)NW * BT) {
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
+            // A/B only (counts wrong): read only the first (KMH_EXCH_CUT - 1) / KMH_EXCH_CUT of
+            // every segment's chunks -- fewer bytes AND fewer LDS adds: an upper bound on what a
+            // denser exchange code could save in this kernel
+            const uint32_t c0 = lo_n & 0xFFFu, nc0 = (hi_n & 0xFFFu) - c0, nc = nc0 - nc0 / KMH_EXCH_CUT;
+#else
             const uint32_t c0 = lo_n & 0xFFFu, nc = (hi_n & 0xFFFu) - c0;
+#endif
             const uint32_t nlast = 8u - (lo_n >> 12);
             ent += nc ? 8u * nc - (lo_n >> 12) : 0u;
             const uint32_t incl = scan64(nc);
@@ -566,12 +568,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             if (total <= (uint32_t)QMAX) {
                 const uint32_t ex = incl - nc;
                 for (uint32_t j = 0; j < nc; ++j) q[ex + j] = (crel + j) | ((j + 1 == nc ? nlast - 1u : 7u) << 20);
-#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
-                // A/B only: the chunks k_partition skipped are queued as re-reads of the segment's
-                // first chunk (an L2 hit), so the count reads the fewer bytes with unchanged LDS work
-                for (uint32_t j = 0; j < nc; ++j)
-                    if ((c0 + j) % KMH_EXCH_CUT == KMH_EXCH_CUT - 1) q[ex + j] = (q[ex + j] & ~0xFFFFFu) | crel;
-#endif
+
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -632,6 +629,11 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     // make it a k_reencode bucket) and widens again.  With split rows (S > 1, added with
     // atomics) the table is checked before it is widened.  One call site of each walk (a
     // third inlined copy made the compiler spill to scratch).
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
+    constexpr bool kCheck = false;   // A/B only: no exactness check (the cut exchange counts garbage)
+#else
+    constexpr bool kCheck = true;
+#endif
     const bool post = S == 1;   // uniform
     bool exact = false, enc = false;
     constexpr uint32_t kStage = (uint32_t)(NW * QMAX) / 2;   // (index, value) pairs
@@ -645,7 +647,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             walk(std::true_type{});
         }
         __syncthreads();
-        if (!post && !exact) {
+        if (kCheck && !post && !exact) {
             uint32_t hs0 = 0u;
             for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) hs0 += halves(tbl4[i]);
             add_hsum(hs0);
@@ -700,7 +702,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
                     if (e[j]) atomicAdd(&orow[8 * i + j], e[j]);
             }
         }
-        if (post && !exact) {   // uniform
+        if (kCheck && post && !exact) {   // uniform
             add_hsum(hs);
             lds_barrier();   // not __syncthreads(): the slice's stores drain behind it
             if (hsum != (unsigned long long)nent) {

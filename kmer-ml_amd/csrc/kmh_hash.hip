@@ -601,7 +601,7 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
 
 // Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel).
 #ifndef KMH_SP_NT_OUT
-#define KMH_SP_NT_OUT 0
+#define KMH_SP_NT_OUT 1   // non-temporal: 42.9 -> 42.5 ms per config-5 step (profiles/r03/r03c_ab_nt.txt)
 #endif
 template <typename T>
 __device__ __forceinline__ void out_store(T* p, T v) {
