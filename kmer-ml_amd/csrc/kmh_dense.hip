@@ -18,6 +18,7 @@
 // "ACGT" only).  Any other byte -- including the '\n' the host puts between records and
 // bytes past a genome's end -- breaks windows, so windows never span records or genomes.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "kmh_device.h"
@@ -496,6 +497,14 @@ constexpr int batch_tiles(int qmax) {
 // queue (chunk index relative to the batch, entries used in the chunk) and streams the queue
 // with all 64 lanes active: U loads in flight per lane, 8 LDS adds per load.  A batch whose
 // chunks overflow the queue (skewed input) is walked lane by lane instead.
+#ifdef KMH_EXPERIMENTS
+// KMH_DENSE_PROF: per-phase clocks of k_bucket_count summed over its waves (lane 0 of each)
+__device__ unsigned long long g_dense_prof[8];
+#define KMH_DP(i) if ((threadIdx.x & 63) == 0) { const unsigned long long t_ = clock64(); atomicAdd(&g_dense_prof[i], t_ - tl_); tl_ = t_; }
+#else
+#define KMH_DP(i)
+#endif
+
 template <int K, int U, bool ENC>
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint16_t* __restrict__ suf, const uint16_t* __restrict__ toff, uint32_t ldt, GenomeMap m,
@@ -523,6 +532,9 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint4* chunks = reinterpret_cast<const uint4*>(suf);
     const uint64_t row0 = (uint64_t)g * (1ull << (2 * K)) + (uint64_t)b * kCBins;
 
+#ifdef KMH_EXPERIMENTS
+    unsigned long long tl_ = clock64();
+#endif
     uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
     for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
     if (threadIdx.x == 0) {
@@ -532,6 +544,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         hsum = 0ull;
     }
     __syncthreads();
+    KMH_DP(0)
 
     uint32_t* q = queue[wave];
     // segment of this lane's tile in batch tw: first chunk, chunks, entries in the last chunk
@@ -604,6 +617,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     // bucket's entries; otherwise the bucket is counted again with returning adds, which log
     // every wrap (skewed genomes only: uniform 100 Mbp genomes stay below 65536 per bin).
     const uint32_t ent = walk(std::false_type{});
+    KMH_DP(1)
     {
         uint32_t e = ent;
 #pragma unroll
@@ -636,6 +650,10 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
 #endif
     const bool post = S == 1;   // uniform
     bool exact = false, enc = false;
+#ifdef KMH_EXPERIMENTS
+    __syncthreads();
+    KMH_DP(2)
+#endif
     constexpr uint32_t kStage = (uint32_t)(NW * QMAX) / 2;   // (index, value) pairs
     uint32_t* stage = &queue[0][0];
     for (;;) {
@@ -702,6 +720,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
                     if (e[j]) atomicAdd(&orow[8 * i + j], e[j]);
             }
         }
+        KMH_DP(3)
         if (kCheck && post && !exact) {   // uniform
             add_hsum(hs);
             lds_barrier();   // not __syncthreads(): the slice's stores drain behind it
@@ -712,6 +731,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         }
         break;
     }
+    KMH_DP(4)
     if (ENC) {
         __syncthreads();
         if (ecnt > kStage) enc = false;                            // uniform
@@ -924,6 +944,19 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
                                s, suf, toff, ldt, m, S, d_out, fl, U4Out{});
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
+#ifdef KMH_EXPERIMENTS
+        if (env_long("KMH_DENSE_PROF", 0)) {
+            unsigned long long hp[8];
+            KMH_HIP(ctx, hipStreamSynchronize(s));
+            KMH_HIP(ctx, hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_dense_prof), sizeof(hp)));
+            const double waves = (double)nG * NBK * S * (kCountThreads / 64);
+            std::fprintf(stderr, "k_bucket_count per wave (kcycles): zero %.1f | walk %.1f | sum+barrier %.1f | "
+                         "widen+stores %.1f | check+barrier %.1f  (%d genomes)\n", hp[0] / waves / 1e3,
+                         hp[1] / waves / 1e3, hp[2] / waves / 1e3, hp[3] / waves / 1e3, hp[4] / waves / 1e3, nG);
+            const unsigned long long z[8] = {};
+            KMH_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_dense_prof), z, sizeof(z)));
+        }
+#endif
         g = h;
     }
     time_begin(ctx, s, "k_fixup");

@@ -43,7 +43,10 @@ constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
-constexpr int kQU = 4;                     // chunk loads in flight per lane
+#ifndef KMH_SP_QU
+#define KMH_SP_QU 4
+#endif
+constexpr int kQU = KMH_SP_QU;             // chunk loads in flight per lane (split kernel)
 
 // Entry width: u32 residues (k <= 21) or u64 (22 <= k <= 32).  A u64 tile holds half the windows,
 // so a tile's entries (128 KiB) and a split item's staging (80 KiB) keep their LDS size.
@@ -645,7 +648,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
     constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E, POS>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
     constexpr int BQ = BPT / 4;   // uint4 words of a thread's bins
-    constexpr int kCaps = Sp<E, POS>::CAPS, U = 4;
+#ifndef KMH_SP_CU
+#define KMH_SP_CU 4
+#endif
+    constexpr int kCaps = Sp<E, POS>::CAPS, U = KMH_SP_CU;
     constexpr bool WIDE = sizeof(E) == 8;
     static_assert(BPT % 4 == 0 && HPT >= 1 && C % NT == 0, "thread layout");
     __shared__ __attribute__((aligned(16))) uint32_t hist[kBins];
