@@ -478,6 +478,10 @@ __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv,
     }
 }
 
+#ifndef KMH_COUNT_DYN
+#define KMH_COUNT_DYN 1   // 1.90 -> 1.76 ms per config-3 count launch (profiles/r03/ab/r03o_*)
+#endif
+
 // Tiles per wave batch: the expected chunks of a batch must fit the wave's queue of qmax
 // entries (a batch that overflows it is walked lane by lane).
 template <int K>
@@ -520,6 +524,9 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     __shared__ uint32_t queue[NW][QMAX];     // chunk queues; escape staging of the epilogue
     __shared__ uint32_t wrapped, ecnt, ebase, nent;
     __shared__ unsigned long long hsum;
+#if KMH_COUNT_DYN
+    __shared__ unsigned long long nextb;     // the next unclaimed tile batch
+#endif
 
     const uint32_t w = xcd_work_id();
     const int s = (int)(w % (uint32_t)S);
@@ -542,6 +549,9 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         ecnt = 0u;
         nent = 0u;
         hsum = 0ull;
+#if KMH_COUNT_DYN
+        nextb = ta;
+#endif
     }
     __syncthreads();
     KMH_DP(0)
@@ -549,9 +559,9 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     uint32_t* q = queue[wave];
     // segment of this lane's tile in batch tw: first chunk, chunks, entries in the last chunk
     // (prefetched one batch ahead)
-    auto bounds = [&](uint64_t tw, uint32_t& lo, uint32_t& hi) {
+    auto bounds = [&](uint64_t tw, uint32_t g, uint32_t& lo, uint32_t& hi) {
         const uint64_t t = tw + (uint64_t)lane;
-        const bool in = lane < BT && t < tb;
+        const bool in = (uint32_t)lane < g && t < tb;
         lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
         hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
     };
@@ -561,9 +571,39 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         constexpr bool EX = decltype(exact)::value;
         uint32_t ent = 0u;
         uint32_t lo_n = 0, hi_n = 0;
+#if KMH_COUNT_DYN
+        // batches claimed from an LDS cursor as the waves get to them, so that the waves of the
+        // workgroup finish together (a static round robin left them waiting at the barrier);
+        // guided: a batch shrinks towards the end of the bucket (at least 4 tiles)
+        auto grab = [&](uint32_t& g) -> uint64_t {
+            unsigned long long t = 0;
+            uint32_t gg = (uint32_t)BT;
+            if (lane == 0) {
+                if (KMH_COUNT_DYN == 2) {
+                    const unsigned long long cur = __hip_atomic_load(&nextb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint64_t left = cur < tb ? tb - cur : 0;
+                    const uint64_t want = (left + 2 * NW - 1) / (2 * NW);
+                    gg = (uint32_t)(want < 4 ? 4 : (want > (uint64_t)BT ? (uint64_t)BT : want));
+                }
+                t = atomicAdd(&nextb, (unsigned long long)gg);
+            }
+            g = (uint32_t)__builtin_amdgcn_readfirstlane((int)gg);
+            return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(t >> 32)) << 32);
+        };
+        uint32_t gcur = BT, gnext = BT;
+        uint64_t tw = grab(gcur);
+#else
+        const uint32_t gcur = BT, gnext = BT;
         uint64_t tw = ta + (uint64_t)wave * BT;
-        if (tw < tb) bounds(tw, lo_n, hi_n);
-        for (; tw < tb; tw += (uint64_t)NW * BT) {
+#endif
+        if (tw < tb) bounds(tw, gcur, lo_n, hi_n);
+        for (uint64_t tnext; tw < tb; tw = tnext) {
+#if KMH_COUNT_DYN
+            tnext = grab(gnext);
+#else
+            tnext = tw + (uint64_t)NW * BT;
+#endif
 #if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
             // A/B only (counts wrong): read only the first (KMH_EXCH_CUT - 1) / KMH_EXCH_CUT of
             // every segment's chunks -- fewer bytes AND fewer LDS adds: an upper bound on what a
@@ -595,7 +635,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
 #pragma unroll
                 for (int u = 0; u < U; ++u) v[u] = chunks[cbat + (qe[u] & 0xFFFFFu)];
                 // next batch's bounds load behind this batch's data loads
-                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+                if (tnext < tb) bounds(tnext, gnext, lo_n, hi_n);
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if ((uint32_t)(u * 64 + lane) < total)
@@ -604,7 +644,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             } else {
-                if (tw + (uint64_t)NW * BT < tb) bounds(tw + (uint64_t)NW * BT, lo_n, hi_n);
+                if (tnext < tb) bounds(tnext, gnext, lo_n, hi_n);
                 for (uint32_t j = 0; j < nc; ++j)
                     count_chunk<EX>(tbl, chunks[cbat + crel + j], j + 1 == nc ? nlast : 8u, L, row0, &wrapped);
             }
@@ -659,7 +699,12 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     for (;;) {
         if (exact) {
             __syncthreads();
-            if (threadIdx.x == 0) ecnt = 0u;   // the first widening's staged escapes are dropped
+            if (threadIdx.x == 0) {
+                ecnt = 0u;   // the first widening's staged escapes are dropped
+#if KMH_COUNT_DYN
+                nextb = ta;
+#endif
+            }
             for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
             __syncthreads();
             walk(std::true_type{});
