@@ -118,17 +118,20 @@ struct Bases {
     uint64_t inv;      // bit 63 = base 0 is not ACGT (or lies past the genome end)
 };
 
-template <bool FAST>
-__device__ __forceinline__ Bases load_bases(const uint8_t* __restrict__ seq, uint64_t base,
-                                            uint64_t gend) {
-    uint4 v[4];
-    if constexpr (FAST) {
+// The 64 bytes behind a thread's windows: 16-byte loads inside the data, byte loads (0 past
+// gend) in the last tile of the data.
+__device__ __forceinline__ void load_raw(const uint8_t* __restrict__ seq, uint64_t base, uint64_t gend, bool fast,
+                                         uint4 (&v)[4]) {
+    if (fast) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const uint4*>(seq + base + 16 * q);
     } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = load16(seq, base + 16 * q, gend);
     }
+}
+
+__device__ __forceinline__ Bases encode_bases(const uint4 (&v)[4], uint64_t base, uint64_t gend) {
     uint32_t c[4], i[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -170,13 +173,19 @@ __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
     }
 }
 
+// Persistent, one workgroup per CU (132 KiB of LDS).  XCD x (= blockIdx % 8) takes a contiguous
+// run of the tiles, so the u16 offsets its workgroups write side by side share L2 lines, and its
+// workgroups stride through that run.  Each tile's 64 bytes per thread are loaded behind the
+// previous tile's LDS work, and each tile's entries drain behind the next tile's: the barriers
+// wait for LDS operations only (lds_barrier), and the one wait for memory -- the next tile's
+// bytes, encoded before this tile's stores are issued -- comes after a tile of LDS work.
 template <int K, int CANON, typename E, bool POS>
 __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __restrict__ seq,
                                                              GenomeMap m,
                                                              E* __restrict__ ent,
                                                              uint32_t* __restrict__ epos,
                                                              uint16_t* __restrict__ toff,
-                                                             uint32_t ldt) {
+                                                             uint32_t ldt, uint32_t ntiles) {
     constexpr int R = 2 * K - kSpBucketBits;
     constexpr uint64_t RM = (1ull << R) - 1ull;
     constexpr int WPT = Sp<E, POS>::WPT, kSpTile = Sp<E, POS>::TILE, EPC = epc<E>();
@@ -189,62 +198,113 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     __shared__ uint32_t wsum[kNW];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t lt = xcd_work_id();
-    const uint64_t gt = m.tile_lo + lt;
-    const int g = find_genome(m, gt);
-    const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)kSpTile;
-    const uint64_t ge = m.goff[g + 1];
+    const uint32_t x = blockIdx.x % 8u, nwg = gridDim.x;
+    const uint32_t nwx = (nwg - x + 7u) / 8u;                      // workgroups on XCD x
+    const uint32_t tq = ntiles / 8u, trem = ntiles % 8u;
+    const uint32_t xa = x * tq + (x < trem ? x : trem), xb = xa + tq + (x < trem ? 1u : 0u);
+    uint32_t lt = xa + blockIdx.x / 8u;
+    if (lt >= xb) return;   // whole workgroup
 
+    // genome cursor (a workgroup's tiles ascend): tiles [tg0, tg1), bytes [gb0, gb1) of genome g
+    int g = find_genome(m, m.tile_lo + lt);
+    uint64_t tg0 = m.tbase[g], tg1 = m.tbase[g + 1], gb0 = m.goff[g], gb1 = m.goff[g + 1];
+    struct Geo {
+        uint64_t base, gend;
+        uint32_t p0;   // window position of this thread's window 0 within its genome (< 2^32 - 1)
+        bool fast;     // 16-byte loads stay inside the data
+    };
+    auto geo = [&](uint32_t t) {
+        const uint64_t gt = m.tile_lo + t;
+        if (gt >= tg1) {   // next genome (rare: the cursor's loads may wait for queued stores)
+            do {
+                ++g;
+                tg0 = tg1;
+                tg1 = m.tbase[g + 1];
+            } while (gt >= tg1);
+            gb0 = m.goff[g];
+            gb1 = m.goff[g + 1];
+        }
+        const uint64_t tstart = gb0 + (gt - tg0) * (uint64_t)kSpTile;
+        Geo r;
+        r.base = tstart + (uint64_t)WPT * (uint64_t)tid;
+        r.gend = gb1;
+        r.p0 = (uint32_t)(r.base - gb0);
+        r.fast = tstart + (uint64_t)kSpTile + 48 <= m.data_end;
+        return r;
+    };
+
+    Geo cur = geo(lt);
+    uint4 v[4];
+    load_raw(seq, cur.base, cur.gend, cur.fast, v);
+    Bases bs = encode_bases(v, cur.base, cur.gend);
     cnt[tid] = 0u;
     __syncthreads();
 
-    const uint64_t base = tstart + (uint64_t)WPT * (uint64_t)tid;
-    const Bases bs = (tstart + (uint64_t)kSpTile + 48 <= m.data_end) ? load_bases<true>(seq, base, ge)
-                                                                     : load_bases<false>(seq, base, ge);
-    each_window<K, CANON, WPT>(bs, [&](uint64_t c, int) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
-    __syncthreads();
+    for (;;) {
+        const uint32_t nlt = lt + nwx;
+        const bool more = nlt < xb;   // uniform
+        Geo nxt = cur;
+        if (more) {
+            nxt = geo(nlt);
+            if (nxt.fast) load_raw(seq, nxt.base, nxt.gend, true, v);   // lands during this tile
+        }
 
-    // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
-    const uint32_t n0 = cnt[tid];
-    uint32_t incl = n0;
+        each_window<K, CANON, WPT>(bs, [&](uint64_t c, int) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
+        lds_barrier();
+
+        // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
+        const uint32_t n0 = cnt[tid];
+        uint32_t incl = n0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(incl, d);
-        if (lane >= d) incl += t;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t pre = 0u, total = 0u;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        lds_barrier();
+        uint32_t pre = 0u, total = 0u;
 #pragma unroll
-    for (int w = 0; w < kNW; ++w) {
-        pre += (w < wave) ? wsum[w] : 0u;
-        total += wsum[w];
-    }
-    const uint32_t s0 = pre + incl - n0;
-    cnt[tid] = s0;
-    toff[(uint64_t)tid * ldt + lt] = (uint16_t)s0;
-    if (tid == 0) toff[(uint64_t)kSpBuckets * ldt + lt] = (uint16_t)total;
-    __syncthreads();
+        for (int w = 0; w < kNW; ++w) {
+            pre += (w < wave) ? wsum[w] : 0u;
+            total += wsum[w];
+        }
+        const uint32_t s0 = pre + incl - n0;
+        cnt[tid] = s0;
+        toff[(uint64_t)tid * ldt + lt] = (uint16_t)s0;
+        if (tid == 0) toff[(uint64_t)kSpBuckets * ldt + lt] = (uint16_t)total;
+        lds_barrier();
 
-    // window position of this thread's window 0, relative to the genome (< 2^32 - 1)
-    const uint32_t p0 = (uint32_t)(base - m.goff[g]);
-    each_window<K, CANON, WPT>(bs, [&](uint64_t c, int j) {
-        const uint32_t slot = atomicAdd(&cnt[(uint32_t)(c >> R)], 1u);
-        sorted[slot] = (E)(c & RM);
-        if constexpr (POS) spos[slot] = p0 + (uint32_t)j;
-    });
-    __syncthreads();
+        const uint32_t p0 = cur.p0;
+        each_window<K, CANON, WPT>(bs, [&](uint64_t c, int j) {
+            const uint32_t slot = atomicAdd(&cnt[(uint32_t)(c >> R)], 1u);
+            sorted[slot] = (E)(c & RM);
+            if constexpr (POS) spos[slot] = p0 + (uint32_t)j;
+        });
+        lds_barrier();
 
-    E* dst = ent + lt * (uint64_t)kSpTile;
-    const uint32_t n4 = total / EPC;
-    for (uint32_t i = tid; i < n4; i += kSpThreads)
-        store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
-    if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
-    if constexpr (POS) {
-        uint32_t* pdst = epos + lt * (uint64_t)kSpTile;
-        for (uint32_t i = tid; i < total / 4; i += kSpThreads)
-            store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
-        if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+        // the next tile's codes: its loads had this tile's LDS work to land, and waiting for
+        // them here (before this tile's stores are queued behind them) costs little
+        if (more) {
+            if (!nxt.fast) load_raw(seq, nxt.base, nxt.gend, false, v);
+            bs = encode_bases(v, nxt.base, nxt.gend);
+        }
+        cnt[tid] = 0u;   // (the cursors are dead; the next histogram starts after a barrier)
+
+        E* dst = ent + (uint64_t)lt * kSpTile;
+        const uint32_t n4 = total / EPC;
+        for (uint32_t i = tid; i < n4; i += kSpThreads)
+            store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
+        if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
+        if constexpr (POS) {
+            uint32_t* pdst = epos + (uint64_t)lt * kSpTile;
+            for (uint32_t i = tid; i < total / 4; i += kSpThreads)
+                store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
+            if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+        }
+        if (!more) break;
+        lds_barrier();   // zeroed counters visible; this tile's LDS reads done before the next scatter
+        lt = nlt;
+        cur = nxt;
     }
 }
 
@@ -285,26 +345,6 @@ struct SplitItem {
     uint32_t per;      // expected entries per tile of this bucket
 };
 
-// f(r, true) for every entry of bucket b in tiles [ta, tb) (and f(x, false) for the other
-// entries of the chunks read, so the caller can stay branch-free), read as 16-byte chunks through a
-// per-wave queue: a wave takes bt tiles at a time (one per lane), lists the chunks that
-// cover their segments (tile-in-batch << 13 | chunk-in-tile) and streams them with kQU
-// loads in flight per lane; entries outside a segment are masked by position.
-//
-// Kept chunks (the split kernel walks a bucket twice, histogram then scatter): a wave whose
-// tiles form a single (first and last) queue step of at most 64 * kQU chunks -- the common case -- keeps them
-// in registers (kv, kq) on the first walk (REUSE = false sets kept) and the second walk
-// (REUSE = true) takes them from there instead of reading the entries again; the segment
-// bounds stay in the wave's LDS slo / shi, which nothing writes in between.  POS: the
-// positions of the chunk's entries ride along (pv).
-template <bool POS>
-struct Kept {
-    uint4 v[kQU];
-    PosChunk pv[POS ? kQU : 1];
-    uint32_t q[kQU];
-    bool kept;
-};
-
 // Positions of entries [4 c, 4 c + 4) (u32 entries) or [2 c, 2 c + 2) (u64) of a tile's layout.
 template <typename E>
 __device__ __forceinline__ PosChunk load_pos(const uint32_t* __restrict__ epos, uint64_t chunk) {
@@ -317,34 +357,32 @@ __device__ __forceinline__ uint32_t pos_of(const PosChunk& v, int i) {
     return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
-template <bool REUSE, bool POS, typename E, typename F>
+// Entries of the chunk starting at entry p0 that lie in the segment [lo, hi): bit i = entry i.
+template <uint32_t EPC>
+__device__ __forceinline__ uint32_t seg_mask(uint32_t p0, uint32_t lo, uint32_t hi) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < EPC; ++i) m |= (p0 + i >= lo && p0 + i < hi) ? 1u << i : 0u;
+    return m;
+}
+
+// f(r, pos, true) for every entry of bucket b in tiles [ta, tb) (and f(x, pos, false) for the
+// other entries of the chunks read, so the caller can stay branch-free), read from memory as
+// 16-byte chunks through a per-wave queue: a wave takes bt tiles at a time (one per lane),
+// lists the chunks that cover their segments (tile-in-batch << 13 | chunk-in-tile) and streams
+// them with kQU loads in flight per lane; entries outside a segment are masked by position.
+// The split kernel's path for a wave whose share of an item does not fit its registers (Held).
+template <bool POS, typename E, typename F>
 __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent, const uint32_t* __restrict__ epos,
                                             const uint16_t* __restrict__ toff, uint32_t ldt,
                                             uint32_t b, uint64_t ta, uint64_t tb, uint32_t bt,
-                                            uint32_t* q, uint32_t* slo, uint32_t* shi, Kept<POS>& kc, F&& f) {
+                                            uint32_t* q, uint32_t* slo, uint32_t* shi, F&& f) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint4* chunks = reinterpret_cast<const uint4*>(ent);
     constexpr uint32_t EPC = (uint32_t)epc<E>();
     constexpr int CB = chunk_bits<E, POS>();
     constexpr uint32_t CM = (1u << CB) - 1u;
     constexpr uint64_t TC = (uint64_t)tile_chunks<E, POS>();
-    if constexpr (REUSE) {
-        if (kc.kept) {   // wave-uniform
-#pragma unroll
-            for (int u = 0; u < kQU; ++u) {
-                const bool live = kc.q[u] != kEmpty;
-                const uint32_t qv = live ? kc.q[u] : 0u;
-                const uint32_t tl = qv >> CB, p0 = (qv & CM) * EPC;
-                const uint32_t l = slo[tl], h = live ? shi[tl] : 0u;
-#pragma unroll
-                for (int i = 0; i < (int)EPC; ++i)
-                    f(lane_of<E>(kc.v[u], i), POS ? pos_of(kc.pv[POS ? u : 0], i) : 0u, p0 + i >= l && p0 + i < h);
-            }
-            return;
-        }
-    } else {
-        kc.kept = false;
-    }
     for (uint64_t tw = ta + (uint64_t)wave * bt; tw < tb; tw += (uint64_t)kNW * bt) {
         const uint64_t t = tw + (uint64_t)lane;
         const bool in = (uint32_t)lane < bt && t < tb;
@@ -390,19 +428,6 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent, const uin
                     for (int i = 0; i < (int)EPC; ++i)
                         f(lane_of<E>(v[u], i), POS ? pos_of(pv[POS ? u : 0], i) : 0u, p0 + i >= l && p0 + i < h);
                 }
-                if constexpr (!REUSE) {
-                    // the wave's only step, in one round: keep the chunks for the second walk
-                    if (total <= 64u * (uint32_t)kQU && tw == ta + (uint64_t)wave * bt &&
-                        tw + (uint64_t)kNW * bt >= tb) {
-                        kc.kept = true;
-#pragma unroll
-                        for (int u = 0; u < kQU; ++u) {
-                            kc.v[u] = v[u];
-                            if constexpr (POS) kc.pv[u] = pv[u];
-                            kc.q[u] = qe[u];
-                        }
-                    }
-                }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -416,10 +441,104 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent, const uin
     }
 }
 
+// A wave's share of one split item held in registers: kQU chunks per lane and the entries of
+// each that lie inside their segment (bit 4u + i: entry i of chunk u).  The split kernel walks
+// an item twice (pass histogram, then scatter) and loads the next item's chunks while it works
+// on the current one.  kept = false (wave-uniform): the share spans more than one queue step or
+// 64 * kQU chunks, and both walks read it from memory (walk_bucket).
+template <bool POS>
+struct Held {
+    uint4 v[kQU];
+    PosChunk pv[POS ? kQU : 1];
+    uint32_t mask;
+    bool kept;
+};
+static_assert(kQU * 4 <= 32, "chunk masks of a lane fit 32 bits");
+
+// Lists the chunks of the wave's tiles [tw, tw + 64) -- this lane's segment [lo, hi) of tile
+// tw + lane -- in the wave's queue with their masks, and issues their loads into h (nobody
+// waits for them here).  single: the wave's share of the item is this one step.
+template <typename E, bool POS>
+__device__ __forceinline__ void hold_chunks(const E* __restrict__ ent, const uint32_t* __restrict__ epos,
+                                            uint64_t tw, uint32_t lo, uint32_t hi, bool single, uint32_t* q,
+                                            Held<POS>& h) {
+    const int lane = threadIdx.x & 63;
+    const uint4* chunks = reinterpret_cast<const uint4*>(ent);
+    constexpr uint32_t EPC = (uint32_t)epc<E>();
+    constexpr int CB = chunk_bits<E, POS>();
+    constexpr uint32_t CM = (1u << CB) - 1u;
+    constexpr uint64_t TC = (uint64_t)tile_chunks<E, POS>();
+    const uint32_t c0 = lo / EPC, nc = hi > lo ? (hi + EPC - 1u) / EPC - c0 : 0u;
+    uint32_t incl = nc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(incl, d);
+        if (lane >= d) incl += x;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    h.mask = 0u;
+    h.kept = single && total <= 64u * (uint32_t)kQU;   // wave-uniform
+    if (h.kept) {
+        // queue entry: mask << 24 | tile-in-step << CB | chunk-in-tile (CB + 6 <= 19 bits)
+        const uint32_t ex = incl - nc;
+        for (uint32_t j = 0; j < nc; ++j)
+            q[ex + j] = (seg_mask<EPC>((c0 + j) * EPC, lo, hi) << 24) | ((uint32_t)lane << CB) | (c0 + j);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // The loads are issued on every path (a wave that does not keep its share loads chunk 0 of
+    // the batch and masks it out), so that the compiler sees them complete at landed() on
+    // every path and does not wait for them again behind the item's stores.
+#pragma unroll
+    for (int u = 0; u < kQU; ++u) {
+        // idle lanes (and a wave with no tiles in this item, whose tw may lie past the batch)
+        // load chunk 0 of the batch, with no entries
+        const uint32_t e = (uint32_t)(u * 64 + lane);
+        const bool live = h.kept && e < total;
+        const uint32_t qe = live ? q[e] : 0u;
+        const uint64_t ci = live ? (tw + ((qe >> CB) & 63u)) * TC + (qe & CM) : 0u;
+        h.v[u] = chunks[ci];
+        if constexpr (POS) h.pv[u] = load_pos<E>(epos, ci);
+        h.mask |= (qe >> 24) << (4 * u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename E, bool POS, typename F>
+__device__ __forceinline__ void each_held(const Held<POS>& h, F&& f) {
+    constexpr int EPC = epc<E>();
+#pragma unroll
+    for (int u = 0; u < kQU; ++u)
+#pragma unroll
+        for (int i = 0; i < EPC; ++i)
+            f(lane_of<E>(h.v[u], i), POS ? pos_of(h.pv[POS ? u : 0], i) : 0u, ((h.mask >> (4 * u + i)) & 1u) != 0u);
+}
+
+// Makes the wave wait here for the loads into h (the compiler waits before an asm statement
+// that reads a register whose load is still in flight).
+template <bool POS>
+__device__ __forceinline__ void landed(const Held<POS>& h) {
+#pragma unroll
+    for (int u = 0; u < kQU; ++u) {
+        asm volatile("" ::"v"(h.v[u].x), "v"(h.v[u].y), "v"(h.v[u].z), "v"(h.v[u].w));
+        if constexpr (POS) asm volatile("" ::"v"(h.pv[u].x), "v"(h.pv[u].y), "v"(h.pv[u].z), "v"(h.pv[u].w));
+    }
+}
+
+// Persistent, one workgroup per CU (124 KiB of LDS).  XCD x (= blockIdx % 8) takes a contiguous
+// run of the items and its workgroups stride through it.  Per item: (A) the next item's chunks
+// are listed and loaded into registers from segment bounds fetched one item earlier, (B) the
+// bounds of the item after that are fetched, (C) this item's entries -- already in registers --
+// are counted by pass (LDS histogram), scanned and scattered into the LDS staging, then the
+// wave waits for A and B, which had C's LDS work to land in, and (D) queues this item's
+// stores, which drain behind the next item's work.  Barriers wait for LDS operations only.
 template <typename E, bool POS>
 __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     const E* __restrict__ ent, const uint32_t* __restrict__ epos, const uint16_t* __restrict__ toff, uint32_t ldt,
-    const SplitItem* __restrict__ items, int R, E* __restrict__ out, uint32_t* __restrict__ opos,
+    const SplitItem* __restrict__ items, uint32_t nitems, int R, E* __restrict__ out, uint32_t* __restrict__ opos,
     uint16_t* __restrict__ toff2, uint32_t* __restrict__ gb_fail) {
     constexpr int kCaps = Sp<E, POS>::CAPS, EPC = epc<E>();
     __shared__ __attribute__((aligned(16))) E sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
@@ -429,70 +548,173 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     __shared__ uint32_t slo[kNW][64], shi[kNW][64];
     __shared__ uint32_t wsum[kMaxPasses / 64], total_sh;
 
-    const uint32_t item = xcd_work_id();
-    const SplitItem it = items[item];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t x = blockIdx.x % 8u, nwg = gridDim.x;
+    const uint32_t nwx = (nwg - x + 7u) / 8u;                      // workgroups on XCD x
+    const uint32_t iq = nitems / 8u, irem = nitems % 8u;
+    const uint32_t xa = x * iq + (x < irem ? x : irem), xb = xa + iq + (x < irem ? 1u : 0u);
+    uint32_t item = xa + blockIdx.x / 8u;
+    if (item >= xb) return;   // whole workgroup
+
+    // this wave's tiles of an item: [t0 + wave * bt, + bt), one per lane; single: no second step
+    auto wave_tiles = [&](const SplitItem& it, uint64_t& tw, bool& single) {
+        const uint32_t bt = split_bt(it.per, (uint32_t)EPC);
+        tw = (uint64_t)it.t0 + (uint64_t)wave * bt;
+        single = tw + (uint64_t)kNW * bt >= it.t1;
+        return bt;
+    };
+    auto bounds = [&](const SplitItem& it, uint32_t& lo, uint32_t& hi) {
+        uint64_t tw;
+        bool single;
+        const uint32_t bt = wave_tiles(it, tw, single);
+        const uint64_t t = tw + (uint64_t)lane;
+        const bool in = (uint32_t)lane < bt && t < it.t1;
+        // unconditional loads (see hold_chunks), masked afterwards
+        const uint32_t l = toff[in ? (uint64_t)it.b * ldt + t : 0u];
+        const uint32_t h = toff[in ? (uint64_t)(it.b + 1) * ldt + t : 0u];
+        lo = in ? l : 0u;
+        hi = in ? h : 0u;
+    };
+
     if (tid < kMaxPasses) hist[tid] = 0u;
+    // kPipe: the next item's chunks load during this item (u32 / u64 entries).  With positions
+    // two items' chunks do not fit the registers (the compiler spills, and every spill reload
+    // waits for all loads and stores in flight), so each item's chunks load when it starts.
+    constexpr bool kPipe = !POS;
+    SplitItem cur = items[item];
+    Held<POS> hc;
+    hc.kept = false;
+    hc.mask = 0u;
+    uint32_t lo_c, hi_c;
+    bounds(cur, lo_c, hi_c);
+    if constexpr (kPipe) {
+        uint64_t tw;
+        bool single;
+        wave_tiles(cur, tw, single);
+        hold_chunks<E, POS>(ent, epos, tw, lo_c, hi_c, single, q[wave], hc);
+    }
+    uint32_t nitem = item + nwx;
+    bool has_n = nitem < xb;
+    SplitItem nxt = cur;
+    uint32_t lo_n = 0u, hi_n = 0u;
+    if (has_n) {
+        nxt = items[nitem];
+        bounds(nxt, lo_n, hi_n);
+    }
+    // complete before the loop on this path too: a wait inside the loop for a load of the
+    // prologue would be executed every item, and would drain the previous item's stores
+    landed(hc);
+    asm volatile("" ::"v"(lo_n), "v"(hi_n), "v"(lo_c), "v"(hi_c));
     __syncthreads();
-    const uint32_t bt = split_bt(it.per, (uint32_t)EPC);
-    const uint32_t np = it.np;
+
     // Branch-free LDS atomics: an entry outside its segment counts into one of 32 dummy
     // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
     // tail of `sorted`, so no exec-mask branch surrounds an atomic.
     const uint32_t dpass = (uint32_t)kMaxPasses + (uint32_t)(lane & 31);
-    Kept<POS> kc;
-    walk_bucket<false, POS>(ent, epos, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc,
-                            [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); });
-    __syncthreads();
-    // exclusive scan of the pass histogram (threads 0..255)
-    uint32_t n0 = 0u, incl = 0u;
-    if (tid < kMaxPasses) {
-        n0 = hist[tid];
-        incl = n0;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
+    for (;;) {
+        // (A) the next item's chunks, (B) the bounds of the one after
+        Held<POS> hn;
+        hn.kept = false;
+        hn.mask = 0u;
+        const uint32_t nnitem = nitem + nwx;
+        const bool has_nn = has_n && nnitem < xb;   // uniform
+        SplitItem nn = nxt;
+        uint32_t lo_nn = 0u, hi_nn = 0u;
+        {   // on every path (after the last item: a copy of the current one, never used)
+            uint64_t tw;
+            bool single;
+            if constexpr (kPipe) {
+                wave_tiles(nxt, tw, single);
+                hold_chunks<E, POS>(ent, epos, tw, lo_n, hi_n, single, q[wave], hn);
+            } else {
+                wave_tiles(cur, tw, single);
+                hold_chunks<E, POS>(ent, epos, tw, lo_c, hi_c, single, q[wave], hc);
+            }
+            nn = items[has_nn ? nnitem : item];
+            bounds(nn, lo_nn, hi_nn);
         }
-        if (lane == 63) wsum[wave] = incl;
-    }
-    __syncthreads();
-    if (tid < kMaxPasses) {
-        uint32_t pre = 0u;
-        for (int w = 0; w < wave; ++w) pre += wsum[w];
-        const uint32_t st = pre + incl - n0;
-        hist[tid] = st;
-        if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)st;
-        if (tid == 0) {
-            uint32_t tot = 0u;
+
+        // (C) this item: pass histogram, scan, scatter
+        const uint32_t np = cur.np;
+        auto count_pass = [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); };
+        const uint32_t bt = split_bt(cur.per, (uint32_t)EPC);
+        if (hc.kept) each_held<E, POS>(hc, count_pass);   // wave-uniform
+        else walk_bucket<POS>(ent, epos, toff, ldt, cur.b, cur.t0, cur.t1, bt, q[wave], slo[wave], shi[wave], count_pass);
+        lds_barrier();
+        // exclusive scan of the pass histogram
+        uint32_t n0 = 0u, incl = 0u;
+        if (tid < kMaxPasses) {
+            n0 = hist[tid];
+            incl = n0;
 #pragma unroll
-            for (int w = 0; w < kMaxPasses / 64; ++w) tot += wsum[w];
-            total_sh = tot;
-            toff2[(uint64_t)item * kT2 + np] = (uint16_t)(tot <= (uint32_t)kCaps ? tot : 0u);
-            if (tot > (uint32_t)kCaps) gb_fail[it.gb] = 1u;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(incl, d);
+                if (lane >= d) incl += t;
+            }
+            if (lane == 63) wsum[wave] = incl;
         }
-    }
-    __syncthreads();
-    const uint32_t total = total_sh;
-    if (total > (uint32_t)kCaps) return;  // staging overflow: the bucket goes to the fallback
-    walk_bucket<true, POS>(ent, epos, toff, ldt, it.b, it.t0, it.t1, bt, q[wave], slo[wave], shi[wave], kc,
-                           [&](E r, uint32_t p, bool ok) {
-        const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
-        const uint32_t at = ok ? slot : (uint32_t)kCaps + (uint32_t)lane;
-        sorted[at] = r;
-        if constexpr (POS) spos[at] = p;
-    });
-    __syncthreads();
-    E* dst = out + (uint64_t)item * kCaps;
-    const uint32_t n4 = total / EPC;
-    for (uint32_t i = tid; i < n4; i += kSpThreads)
-        store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
-    if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
-    if constexpr (POS) {
-        uint32_t* pdst = opos + (uint64_t)item * kCaps;
-        for (uint32_t i = tid; i < total / 4; i += kSpThreads)
-            store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
-        if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+        lds_barrier();
+        if (tid < kMaxPasses) {
+            uint32_t pre = 0u;
+            for (int w = 0; w < wave; ++w) pre += wsum[w];
+            const uint32_t st = pre + incl - n0;
+            hist[tid] = st;
+            if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)st;
+            if (tid == 0) {
+                uint32_t tot = 0u;
+#pragma unroll
+                for (int w = 0; w < kMaxPasses / 64; ++w) tot += wsum[w];
+                total_sh = tot;
+                toff2[(uint64_t)item * kT2 + np] = (uint16_t)(tot <= (uint32_t)kCaps ? tot : 0u);
+                if (tot > (uint32_t)kCaps) gb_fail[cur.gb] = 1u;   // staging overflow: the bucket goes to the fallback
+            }
+        }
+        lds_barrier();
+        const uint32_t total = total_sh;
+        const bool fits = total <= (uint32_t)kCaps;   // uniform
+        if (fits) {
+            auto scatter = [&](E r, uint32_t p, bool ok) {
+                const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
+                const uint32_t at = ok ? slot : (uint32_t)kCaps + (uint32_t)lane;
+                sorted[at] = r;
+                if constexpr (POS) spos[at] = p;
+            };
+            if (hc.kept) each_held<E, POS>(hc, scatter);
+            else walk_bucket<POS>(ent, epos, toff, ldt, cur.b, cur.t0, cur.t1, bt, q[wave], slo[wave], shi[wave], scatter);
+        }
+        lds_barrier();
+
+        // A and B have landed by now (waited for here, not behind D's stores)
+        if constexpr (kPipe) landed(hn);
+        asm volatile("" ::"v"(lo_nn), "v"(hi_nn));
+        if (tid < kMaxPasses) hist[tid] = 0u;   // the cursors are dead; the next item starts after a barrier
+
+        // (D) this item's stores
+        if (fits) {
+            E* dst = out + (uint64_t)item * kCaps;
+            const uint32_t n4 = total / EPC;
+            for (uint32_t i = tid; i < n4; i += kSpThreads)
+                store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
+            if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
+            if constexpr (POS) {
+                uint32_t* pdst = opos + (uint64_t)item * kCaps;
+                for (uint32_t i = tid; i < total / 4; i += kSpThreads)
+                    store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
+                if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+            }
+        }
+        if (!has_n) break;
+        lds_barrier();   // zeroed histogram visible; the staging's reads done before the next scatter
+        item = nitem;
+        cur = nxt;
+        if constexpr (kPipe) hc = hn;
+        nitem = nnitem;
+        has_n = has_nn;
+        nxt = nn;
+        lo_c = lo_n;
+        hi_c = hi_n;
+        lo_n = lo_nn;
+        hi_n = hi_nn;
     }
 }
 
@@ -1118,30 +1340,30 @@ void* carve(char*& p, size_t bytes) {
 }
 
 template <int K, int CANON, typename E, bool POS>
-void launch_partition(unsigned tiles, hipStream_t s, const uint8_t* seq, const GenomeMap& m,
+void launch_partition(unsigned tiles, unsigned grid, hipStream_t s, const uint8_t* seq, const GenomeMap& m,
                       E* ent, uint32_t* epos, uint16_t* toff, uint32_t ldt) {
-    hipLaunchKernelGGL((k_sp_partition<K, CANON, E, POS>), dim3(tiles), dim3(kSpThreads), 0, s, seq, m, ent,
-                       epos, toff, ldt);
+    hipLaunchKernelGGL((k_sp_partition<K, CANON, E, POS>), dim3(grid), dim3(kSpThreads), 0, s, seq, m, ent,
+                       epos, toff, ldt, (uint32_t)tiles);
 }
 
 template <int K, typename E, bool POS>
-void partition_k(int canonical, unsigned tiles, hipStream_t s, const uint8_t* seq,
+void partition_k(int canonical, unsigned tiles, unsigned grid, hipStream_t s, const uint8_t* seq,
                  const GenomeMap& m, E* ent, uint32_t* epos, uint16_t* toff, uint32_t ldt) {
-    if (canonical) launch_partition<K, 1, E, POS>(tiles, s, seq, m, ent, epos, toff, ldt);
-    else launch_partition<K, 0, E, POS>(tiles, s, seq, m, ent, epos, toff, ldt);
+    if (canonical) launch_partition<K, 1, E, POS>(tiles, grid, s, seq, m, ent, epos, toff, ldt);
+    else launch_partition<K, 0, E, POS>(tiles, grid, s, seq, m, ent, epos, toff, ldt);
 }
 
 template <typename E, bool POS>
-void launch_partition_k(int k, int canonical, unsigned tiles, hipStream_t s, const uint8_t* seq,
+void launch_partition_k(int k, int canonical, unsigned tiles, unsigned grid, hipStream_t s, const uint8_t* seq,
                         const GenomeMap& m, E* ent, uint32_t* epos, uint16_t* toff, uint32_t ldt) {
-#define KMH_PK(KK) case KK: partition_k<KK, E, POS>(canonical, tiles, s, seq, m, ent, epos, toff, ldt); break;
+#define KMH_PK(KK) case KK: partition_k<KK, E, POS>(canonical, tiles, grid, s, seq, m, ent, epos, toff, ldt); break;
     if constexpr (sizeof(E) == 4) {
         switch (k) { KMH_PK(13) KMH_PK(14) KMH_PK(15) KMH_PK(16) KMH_PK(17) KMH_PK(18) KMH_PK(19) KMH_PK(20)
-                     default: partition_k<21, E, POS>(canonical, tiles, s, seq, m, ent, epos, toff, ldt); break; }
+                     default: partition_k<21, E, POS>(canonical, tiles, grid, s, seq, m, ent, epos, toff, ldt); break; }
     } else {
         switch (k) { KMH_PK(22) KMH_PK(23) KMH_PK(24) KMH_PK(25) KMH_PK(26) KMH_PK(27) KMH_PK(28) KMH_PK(29)
                      KMH_PK(30) KMH_PK(31)
-                     default: partition_k<32, E, POS>(canonical, tiles, s, seq, m, ent, epos, toff, ldt); break; }
+                     default: partition_k<32, E, POS>(canonical, tiles, grid, s, seq, m, ent, epos, toff, ldt); break; }
     }
 #undef KMH_PK
 }
@@ -1300,7 +1522,11 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         if (tiles == 0) continue;
         GenomeMap m{d_goff, d_tbase, g0, g1, L.tbase[g0], L.goff[G]};
         time_begin(ctx, s, "k_sp_partition");
-        launch_partition_k<E, POS>(k, canonical, (unsigned)tiles, s, d_seq, m, ent, epos, toff, ldt);
+        // persistent partition: one workgroup per CU (KMH_SP_PART_GRID = 0: one per tile, the
+        // launch of rounds 1-2, kept for A/B runs)
+        const long pg = env_long("KMH_SP_PART_GRID", std::max(1, ctx->num_cu));
+        const unsigned pgrid = (unsigned)std::min<uint64_t>(tiles, pg > 0 ? (uint64_t)pg : tiles);
+        launch_partition_k<E, POS>(k, canonical, (unsigned)tiles, pgrid, s, d_seq, m, ent, epos, toff, ldt);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 
@@ -1354,8 +1580,11 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         time_begin(ctx, s, "k_sp_split");
-        hipLaunchKernelGGL((k_sp_split<E, POS>), dim3((unsigned)nsi), dim3(kSpThreads), 0, s, ent, epos, toff, ldt,
-                           d_sitems, R, d_split, d_spos, d_toff2, d_gbfail);
+        // persistent split: one workgroup per CU (KMH_SP_SPLIT_GRID = 0: one per item)
+        const long sg = env_long("KMH_SP_SPLIT_GRID", std::max(1, ctx->num_cu));
+        const unsigned sgrid = (unsigned)std::min<uint64_t>(nsi, sg > 0 ? (uint64_t)sg : nsi);
+        hipLaunchKernelGGL((k_sp_split<E, POS>), dim3(sgrid), dim3(kSpThreads), 0, s, ent, epos, toff, ldt,
+                           d_sitems, (uint32_t)nsi, R, d_split, d_spos, d_toff2, d_gbfail);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
         time_begin(ctx, s, "k_sp_count");

@@ -746,6 +746,15 @@ def _torchrun(args, timeout=600, nproc=1, env=None):
                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _failure(r):
+    """The first rank traceback of a failed torchrun (the launcher's own report follows it and
+    would push it out of a plain tail), then the tail."""
+    err = r.stderr or ""
+    i = err.find("Traceback")
+    head = err[i:i + 4000] if i >= 0 else ""
+    return head + "\n...\n" + err[-1500:]
+
+
 def test_count_matrix_rccl_assembly(tmp_path, oracle_lib):
     """count_matrix under an RCCL process group (world size 1 on the test box): encode u4 +
     escapes, all-reduce, all-gather, decode -- bit-identical to counting directly."""
@@ -760,7 +769,7 @@ def test_count_matrix_rccl_assembly(tmp_path, oracle_lib):
     out = tmp_path / "m.npy"
     here = os.path.dirname(os.path.abspath(__file__))
     r = _torchrun([os.path.join(here, "rccl_probe.py"), str(out), "8"] + files)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     got = np.load(out).view(np.uint32)
     want = np.stack([kmatrix._hip_count_block([f], 8, 0).cpu().numpy().view(np.uint32)[0] for f in files])
     assert got.shape == want.shape and got.max() > 255
@@ -778,7 +787,7 @@ def test_count_genome_split(tmp_path, oracle_lib, backend, nproc):
     osynth.write_fasta(fa, recs)
     here = os.path.dirname(os.path.abspath(__file__))
     r = _torchrun([os.path.join(here, "split_probe.py"), str(tmp_path), "12", str(fa), backend], nproc=nproc)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     buf, _ = kmatrix.pack_genomes([str(fa)], 12)
     want = oracle_lib.count_dense(bytes(buf), 12)
     for q in range(nproc):
@@ -818,7 +827,7 @@ def test_bench_pipelined_u8_assembly_rccl():
     """bench.py's pipelined u8 all-gather path (the N > 1 default) through RCCL, one rank."""
     r = _torchrun(["bench.py", "--assemble", "u8", "--genomes", "3", "--genome-len", "3000000",
                    "--steps", "3", "--warmup", "1", "--cpu-sample", "0"])
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["rows_checked"] is True and d["config"]["assembly"] == "u8"
@@ -828,7 +837,7 @@ def test_bench_pipelined_u4_assembly_rccl():
     """bench.py's pipelined u4 all-gather path (the N > 1 default) through RCCL, one rank."""
     r = _torchrun(["bench.py", "--assemble", "u4", "--genomes", "3", "--genome-len", "3000000",
                    "--steps", "3", "--warmup", "1", "--cpu-sample", "0"])
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["config"]["assembly"] == "u4"
     assert d["allgather"]["allgather_ms"] > 0 and d["allgather"]["received_bytes_per_rank"] == 0
@@ -843,7 +852,7 @@ def test_bench_pipelined_assembly_two_ranks(wire):
     r = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--single-device", "--assemble", wire,
                    "--genomes", "4", "--genome-len", "6000000", "--k", "10", "--steps", "3", "--warmup", "1",
                    "--cpu-sample", "0"], nproc=2)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["n_gpus"] == 2 and d["config"]["assembly"] == wire
     ag = d["allgather"]                 # the assembly's all-gather reported on its own
@@ -887,7 +896,7 @@ def test_assembled_matrix_compact_two_ranks(tmp_path, caps, wire):
     here = os.path.dirname(os.path.abspath(__file__))
     r = _torchrun([os.path.join(here, "assembly_probe.py"), str(tmp_path), "5", "2000000", "10", "gloo",
                    "--single-device", "--compact"], nproc=2, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     res = json.load(open(tmp_path / "result.json"))
     assert res == {"wire": wire, "assembly_checked": True, "world": 2}
 
@@ -897,7 +906,7 @@ def test_bench_simulated_rank():
     assembly, the all-gather's writes modelled by device copies), labelled as a projection."""
     r = _torchrun(["bench.py", "--simulate-ranks", "4", "--genomes", "8", "--genome-len", "3000000",
                    "--steps", "3", "--warmup", "1", "--cpu-sample", "0"])
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["simulated_ranks"] == 4
     assert d["config"]["workload"].startswith("projection")
@@ -1002,7 +1011,7 @@ def test_config4_per_rank_workload_eight_ranks(tmp_path, oracle_lib, wire):
     r = _torchrun(["bench.py", "--gpus", "8", "--backend", "gloo", "--single-device", "--assemble", wire,
                    "--steps", "2", "--warmup", "1", "--cpu-sample", "0", "--check-dir", str(tmp_path)],
                   nproc=8, timeout=800)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["assembly_checked"] is True
     assert d["n_gpus"] == 8 and d["single_device"] is True and d["config"]["assembly"] == wire
@@ -1026,7 +1035,7 @@ def test_config4_assembly_fallbacks_full_size(tmp_path, oracle_lib, caps, wire):
     here = os.path.dirname(os.path.abspath(__file__))
     r = _torchrun([os.path.join(here, "assembly_probe.py"), str(tmp_path), "64", "100000000", "12", "gloo",
                    "--single-device"], nproc=8, timeout=800, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     res = json.load(open(tmp_path / "result.json"))
     assert res == {"wire": wire, "assembly_checked": True, "world": 8}
     rep = b"ACGTTGCA" * 125_000
