@@ -205,33 +205,6 @@ constexpr int num_buckets() { return 1 << (2 * K - kCBits); }
 template <int K>
 constexpr int tile_cap() { return kPTile + 7 * num_buckets<K>(); }
 
-// DPP: v of lane (lane - D) in the same 16-lane row, 0 where that lane lies outside it.
-template <int D>
-__device__ __forceinline__ uint32_t dpp_shr(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + D, 0xF, 0xF, true);
-}
-// Inclusive scan inside each group of 8 lanes (lanes 8i .. 8i+7).
-__device__ __forceinline__ uint32_t scan8(uint32_t s, int lane) {
-    const int q = lane & 7;
-    uint32_t t = dpp_shr<1>(s);
-    s += q >= 1 ? t : 0u;
-    t = dpp_shr<2>(s);
-    s += q >= 2 ? t : 0u;
-    t = dpp_shr<4>(s);
-    s += q >= 4 ? t : 0u;
-    return s;
-}
-// Inclusive scan over the 64 lanes of a wave.
-__device__ __forceinline__ uint32_t scan64(uint32_t s) {
-    s += dpp_shr<1>(s);
-    s += dpp_shr<2>(s);
-    s += dpp_shr<4>(s);
-    s += dpp_shr<8>(s);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xC, 0xF, false);  // row_bcast:31
-    return s;
-}
-
 // The 32 window codes of this thread from its 48 loaded bytes (invalid windows: INV, which
 // k_partition makes bucket NBK, suffix 0).
 template <int K, uint32_t INV>

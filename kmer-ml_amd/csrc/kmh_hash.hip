@@ -326,9 +326,13 @@ __global__ __launch_bounds__(256) void k_sp_sizes(const uint16_t* __restrict__ t
     if (threadIdx.x == 0) nb[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// np <= 256 and r < 2^R with R <= 54: the product fits 64 bits
-__device__ __forceinline__ uint32_t pass_of(uint64_t r, uint32_t np, int R) {
-    return (uint32_t)((r * np) >> R);
+// Pass of residue r (R bits) in a bucket of np passes: floor(r * np / 2^R).  u32 residues
+// (R <= 32): the high half of (r << (32 - R)) * np, one 32-bit multiply; u64 (R <= 54, np <=
+// 1024): the 64-bit product fits.
+template <typename E>
+__device__ __forceinline__ uint32_t pass_of(E r, uint32_t np, int R) {
+    if constexpr (sizeof(E) == 4) return __umulhi((uint32_t)r << (32 - R), np);
+    else return (uint32_t)(((uint64_t)r * np) >> R);
 }
 
 // Entry i of a 16-byte chunk (4 u32 or 2 u64 entries).
@@ -389,13 +393,8 @@ __device__ __forceinline__ void walk_bucket(const E* __restrict__ ent, const uin
         const uint32_t lo = in ? toff[(uint64_t)b * ldt + t] : 0u;
         const uint32_t hi = in ? toff[(uint64_t)(b + 1) * ldt + t] : 0u;
         const uint32_t c0 = lo / EPC, nc = hi > lo ? (hi + EPC - 1u) / EPC - c0 : 0u;
-        uint32_t incl = nc;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
-        }
-        const uint32_t total = __shfl(incl, 63);
+        const uint32_t incl = scan64(nc);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         if (total == 0u) continue;
         if (total <= (uint32_t)kQueue) {
             slo[lane] = lo;
@@ -469,20 +468,18 @@ __device__ __forceinline__ void hold_chunks(const E* __restrict__ ent, const uin
     constexpr uint32_t CM = (1u << CB) - 1u;
     constexpr uint64_t TC = (uint64_t)tile_chunks<E, POS>();
     const uint32_t c0 = lo / EPC, nc = hi > lo ? (hi + EPC - 1u) / EPC - c0 : 0u;
-    uint32_t incl = nc;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t x = __shfl_up(incl, d);
-        if (lane >= d) incl += x;
-    }
-    const uint32_t total = __shfl(incl, 63);
+    const uint32_t incl = scan64(nc);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     h.mask = 0u;
     h.kept = single && total <= 64u * (uint32_t)kQU;   // wave-uniform
     if (h.kept) {
-        // queue entry: mask << 24 | tile-in-step << CB | chunk-in-tile (CB + 6 <= 19 bits)
-        const uint32_t ex = incl - nc;
+        // queue entry: mask << 24 | tile-in-step << CB | chunk-in-tile (CB + 6 <= 19 bits); only
+        // a segment's first and last chunks hold entries of other segments
+        constexpr uint32_t FULL = (1u << EPC) - 1u;
+        const uint32_t mf = seg_mask<EPC>(c0 * EPC, lo, hi), ml = seg_mask<EPC>((c0 + nc - 1u) * EPC, lo, hi);
+        const uint32_t ex = incl - nc, lt = (uint32_t)lane << CB;
         for (uint32_t j = 0; j < nc; ++j)
-            q[ex + j] = (seg_mask<EPC>((c0 + j) * EPC, lo, hi) << 24) | ((uint32_t)lane << CB) | (c0 + j);
+            q[ex + j] = (((j == 0 ? mf : FULL) & (j + 1 == nc ? ml : FULL)) << 24) | lt | (c0 + j);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -528,6 +525,14 @@ __device__ __forceinline__ void landed(const Held<POS>& h) {
     }
 }
 
+#ifdef KMH_EXPERIMENTS
+// KMH_SP_PROF=1: per-phase clocks of k_sp_split summed over its waves (lane 0 of each); [15] = waves
+__device__ unsigned long long g_split_prof[16];
+#define KMH_ST(i) if (lane == 0) { const unsigned long long t_ = clock64(); st_[i] += t_ - stl_; stl_ = t_; }
+#else
+#define KMH_ST(i)
+#endif
+
 // Persistent, one workgroup per CU (124 KiB of LDS).  XCD x (= blockIdx % 8) takes a contiguous
 // run of the items and its workgroups stride through it.  Per item: (A) the next item's chunks
 // are listed and loaded into registers from segment bounds fetched one item earlier, (B) the
@@ -543,10 +548,17 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     constexpr int kCaps = Sp<E, POS>::CAPS, EPC = epc<E>();
     __shared__ __attribute__((aligned(16))) E sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
     __shared__ __attribute__((aligned(16))) uint32_t spos[POS ? kCaps + 64 : 4];
-    __shared__ uint32_t hist[kMaxPasses + 32];   // + dummy passes
+    // pass counters: np <= kRepP passes -- every item of config 5 (~32) -- count in 32 bank
+    // replicas each (pass * 32 + lane % 32: the 32 lanes of a lane group never share an
+    // address or a bank, where 64 lanes on ~32 plain counters collided); more passes: one
+    // counter each.  Out-of-segment entries count into 32 dummies past the replicas.
+    constexpr int kRepP = 128;
+    static_assert(kRepP * 32 == 4 * kSpThreads && kMaxPasses + 32 <= kRepP * 32, "counter layout");
+    __shared__ __attribute__((aligned(16))) uint32_t hist[kRepP * 32 + 32];
     __shared__ uint32_t q[kNW][kQueue];
     __shared__ uint32_t slo[kNW][64], shi[kNW][64];
-    __shared__ uint32_t wsum[kMaxPasses / 64], total_sh;
+    __shared__ uint32_t wsum[kNW], total_sh;
+    uint4* hist4 = reinterpret_cast<uint4*>(hist);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t x = blockIdx.x % 8u, nwg = gridDim.x;
@@ -576,7 +588,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         hi = in ? h : 0u;
     };
 
-    if (tid < kMaxPasses) hist[tid] = 0u;
+    hist4[tid] = make_uint4(0u, 0u, 0u, 0u);
     // kPipe: the next item's chunks load during this item (u32 / u64 entries).  With positions
     // two items' chunks do not fit the registers (the compiler spills, and every spill reload
     // waits for all loads and stores in flight), so each item's chunks load when it starts.
@@ -601,6 +613,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         nxt = items[nitem];
         bounds(nxt, lo_n, hi_n);
     }
+    // descriptors are read one item ahead of their bounds (a scalar load's result is first
+    // needed an item later)
+    SplitItem nn = items[has_n && nitem + nwx < xb ? nitem + nwx : item];
     // complete before the loop on this path too: a wait inside the loop for a load of the
     // prologue would be executed every item, and would drain the previous item's stores
     landed(hc);
@@ -610,7 +625,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // Branch-free LDS atomics: an entry outside its segment counts into one of 32 dummy
     // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
     // tail of `sorted`, so no exec-mask branch surrounds an atomic.
-    const uint32_t dpass = (uint32_t)kMaxPasses + (uint32_t)(lane & 31);
+    const uint32_t rl = (uint32_t)(lane & 31);
+#ifdef KMH_EXPERIMENTS
+    unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stl_ = clock64();
+#endif
     for (;;) {
         // (A) the next item's chunks, (B) the bounds of the one after
         Held<POS> hn;
@@ -618,8 +636,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         hn.mask = 0u;
         const uint32_t nnitem = nitem + nwx;
         const bool has_nn = has_n && nnitem < xb;   // uniform
-        SplitItem nn = nxt;
         uint32_t lo_nn = 0u, hi_nn = 0u;
+        SplitItem nnn;
         {   // on every path (after the last item: a copy of the current one, never used)
             uint64_t tw;
             bool single;
@@ -630,51 +648,70 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                 wave_tiles(cur, tw, single);
                 hold_chunks<E, POS>(ent, epos, tw, lo_c, hi_c, single, q[wave], hc);
             }
-            nn = items[has_nn ? nnitem : item];
+            KMH_ST(0)
             bounds(nn, lo_nn, hi_nn);
+            nnn = items[has_nn && nnitem + nwx < xb ? nnitem + nwx : item];
+            KMH_ST(1)
         }
 
         // (C) this item: pass histogram, scan, scatter
         const uint32_t np = cur.np;
-        auto count_pass = [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u); };
+        const bool rep = np <= (uint32_t)kRepP;   // uniform
+        const uint32_t csh = rep ? 5u : 0u, crl = rep ? rl : 0u, cdum = (uint32_t)(kRepP * 32) + rl;
+        auto ctr = [&](E r, bool ok) {   // branch-free: the dummy is a select
+            const uint32_t c = (pass_of<E>(r, np, R) << csh) | crl;
+            return ok ? c : cdum;
+        };
+        auto count_pass = [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ctr(r, ok)], 1u); };
         const uint32_t bt = split_bt(cur.per, (uint32_t)EPC);
         if (hc.kept) each_held<E, POS>(hc, count_pass);   // wave-uniform
         else walk_bucket<POS>(ent, epos, toff, ldt, cur.b, cur.t0, cur.t1, bt, q[wave], slo[wave], shi[wave], count_pass);
+        KMH_ST(2)
         lds_barrier();
-        // exclusive scan of the pass histogram
-        uint32_t n0 = 0u, incl = 0u;
-        if (tid < kMaxPasses) {
-            n0 = hist[tid];
-            incl = n0;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t t = __shfl_up(incl, d);
-                if (lane >= d) incl += t;
+        KMH_ST(3)
+        // exclusive scan of the counters (pass-major): thread t owns counters 4t .. 4t + 3
+        // (replicated) or counter t; pass p starts at counter 32p (thread 8p) or p
+        {
+            uint4 cv = make_uint4(0u, 0u, 0u, 0u);
+            if (rep) {
+                if ((uint32_t)tid < np * 8u) cv = hist4[tid];
+            } else {
+                cv.x = hist[tid];
             }
+            const uint32_t sm = cv.x + cv.y + cv.z + cv.w;
+            const uint32_t incl = scan64(sm);
             if (lane == 63) wsum[wave] = incl;
-        }
-        lds_barrier();
-        if (tid < kMaxPasses) {
-            uint32_t pre = 0u;
-            for (int w = 0; w < wave; ++w) pre += wsum[w];
-            const uint32_t st = pre + incl - n0;
-            hist[tid] = st;
-            if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)st;
-            if (tid == 0) {
-                uint32_t tot = 0u;
+            lds_barrier();
+            uint32_t pre = 0u, tot = 0u;
 #pragma unroll
-                for (int w = 0; w < kMaxPasses / 64; ++w) tot += wsum[w];
+            for (int w = 0; w < kNW; ++w) {
+                const uint32_t x = wsum[w];
+                pre += w < wave ? x : 0u;
+                tot += x;
+            }
+            const uint32_t ex = pre + incl - sm;
+            if (rep) {
+                if ((uint32_t)tid < np * 8u) {
+                    hist4[tid] = make_uint4(ex, ex + cv.x, ex + cv.x + cv.y, ex + cv.x + cv.y + cv.z);
+                    if ((tid & 7) == 0) toff2[(uint64_t)item * kT2 + (uint32_t)tid / 8u] = (uint16_t)ex;
+                }
+            } else {
+                hist[tid] = ex;
+                if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)ex;
+            }
+            if (tid == 0) {
                 total_sh = tot;
                 toff2[(uint64_t)item * kT2 + np] = (uint16_t)(tot <= (uint32_t)kCaps ? tot : 0u);
                 if (tot > (uint32_t)kCaps) gb_fail[cur.gb] = 1u;   // staging overflow: the bucket goes to the fallback
             }
         }
         lds_barrier();
+        KMH_ST(4)
         const uint32_t total = total_sh;
         const bool fits = total <= (uint32_t)kCaps;   // uniform
         if (fits) {
             auto scatter = [&](E r, uint32_t p, bool ok) {
-                const uint32_t slot = atomicAdd(&hist[ok ? pass_of(r, np, R) : dpass], 1u);
+                const uint32_t slot = atomicAdd(&hist[ctr(r, ok)], 1u);
                 const uint32_t at = ok ? slot : (uint32_t)kCaps + (uint32_t)lane;
                 sorted[at] = r;
                 if constexpr (POS) spos[at] = p;
@@ -682,12 +719,15 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             if (hc.kept) each_held<E, POS>(hc, scatter);
             else walk_bucket<POS>(ent, epos, toff, ldt, cur.b, cur.t0, cur.t1, bt, q[wave], slo[wave], shi[wave], scatter);
         }
+        KMH_ST(5)
         lds_barrier();
+        KMH_ST(6)
 
         // A and B have landed by now (waited for here, not behind D's stores)
         if constexpr (kPipe) landed(hn);
         asm volatile("" ::"v"(lo_nn), "v"(hi_nn));
-        if (tid < kMaxPasses) hist[tid] = 0u;   // the cursors are dead; the next item starts after a barrier
+        KMH_ST(7)
+        hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next item starts after a barrier
 
         // (D) this item's stores
         if (fits) {
@@ -703,19 +743,28 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                 if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
             }
         }
+        KMH_ST(8)
         if (!has_n) break;
         lds_barrier();   // zeroed histogram visible; the staging's reads done before the next scatter
+        KMH_ST(9)
         item = nitem;
         cur = nxt;
         if constexpr (kPipe) hc = hn;
         nitem = nnitem;
         has_n = has_nn;
         nxt = nn;
+        nn = nnn;
         lo_c = lo_n;
         hi_c = hi_n;
         lo_n = lo_nn;
         hi_n = hi_nn;
     }
+#ifdef KMH_EXPERIMENTS
+    if (lane == 0) {
+        for (int i = 0; i < 10; ++i) atomicAdd(&g_split_prof[i], st_[i]);
+        atomicAdd(&g_split_prof[15], 1ull);
+    }
+#endif
 }
 
 // Count work item: pass p of bucket b of genome g; its entries are segment p of split items
@@ -920,7 +969,12 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     const CountItem it = items[item];
     if (gb_fail[it.gb]) continue;  // the split overflowed: the fallback counts this bucket
     const uint32_t np = it.np;
-    auto bin_of = [&](E r) -> uint32_t { return (uint32_t)((((uint64_t)r * np) & RMK) >> SH); };
+    // bin = top 13 bits of (r * np) mod 2^R; u32 residues: (r << (32 - R)) * np mod 2^32 is that
+    // value shifted to the top of a word (one 32-bit multiply)
+    auto bin_of = [&](E r) -> uint32_t {
+        if constexpr (sizeof(E) == 4) return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
+        else return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
+    };
 
     // f(key) for every key of the item.  Per group of up to 64 split items every wave reads the
     // segment bounds (lane j: split item g + j), scans their lengths and takes an equal share
@@ -1587,6 +1641,20 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
                            d_sitems, (uint32_t)nsi, R, d_split, d_spos, d_toff2, d_gbfail);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
+#ifdef KMH_EXPERIMENTS
+        if (env_long("KMH_SP_PROF", 0) == 1) {
+            unsigned long long h[16];
+            KMH_HIP(ctx, hipStreamSynchronize(s));
+            KMH_HIP(ctx, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_split_prof), sizeof(h)));
+            const double w = (double)h[15];
+            std::fprintf(stderr, "k_sp_split per wave over %zu items on %u WGs (Mcyc): A hold %.2f | B bounds %.2f | "
+                         "hist %.2f | bar %.2f | scan %.2f | scatter %.2f | bar %.2f | landed %.2f | stores %.2f | "
+                         "bar %.2f\n", nsi, sgrid, h[0] / w / 1e6, h[1] / w / 1e6, h[2] / w / 1e6, h[3] / w / 1e6,
+                         h[4] / w / 1e6, h[5] / w / 1e6, h[6] / w / 1e6, h[7] / w / 1e6, h[8] / w / 1e6, h[9] / w / 1e6);
+            const unsigned long long z[16] = {};
+            KMH_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_split_prof), z, sizeof(z)));
+        }
+#endif
         time_begin(ctx, s, "k_sp_count");
         const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
         hipLaunchKernelGGL((k_sp_count<E, POS>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_toff2,
