@@ -65,6 +65,11 @@ const char* kmh_build_id(void);
  * an empty device workspace.  Replaces nothing in the reference (it has no device). */
 int kmh_ctx_create(int device, kmh_ctx** out);
 void kmh_ctx_destroy(kmh_ctx* ctx);
+/* Free the context's cached device workspace and pinned staging (they grow to the largest
+ * call: tens of GB after a config-5 batch) after waiting for the work queued on the null
+ * stream and the context stream; the next call allocates again.  For long-lived processes
+ * that hand the device to other work.  Replaces nothing in the reference. */
+int kmh_ctx_release(kmh_ctx* ctx);
 
 /* Last error message of `ctx`, or of the calling thread's context-free calls when
  * ctx == NULL.  Never NULL; "" when there was no error. */

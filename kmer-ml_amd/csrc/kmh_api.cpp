@@ -147,15 +147,38 @@ int kmh_ctx_create(int device, kmh_ctx** out) {
     return KMH_OK;
 }
 
+// Every cached device buffer and the pinned staging (after the queued work that may read them).
+static void free_workspace(kmh_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipDeviceSynchronize();
+    auto drop = [](kmh::DevBuf& b) {
+        if (b.ptr) (void)hipFree(b.ptr);
+        b.ptr = nullptr;
+        b.bytes = 0;
+    };
+    for (kmh::DevBuf* b : {&ctx->seq, &ctx->suf, &ctx->toff, &ctx->meta, &ctx->out, &ctx->out2, &ctx->fix,
+                           &ctx->redo, &ctx->order, &ctx->sort_tmp, &ctx->scan_tmp, &ctx->first})
+        drop(*b);
+    for (auto& b : ctx->sparse) drop(b);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_bytes = 0;
+}
+
+int kmh_ctx_release(kmh_ctx* ctx) {
+    if (!ctx) {
+        kmh::set_thread_error("kmh_ctx_release: ctx is NULL");
+        return KMH_ERR_INVALID;
+    }
+    KMH_HIP(ctx, hipSetDevice(ctx->device));
+    free_workspace(ctx);
+    return KMH_OK;
+}
+
 void kmh_ctx_destroy(kmh_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-    for (kmh::DevBuf* b : {&ctx->seq, &ctx->suf, &ctx->toff, &ctx->meta, &ctx->out, &ctx->out2, &ctx->fix})
-        if (b->ptr) (void)hipFree(b->ptr);
-    for (auto& b : ctx->sparse)
-        if (b.ptr) (void)hipFree(b.ptr);
-    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    free_workspace(ctx);
     if (ctx->pinned_ready) (void)hipEventDestroy(ctx->pinned_ready);
     for (auto& t : ctx->launches) {
         if (t.start) (void)hipEventDestroy(t.start);

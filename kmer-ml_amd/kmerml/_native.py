@@ -34,6 +34,7 @@ SIGNATURES = [
     ("kmh_build_id", _c.c_char_p, []),
     ("kmh_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_vp)]),
     ("kmh_ctx_destroy", None, [_vp]),
+    ("kmh_ctx_release", _c.c_int, [_vp]),
     ("kmh_last_error", _c.c_char_p, [_vp]),
     ("kmh_timing_enable", _c.c_int, [_vp, _c.c_int]),
     ("kmh_timing_report", _c.c_int, [_vp, _c.POINTER(_c.c_char_p), _u64p,
@@ -153,6 +154,11 @@ class Context:
         if self._h:
             lib().kmh_ctx_destroy(self._h)
             self._h = None
+
+    def release(self):
+        """Free the cached device workspace (kmh_ctx_release); the next call allocates again."""
+        if self._h:
+            _check(lib().kmh_ctx_release(self._h), self._h)
 
     def __del__(self):
         try:
@@ -284,6 +290,15 @@ def context(device=0):
             ctx = Context(device)
             _contexts[device] = ctx
     return ctx
+
+
+def release_all():
+    """kmh_ctx_release on every process-wide context (before handing the GPU to other
+    processes, e.g. ranks started on the same device)."""
+    with _ctx_lock:
+        ctxs = list(_contexts.values())
+    for c in ctxs:
+        c.release()
 
 
 def _as_u8(seq):

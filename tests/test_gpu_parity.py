@@ -733,9 +733,16 @@ def test_sparse_dev_rejects_k(ctx, dev, k):
 
 # ---------------------------------------------------------------- RCCL code paths, one GPU
 def _torchrun(args, timeout=600, nproc=1, env=None):
+    import gc
     import socket
     import subprocess
     import sys
+    # the ranks share this process's GPU: hand back what earlier tests left in torch's
+    # caching allocator (the config-5 batch tests cache ~100 GB), or eight ranks of config 4
+    # (~22 GiB each) run out of the 288 GB; the library's contexts cache tens of GB more
+    _native.release_all()
+    gc.collect()
+    torch.cuda.empty_cache()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
