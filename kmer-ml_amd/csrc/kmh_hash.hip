@@ -910,6 +910,18 @@ __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks 
 #define KMH_PT(i)
 #endif
 
+// Persistent, two workgroups per CU; XCD x (= blockIdx % 8) takes a contiguous run of the
+// items (the passes of a bucket read neighbouring segments and the same toff2 lines, which then
+// meet in one L2) and its workgroups stride through it.  Software-pipelined over items, so that
+// no global latency is waited for inside an item: the keys of item i + 1 are loaded into
+// registers right after item i's scatter (its own keys are dead then) and land during item i's
+// emission; they are counted into the histogram (cleared behind the emission) before item i's
+// output stores are issued, so the wait for them never queues behind those stores (loads and
+// stores share one in-order counter); segment bounds are loaded one item ahead of their keys
+// and descriptors one item ahead of their bounds; the output base (one global atomic per item)
+// returns during the next item's histogram.  Item i's keys are re-read from `sorted` for its
+// stores (still intact: item i + 1's scatter comes after them), so a lane holds only the next
+// item's keys, its emission flags and its packed counts across the phases.
 template <typename E, bool POS>
 __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_count(
     const E* __restrict__ split, const uint32_t* __restrict__ opos, const uint16_t* __restrict__ toff2,
@@ -924,10 +936,14 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #endif
     constexpr int kCaps = Sp<E, POS>::CAPS, U = KMH_SP_CU;
     constexpr bool WIDE = sizeof(E) == 8;
-    static_assert(BPT % 4 == 0 && HPT >= 1 && C % NT == 0, "thread layout");
-    __shared__ __attribute__((aligned(16))) uint32_t hist[kBins];
-    __shared__ __attribute__((aligned(16))) E sorted[C];
-    __shared__ uint32_t spos[POS ? C : 1];          // positions of sorted[] (POS)
+    constexpr int KPL = C / NT;          // keys per lane of a single-group item
+    constexpr int ECW = (KPL + 3) / 4;   // words of a lane's emission counts, 8 bits each (<= kBig)
+    static_assert(BPT % 4 == 0 && HPT >= 1 && C % NT == 0 && KPL <= 32 && kBig < 256, "thread layout");
+    // + 32 dummy counters and a 64-entry scratch tail: a lane past its keys adds to a dummy and
+    // scatters into the tail, so no exec-mask branch surrounds the atomics of a key
+    __shared__ __attribute__((aligned(16))) uint32_t hist[kBins + 32];
+    __shared__ __attribute__((aligned(16))) E sorted[C + 64];
+    __shared__ uint32_t spos[POS ? C + 64 : 1];     // positions of sorted[] (POS)
     __shared__ uint32_t hmin[POS ? kHSlots : 1];    // first position of each big-bin slot (POS)
     __shared__ unsigned long long htab[kHSlots];
     __shared__ uint32_t bigl[kMaxBig];
@@ -944,6 +960,13 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     const int SH = R - kBinBits;                         // R >= 16
     const uint32_t cap = limit < (uint32_t)C ? limit : (uint32_t)C;
 
+    const uint32_t x = blockIdx.x % 8u, nwg = gridDim.x;
+    const uint32_t nwx = (nwg - x + 7u) / 8u;                      // workgroups on XCD x
+    const uint32_t iq = nitems / 8u, irem = nitems % 8u;
+    const uint32_t xa = x * iq + (x < irem ? x : irem), xb = xa + iq + (x < irem ? 1u : 0u);
+    uint32_t item = xa + blockIdx.x / 8u;
+    if (item >= xb) return;   // whole workgroup
+
     uint4* h4 = reinterpret_cast<uint4*>(hist);
     auto zero_bins = [&] {
 #pragma unroll
@@ -957,49 +980,112 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         for (int q = 0; q < HPT; ++q) hmin[q * NT + tid] = 0xFFFFFFFFu;
     }
     if (tid == 0) nbig = bad = 0u;
-    lds_barrier();
-#ifdef KMH_EXPERIMENTS
-    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = clock64();
-#endif
 
-    // Persistent: the workgroups walk the items.  Every branch on item data below is
-    // workgroup-uniform (the values come from LDS after a barrier or are computed alike by
-    // every wave), so all threads meet the same barriers.
-    for (uint32_t item = blockIdx.x; item < nitems; item += gridDim.x) {
-    const CountItem it = items[item];
-    if (gb_fail[it.gb]) continue;  // the split overflowed: the fallback counts this bucket
-    const uint32_t np = it.np;
     // bin = top 13 bits of (r * np) mod 2^R; u32 residues: (r << (32 - R)) * np mod 2^32 is that
     // value shifted to the top of a word (one 32-bit multiply)
-    auto bin_of = [&](E r) -> uint32_t {
+    auto bin_of = [&](E r, uint32_t np) -> uint32_t {
         if constexpr (sizeof(E) == 4) return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
         else return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
     };
 
-    // f(key) for every key of the item.  Per group of up to 64 split items every wave reads the
-    // segment bounds (lane j: split item g + j), scans their lengths and takes an equal share
-    // of the group's entries (concatenated in split-item order: entry e lies in the last
-    // segment whose exclusive start is <= e), U loads of 64 entries in flight.  Returns the
-    // item's key count.
-    auto walk = [&](auto&& f) -> uint32_t {
+    // An item as loaded: its descriptor and the gb_fail flag of its bucket (a pass of a bucket
+    // whose split overflowed is left to the fallback: it counts as an item without keys).
+    // Used an item after it was loaded, so the scalar loads have landed.
+    struct Desc {
+        CountItem c;
+        uint32_t skip;
+    };
+    auto load_desc = [&](uint32_t i) {
+        Desc d;
+        d.c = items[i];
+        d.skip = gb_fail[d.c.gb];
+        return d;
+    };
+    // split items of the item's group (0 for a skipped item); single: at most one group of 64
+    auto nseg = [&](const Desc& d) -> uint32_t { return d.skip ? 0u : d.c.s1 - d.c.s0; };
+    // this lane's segment [lo, hi) of split item s0 + lane of a single-group item; the loads are
+    // unconditional (entry 0 for lanes past the group) and masked where they are used
+    struct Bnd {
+        uint32_t lo, hi;
+    };
+    auto load_bounds = [&](const Desc& d) {
+        const uint32_t ns = nseg(d);
+        const bool in = ns <= 64u && (uint32_t)lane < ns;
+        const uint64_t r = in ? (uint64_t)(d.c.s0 + (uint32_t)lane) * kT2 + d.c.p : 0u;
+        Bnd b;
+        b.lo = toff2[r];
+        b.hi = toff2[r + (in ? 1u : 0u)];
+        return b;
+    };
+
+    // Issues the loads of a single-group item's keys into kr / kp (every lane's share of at most
+    // KPL keys, all in flight, nobody waits for them here; segment lookup by wave-uniform
+    // shuffles) and returns the item's key count (0 for a multi-group item, which walk() counts).
+    auto issue_keys = [&](const Desc& d, const Bnd& bd, E (&kr)[KPL], uint32_t (&kp)[POS ? KPL : 1],
+                          uint32_t& kn) -> uint32_t {
+        kn = 0u;
+        const uint32_t ns = nseg(d);
+        if (ns > 64u) return 0u;   // uniform
+        const uint32_t in = (uint32_t)lane < ns ? 1u : 0u;
+        const uint32_t lo = in ? bd.lo : 0u, len = in ? bd.hi - bd.lo : 0u;
+        const uint32_t incl = scan64(len);
+        const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63), excl = incl - len;
+        const uint64_t sb = (uint64_t)(d.c.s0 + (uint32_t)lane) * kCaps + lo - excl;   // segment base - its start
+        const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
+        const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
+        const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
+        if (n <= (uint32_t)C && ea < eb) {
+#pragma unroll
+            for (int u = 0; u < KPL; ++u) {
+                const uint32_t e0 = ea + 64u * (uint32_t)u;
+                const uint32_t e = e0 + (uint32_t)lane;
+                kn += e < eb ? 1u : 0u;
+                // lanes past the share read a valid entry (lane 0's, or entry ea)
+                const uint32_t e1 = e0 < eb ? e0 : ea;
+                const uint32_t es = e < eb ? e : e1;
+                // the 64 entries [e0, e0 + 63] lie in segments s0 .. s1 (wave-uniform, almost
+                // always one or two): each lane takes the last of them whose start is <= its
+                // entry, with the segments' starts and bases read by v_readlane (no LDS-pipe
+                // shuffles: ds_bpermute would compete with the item's LDS atomics)
+                const uint32_t el = e0 < eb ? min(e0 + 63u, eb - 1u) : ea;
+                const int s0 = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
+                const int s1 = __popcll(__ballot((uint32_t)lane < ns && excl <= el)) - 1;
+                uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)sb_lo, s0);
+                uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)sb_hi, s0);
+                for (int sx = s0 + 1; sx <= s1; ++sx) {
+                    const uint32_t xs = (uint32_t)__builtin_amdgcn_readlane((int)excl, sx);
+                    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)sb_lo, sx);
+                    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)sb_hi, sx);
+                    blo = es >= xs ? l : blo;
+                    bhi = es >= xs ? h : bhi;
+                }
+                const uint64_t base = ((uint64_t)bhi << 32) | blo;
+                kr[u] = split[base + es];
+                if constexpr (POS) kp[u] = opos[base + es];
+            }
+        }
+        return n;
+    };
+
+    // f(key, position, true) for every key of a multi-group item (and f(x, p, false) for idle lanes) (a bucket of more than 64 split
+    // items: organisms of >= ~0.8 G windows), read from memory: per group of 64 split items
+    // every wave reads the segment bounds (lane j: split item g + j), scans their lengths and
+    // takes an equal share of the group's entries, U loads of 64 entries in flight.  Returns
+    // the item's key count.
+    auto walk = [&](const Desc& d, auto&& f) -> uint32_t {
         uint32_t ntot = 0u;
-        for (uint32_t g = it.s0; g < it.s1; g += 64u) {
-            const uint32_t ns = min(64u, it.s1 - g);
+        for (uint32_t g = d.c.s0; g < d.c.s1; g += 64u) {
+            const uint32_t ns = min(64u, d.c.s1 - g);
             const uint32_t j = g + (uint32_t)lane;
             uint32_t lo = 0u, len = 0u;
             if ((uint32_t)lane < ns) {
-                lo = toff2[(uint64_t)j * kT2 + it.p];
-                len = (uint32_t)toff2[(uint64_t)j * kT2 + it.p + 1] - lo;
+                lo = toff2[(uint64_t)j * kT2 + d.c.p];
+                len = (uint32_t)toff2[(uint64_t)j * kT2 + d.c.p + 1] - lo;
             }
-            uint32_t incl = len;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t x = __shfl_up(incl, d);
-                if (lane >= d) incl += x;
-            }
-            const uint32_t n = __shfl(incl, 63), excl = incl - len;
+            const uint32_t incl = scan64(len);
+            const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63), excl = incl - len;
             ntot += n;
-            const uint64_t sb = (uint64_t)j * kCaps + lo - excl;   // segment base - its start
+            const uint64_t sb = (uint64_t)j * kCaps + lo - excl;
             const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
             const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
             const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
@@ -1009,10 +1095,9 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 bool ok[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const uint32_t e0 = c + 64u * (uint32_t)u;   // entry of lane 0
+                    const uint32_t e0 = c + 64u * (uint32_t)u;
                     const uint32_t e = e0 + (uint32_t)lane;
                     ok[u] = e < eb;
-                    // lanes past the share read a valid entry (lane 0's, or entry c)
                     const uint32_t e1 = e0 < eb ? e0 : c;
                     const uint32_t es = ok[u] ? e : e1;
                     int sj = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
@@ -1027,304 +1112,332 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     r[u] = split[base + es];
                     rp[u] = POS ? opos[base + es] : 0u;
                 }
+                // every lane consumes every load (f is branch-free: ok selects a dummy), so no
+                // load of the walk is left in flight on any path
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (ok[u]) f(r[u], rp[u]);
+                for (int u = 0; u < U; ++u) f(r[u], rp[u], ok[u]);
             }
         }
         return ntot;
     };
 
-    // 1. histogram of the bins.  An item of at most 64 split items (all but items of huge
-    //    buckets) is read once: every wave's share (<= C / kNW keys) is loaded in one round
-    //    of KPL loads per lane and kept in registers for the scatter.
-    constexpr int KPL = C / NT;                 // keys per lane of a single-group share
-    const bool single = it.s1 - it.s0 <= 64u;   // uniform
+    // the histogram of an item: from the registers (single group) or walked from memory
+    const uint32_t kDummy = (uint32_t)kBins + (uint32_t)(lane & 31);
     E kr[KPL];
-    uint32_t kp[POS ? KPL : 1];                 // their positions (POS)
-    uint32_t kn = 0u;                           // valid keys of this lane (a prefix of kr)
-    uint32_t ntot;
-    if (single) {
-        const uint32_t ns = it.s1 - it.s0;
-        const uint32_t j = it.s0 + (uint32_t)lane;
-        uint32_t lo = 0u, len = 0u;
-        if ((uint32_t)lane < ns) {
-            lo = toff2[(uint64_t)j * kT2 + it.p];
-            len = (uint32_t)toff2[(uint64_t)j * kT2 + it.p + 1] - lo;
-        }
-        uint32_t incl = len;
+    uint32_t kp[POS ? KPL : 1];
+    uint32_t kn = 0u;   // valid keys of this lane (a prefix of kr)
+    auto count_keys = [&](const Desc& d, uint32_t n_single) -> uint32_t {
+        if (nseg(d) <= 64u) {   // uniform
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
+            for (int u = 0; u < KPL; ++u) atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], d.c.np) : kDummy], 1u);
+            return n_single;
         }
-        const uint32_t n = __shfl(incl, 63), excl = incl - len;
-        ntot = n;
-        const uint64_t sb = (uint64_t)j * kCaps + lo - excl;
-        const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
-        const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
-        const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
-        if (n <= (uint32_t)C && ea < eb) {
+        return walk(d, [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ok ? bin_of(r, d.c.np) : kDummy], 1u); });
+    };
+
+    // makes the wave wait for the loads into kr / kp on every path (the compiler waits before
+    // an asm statement that reads a register whose load is in flight)
+    auto landed_keys = [&] {
 #pragma unroll
-            for (int u = 0; u < KPL; ++u) {
-                const uint32_t e0 = ea + 64u * (uint32_t)u;
-                const uint32_t e = e0 + (uint32_t)lane;
-                kn += e < eb ? 1u : 0u;
-                const uint32_t e1 = e0 < eb ? e0 : ea;
-                const uint32_t es = e < eb ? e : e1;
-                int sj = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
-                for (;;) {
-                    const uint32_t nx = __shfl(excl, sj < 63 ? sj + 1 : 63);
-                    const bool adv = sj + 1 < (int)ns && nx <= es;
-                    if (!__ballot(adv)) break;
-                    sj += adv ? 1 : 0;
+        for (int u = 0; u < KPL; ++u) {
+            asm volatile("" : "+v"(kr[u]));
+            if constexpr (POS) asm volatile("" : "+v"(kp[u]));
+        }
+    };
+
+    // prologue: descriptors of the first three items, bounds of the first two, keys and
+    // histogram of the first
+    Desc cur = load_desc(item);
+    uint32_t nitem = item + nwx;
+    bool has_n = nitem < xb;
+    Desc nxt = load_desc(has_n ? nitem : item);
+    uint32_t nnitem = nitem + nwx;
+    bool has_nn = has_n && nnitem < xb;
+    Desc nn = load_desc(has_nn ? nnitem : item);
+    Bnd bc = load_bounds(cur);
+    Bnd bn = load_bounds(nxt);
+    uint32_t ntot = issue_keys(cur, bc, kr, kp, kn);
+    lds_barrier();   // cleared state visible
+    ntot = count_keys(cur, ntot);
+    landed_keys();
+    asm volatile("" ::"v"(bn.lo), "v"(bn.hi));
+    lds_barrier();
+#ifdef KMH_EXPERIMENTS
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = clock64();
+#endif
+
+    // Every branch on item data below is workgroup-uniform (descriptor fields, LDS values read
+    // after a barrier, or wave totals), so all threads meet the same barriers.
+    for (;;) {
+        const uint32_t np = cur.c.np;
+        const uint64_t obo = out_off[cur.c.g];  // (scalar; lands by the first barrier)
+        const bool over = ntot > (uint32_t)C;   // more keys than the staging holds: fallback
+        // 1. exclusive scan: thread t owns bins 16t .. 16t + 15; bins of more than kBig keys are
+        //    listed; bin b's counter becomes start | start << 16.  2. scatter: the returning add
+        //    of 1 << 16 hands each key its slot, so hist[b] ends as start | end << 16 (one read
+        //    gives a bin's range; starts and ends <= C < 2^16)
+        if (!over) {
+            uint32_t v[BPT];
+#pragma unroll
+            for (int q = 0; q < BQ; ++q) {
+                const uint4 a = h4[BQ * tid + q];
+                v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+            }
+            uint32_t tsum = 0u;
+#pragma unroll
+            for (int i = 0; i < BPT; ++i) tsum += v[i];
+            const uint32_t incl = scan64(tsum);
+            if (lane == 63) wtot[wave] = incl;
+#pragma unroll
+            for (int i = 0; i < BPT; ++i) {
+                if (v[i] > (uint32_t)kBig) {
+                    const uint32_t at = atomicAdd(&nbig, 1u);
+                    if (at < (uint32_t)kMaxBig) bigl[at] = (uint32_t)(BPT * tid + i);
                 }
-                const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
-                                      (uint32_t)__shfl((int)sb_lo, sj);
-                kr[u] = split[base + es];
-                if constexpr (POS) kp[u] = opos[base + es];
             }
+            lds_barrier();
+            uint32_t st = incl - tsum;
+            for (int w = 0; w < wave; ++w) st += wtot[w];
+            {
+                uint32_t o[BPT];
 #pragma unroll
-            for (int u = 0; u < KPL; ++u)
-                if ((uint32_t)u < kn) atomicAdd(&hist[bin_of(kr[u])], 1u);
-        }
-    } else {
-        ntot = walk([&](E r, uint32_t) { atomicAdd(&hist[bin_of(r)], 1u); });
-    }
-    KMH_PT(0)
-    lds_barrier();
-    KMH_PT(1)
-    if (ntot > (uint32_t)C) {   // more keys than the staging holds: fallback (uniform)
-        zero_bins();
-        if (tid == 0) {
-            const uint32_t at = atomicAdd(&failed[0], 1u);
-            failed[1 + at] = item;
-        }
-        lds_barrier();
-        continue;
-    }
-
-    // 2. exclusive scan: thread t owns bins 8t .. 8t + 7; bins of more than kBig keys are listed
-    uint32_t v[BPT];
+                for (int i = 0; i < BPT; ++i) {
+                    o[i] = st;
+                    st += v[i];
+                }
 #pragma unroll
-    for (int q = 0; q < BQ; ++q) {
-        const uint4 a = h4[BQ * tid + q];
-        v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
-    }
-    uint32_t tsum = 0u;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) tsum += v[i];
-    uint32_t incl = tsum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t x = __shfl_up(incl, d);
-        if (lane >= d) incl += x;
-    }
-    if (lane == 63) wtot[wave] = incl;
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-        if (v[i] > (uint32_t)kBig) {
-            const uint32_t at = atomicAdd(&nbig, 1u);
-            if (at < (uint32_t)kMaxBig) bigl[at] = (uint32_t)(BPT * tid + i);
-        }
-    }
-    lds_barrier();
-    uint32_t st = incl - tsum;
-    for (int w = 0; w < wave; ++w) st += wtot[w];
-    {
-        uint32_t o[BPT];
-#pragma unroll
-        for (int i = 0; i < BPT; ++i) {
-            o[i] = st;
-            st += v[i];
-        }
-#pragma unroll
-        for (int q = 0; q < BQ; ++q) h4[BQ * tid + q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-    }
-    lds_barrier();
-    KMH_PT(2)
-
-    // 3. scatter: hist[b] ends as the end of bin b
-    if (single) {
-#pragma unroll
-        for (int u = 0; u < KPL; ++u)
-            if ((uint32_t)u < kn) {
-                const uint32_t at = atomicAdd(&hist[bin_of(kr[u])], 1u);
-                sorted[at] = kr[u];
-                if constexpr (POS) spos[at] = kp[u];
+                for (int q = 0; q < BQ; ++q)
+                    h4[BQ * tid + q] = make_uint4(o[4 * q] * 0x10001u, o[4 * q + 1] * 0x10001u, o[4 * q + 2] * 0x10001u,
+                                                  o[4 * q + 3] * 0x10001u);
             }
-    } else {
-        walk([&](E r, uint32_t p) {
-            const uint32_t at = atomicAdd(&hist[bin_of(r)], 1u);
-            sorted[at] = r;
-            if constexpr (POS) spos[at] = p;
-        });
-    }
-    lds_barrier();
-    KMH_PT(3)
-    const uint32_t nb = nbig;
+            lds_barrier();
+            KMH_PT(0)
+            if (nseg(cur) <= 64u) {
+#pragma unroll
+                for (int u = 0; u < KPL; ++u) {
+                    const bool ok = (uint32_t)u < kn;
+                    const uint32_t slot = atomicAdd(&hist[ok ? bin_of(kr[u], np) : kDummy], 0x10000u) >> 16;
+                    const uint32_t at = ok ? slot : (uint32_t)C + (uint32_t)lane;
+                    sorted[at] = kr[u];
+                    if constexpr (POS) spos[at] = kp[u];
+                }
+            } else {
+                walk(cur, [&](E r, uint32_t p, bool ok) {
+                    const uint32_t slot = atomicAdd(&hist[ok ? bin_of(r, np) : kDummy], 0x10000u) >> 16;
+                    const uint32_t at = ok ? slot : (uint32_t)C + (uint32_t)lane;
+                    sorted[at] = r;
+                    if constexpr (POS) spos[at] = p;
+                });
+            }
+            lds_barrier();
+        }
+        KMH_PT(1)
 
-    // 4. big bins: their keys into the hash table (linear probing, CAS(empty -> key|1), +1 on
-    //    a slot holding the key)
-    if (nb) {
-        if (nb > (uint32_t)kMaxBig) {
-            if (tid == 0) bad = 1u;
-        } else {
-            for (uint32_t x = 0; x < nb; ++x) {
-                const uint32_t b = bigl[x];
-                const uint32_t s = b ? hist[b - 1] : 0u, e = hist[b];
-                for (uint32_t i = s + (uint32_t)tid; i < e; i += NT) {
-                    const E key = sorted[i];
-                    uint32_t h = (uint32_t)key ^ (uint32_t)((uint64_t)key >> 29) * 0x9E3779B1u;
-                    h = (uint32_t)__umul24(h ^ (h >> 15), 0x9E3779u) >> (32 - 10);
-                    for (uint32_t probe = 0;; ++probe) {
-                        if (probe == (uint32_t)kHSlots) {
-                            bad = 1u;
-                            break;
+        // 3. this item's keys are dead: the next item's keys load behind this item's emission,
+        //    the bounds of the one after behind the next item, the descriptor after that behind
+        //    two items
+        uint32_t ntot_n = 0u;
+        if (has_n) ntot_n = issue_keys(nxt, bn, kr, kp, kn);
+        const Bnd bnn = load_bounds(nn);
+        const uint32_t nnnitem = nnitem + nwx;
+        const bool has_nnn = has_nn && nnnitem < xb;
+        const Desc nnn = load_desc(has_nnn ? nnnitem : item);
+        KMH_PT(2)
+
+        // 4. big bins: their keys into the hash table (linear probing, CAS(empty -> key|1), +1
+        //    on a slot holding the key)
+        const uint32_t nb = over ? 0u : nbig;
+        if (nb) {
+            if (nb > (uint32_t)kMaxBig) {
+                if (tid == 0) bad = 1u;
+            } else {
+                for (uint32_t xb2 = 0; xb2 < nb; ++xb2) {
+                    const uint32_t b = bigl[xb2];
+                    const uint32_t hb = hist[b], s = hb & 0xFFFFu, e = hb >> 16;
+                    for (uint32_t i = s + (uint32_t)tid; i < e; i += NT) {
+                        const E key = sorted[i];
+                        uint32_t h = (uint32_t)key ^ (uint32_t)((uint64_t)key >> 29) * 0x9E3779B1u;
+                        h = (uint32_t)__umul24(h ^ (h >> 15), 0x9E3779u) >> (32 - 10);
+                        for (uint32_t probe = 0;; ++probe) {
+                            if (probe == (uint32_t)kHSlots) {
+                                bad = 1u;
+                                break;
+                            }
+                            unsigned long long* slot = &htab[h];
+                            const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)key << CB) | 1ull);
+                            if (old == 0ull) {
+                                if constexpr (POS) atomicMin(&hmin[h], spos[i]);
+                                break;
+                            }
+                            if ((E)(old >> CB) == key) {
+                                const unsigned long long prev = atomicAdd(slot, 1ull);
+                                if (WIDE && (prev & CM) == CM) bad = 1u;   // count field full
+                                if constexpr (POS) atomicMin(&hmin[h], spos[i]);
+                                break;
+                            }
+                            h = (h + 1u) & (uint32_t)(kHSlots - 1);
                         }
-                        unsigned long long* slot = &htab[h];
-                        const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)key << CB) | 1ull);
-                        if (old == 0ull) {
-                            if constexpr (POS) atomicMin(&hmin[h], spos[i]);
-                            break;
-                        }
-                        if ((E)(old >> CB) == key) {
-                            const unsigned long long prev = atomicAdd(slot, 1ull);
-                            if (WIDE && (prev & CM) == CM) bad = 1u;   // count field full
-                            if constexpr (POS) atomicMin(&hmin[h], spos[i]);
-                            break;
-                        }
-                        h = (h + 1u) & (uint32_t)(kHSlots - 1);
                     }
                 }
             }
+            lds_barrier();
         }
-        lds_barrier();
-    }
 
-    // 5. emission, position-parallel: the key at sorted position i (i = j * NT + tid, so a wave
-    //    reads 64 consecutive keys) is emitted if no earlier key of its bin equals it, with the
-    //    number of equal keys of the bin as its count (bins hold about one key: the loops run
-    //    zero or one times); keys of big bins are emitted from the hash table instead.  First
-    //    the flags and counts (kept in registers), then the item's output base, then the
-    //    stores, compacted per wave with ballot + mbcnt so that they are coalesced.
-    E ek[KPL];
-    uint32_t ec[KPL];
-    uint32_t ef[POS ? KPL : 1];   // first position of the key (POS): the minimum over its bin's copies
-    uint32_t fm = 0u;   // bit j: position j * NT + tid is emitted
+        // 5. emission flags, position-parallel: the key at sorted position i (i = j * NT + tid,
+        //    so a wave reads 64 consecutive keys) is emitted if no earlier key of its bin equals
+        //    it, with the number of equal keys of the bin as its count (bins hold about one key:
+        //    the loops run zero or one times); keys of big bins are emitted from the hash table
+        uint32_t fm = 0u;   // bit j: position j * NT + tid is emitted
+        uint32_t ecw[ECW];
+        uint32_t ef[POS ? KPL : 1];   // first position of the key (POS): the minimum over its bin's copies
 #pragma unroll
-    for (int jj = 0; jj < KPL; ++jj) {
-        const uint32_t i = (uint32_t)(jj * NT + tid);
-        const uint32_t ic = i < ntot ? i : 0u;
-        const E key = sorted[ic];
-        const uint32_t b = bin_of(key);
-        const uint32_t bs = b ? hist[b - 1] : 0u, be = hist[b];
-        bool first = i < ntot && be - bs <= (uint32_t)kBig;
-        uint32_t c = 1u;
-        uint32_t fp = POS ? spos[ic] : 0u;
-        // bins of up to 4 keys (all but a fraction of a percent): four independent reads, so
-        // the twelve positions of a thread overlap their LDS round trips; larger bins loop
+        for (int q = 0; q < ECW; ++q) ecw[q] = 0u;
+        uint32_t wmine = 0u;   // the wave's emitted keys
+        if (!over) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const uint32_t y = bs + (uint32_t)t;
-            const uint32_t yc = y < be ? y : bs;
-            const E o = sorted[yc];
-            first = first && !(y < i && o == key);
-            c += (y > i && y < be && o == key) ? 1u : 0u;
-            if constexpr (POS) fp = (y > i && y < be && o == key) ? min(fp, spos[yc]) : fp;
-        }
-        if (first && be - bs > 4u) {
-            for (uint32_t y = bs + 4u; y < be; ++y) {
-                const E o = sorted[y];
-                first = first && !(y < i && o == key);
-                c += (y > i && o == key) ? 1u : 0u;
-                if constexpr (POS) fp = (y > i && o == key) ? min(fp, spos[y]) : fp;
+            for (int jj = 0; jj < KPL; ++jj) {
+                const uint32_t i = (uint32_t)(jj * NT + tid);
+                const uint32_t ic = i < ntot ? i : 0u;
+                const E key = sorted[ic];
+                const uint32_t b = bin_of(key, np);
+                const uint32_t hb = hist[b], bs = hb & 0xFFFFu, be = hb >> 16;
+                bool first = i < ntot && be - bs <= (uint32_t)kBig;
+                uint32_t c = 1u;
+                uint32_t fp = POS ? spos[ic] : 0u;
+                // bins of up to 4 keys (all but a fraction of a percent): four independent
+                // reads, so the positions of a thread overlap their LDS round trips; a lane
+                // reads only its bin's other keys (most bins hold one key: few lanes per read)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t y = bs + (uint32_t)t;
+                    if (y < be && y != i) {
+                        const E o = sorted[y];
+                        first = first && !(y < i && o == key);
+                        c += (y > i && o == key) ? 1u : 0u;
+                        if constexpr (POS) fp = (y > i && o == key) ? min(fp, spos[y]) : fp;
+                    }
+                }
+                if (first && be - bs > 4u) {
+                    for (uint32_t y = bs + 4u; y < be; ++y) {
+                        const E o = sorted[y];
+                        first = first && !(y < i && o == key);
+                        c += (y > i && o == key) ? 1u : 0u;
+                        if constexpr (POS) fp = (y > i && o == key) ? min(fp, spos[y]) : fp;
+                    }
+                }
+                ecw[jj / 4] |= c << (8 * (jj % 4));
+                if constexpr (POS) ef[jj] = fp;
+                fm |= first ? (1u << jj) : 0u;
+            }
+#pragma unroll
+            for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
+            if (nb) {
+#pragma unroll
+                for (int q = 0; q < HPT; ++q) wmine += (uint32_t)__popcll(__ballot((htab[q * NT + tid] & CM) != 0ull));
             }
         }
-        ek[jj] = key;
-        ec[jj] = c;
-        if constexpr (POS) ef[jj] = fp;
-        fm |= first ? (1u << jj) : 0u;
-    }
-    unsigned long long hs[HPT];
-    uint32_t hf[POS ? HPT : 1];
+        KMH_PT(3)
+        if (lane == 0) wtot[wave] = wmine;
+        lds_barrier();   // (also: every read of hist, and of htab for the totals, is done)
+        uint32_t before = 0u, used = 0u;
 #pragma unroll
-    for (int q = 0; q < HPT; ++q) hs[q] = nb ? htab[q * NT + tid] : 0ull;
-    if constexpr (POS) {
-#pragma unroll
-        for (int q = 0; q < HPT; ++q) hf[q] = hmin[q * NT + tid];
-    }
-    uint32_t wmine = 0u;   // the wave's emitted keys
-#pragma unroll
-    for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
-#pragma unroll
-    for (int q = 0; q < HPT; ++q) wmine += (uint32_t)__popcll(__ballot((hs[q] & CM) != 0ull));
-    KMH_PT(4)
-    lds_barrier();   // everybody has read hist / htab / nbig of this item
-    if (lane == 0) wtot[wave] = wmine;
-    lds_barrier();
-    uint32_t before = 0u, used = 0u;
-#pragma unroll
-    for (int w = 0; w < kNW; ++w) {
-        const uint32_t x = wtot[w];
-        before += w < wave ? x : 0u;
-        used += x;
-    }
-    KMH_PT(5)
-    const bool fail_item = bad != 0u || used > cap;
-    if (tid == 0) {
-        if (fail_item) {
-            const uint32_t at = atomicAdd(&failed[0], 1u);
-            failed[1 + at] = item;
-        } else {
-            obase = atomicAdd(&nk[it.g], (unsigned long long)used);
+        for (int w = 0; w < kNW; ++w) {
+            const uint32_t xw = wtot[w];
+            before += w < wave ? xw : 0u;
+            used += xw;
         }
-    }
-    // clear this item's state for the next one (every read of it happened before the barrier above)
-    zero_bins();
-    if (nb) {
-#pragma unroll
-        for (int q = 0; q < HPT; ++q) htab[q * NT + tid] = 0ull;
-        if constexpr (POS) {
-#pragma unroll
-            for (int q = 0; q < HPT; ++q) hmin[q * NT + tid] = 0xFFFFFFFFu;
-        }
-    }
-    lds_barrier();
-    if (!fail_item) {
-        const uint64_t at = out_off[it.g] + obase + before;
-        const uint64_t hib = (uint64_t)it.b << R;
-        const uint64_t below = (1ull << lane) - 1ull;
-        uint32_t run = 0u;
-#pragma unroll
-        for (int jj = 0; jj < KPL; ++jj) {
-            const bool f = (fm >> jj) & 1u;
-            const uint64_t m = __ballot(f);
-            if (f) {
-                const uint64_t o = at + run + (uint32_t)__popcll(m & below);
-                out_store(codes + o, hib | (uint64_t)ek[jj]);
-                out_store(counts + o, ec[jj]);
-                if constexpr (POS) firsts[o] = ef[jj];
+        const bool fail_item = over || bad != 0u || used > cap;   // uniform
+        // the output base: one atomic per item, returning during the next item's histogram
+        // (its value is first used there: an add here would wait for it)
+        unsigned long long ob = 0ull;
+        if (tid == 0) {
+            if (fail_item) {
+                const uint32_t at = atomicAdd(&failed[0], 1u);
+                failed[1 + at] = item;
+            } else if (used) {
+                // (the address laundered through a VGPR: with a uniform address the compiler
+                // rewrites the atomic into a wave reduction whose result is waited for at once)
+                uint64_t pa = reinterpret_cast<uint64_t>(nk + cur.c.g);
+                asm volatile("" : "+v"(pa));
+                using g64 = __attribute__((address_space(1))) unsigned long long;   // global, not flat
+                ob = __hip_atomic_fetch_add(reinterpret_cast<g64*>(pa), (unsigned long long)used, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
             }
-            run += (uint32_t)__popcll(m);
         }
+        zero_bins();
+        KMH_PT(4)
+        lds_barrier();   // cleared bins visible; `bad` read by everybody
+
+        // 6. the next item's histogram (the wait for its keys), before this item's stores
+        if (has_n) ntot_n = count_keys(nxt, ntot_n);
+        // Everything loaded so far has landed here, on every path: the next item's keys (counted
+        // above, but only by the lanes that hold keys) and the bounds after them.  A load still
+        // in flight at the stores below would be waited for behind them later (one in-order
+        // counter: vmcnt(0) at a register copy or at the scatter).
+        landed_keys();
+        asm volatile("" ::"v"(bnn.lo), "v"(bnn.hi));
+        if (tid == 0) {
+            obase = ob + obo;
+            nbig = bad = 0u;
+        }
+        KMH_PT(5)
+        lds_barrier();
+
+        // 7. this item's stores, compacted per wave with ballot + mbcnt so that they are
+        //    coalesced; keys re-read from `sorted` (the next scatter comes after a barrier)
+        if (!fail_item && used) {   // uniform
+            const uint64_t at = obase + before;
+            const uint64_t hib = (uint64_t)cur.c.b << R;
+            const uint64_t below = (1ull << lane) - 1ull;
+            uint32_t run = 0u;
 #pragma unroll
-        for (int q = 0; q < HPT; ++q) {
-            const bool f = (hs[q] & CM) != 0ull;
-            const uint64_t m = __ballot(f);
-            if (f) {
-                const uint64_t o = at + run + (uint32_t)__popcll(m & below);
-                codes[o] = hib | (hs[q] >> CB);
-                counts[o] = (uint32_t)(hs[q] & CM);
-                if constexpr (POS) firsts[o] = hf[q];
+            for (int jj = 0; jj < KPL; ++jj) {
+                const bool f = (fm >> jj) & 1u;
+                const uint64_t m = __ballot(f);
+                if (f) {
+                    const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                    out_store(codes + o, hib | (uint64_t)sorted[jj * NT + tid]);
+                    out_store(counts + o, (ecw[jj / 4] >> (8 * (jj % 4))) & 0xFFu);
+                    if constexpr (POS) firsts[o] = ef[jj];
+                }
+                run += (uint32_t)__popcll(m);
             }
-            run += (uint32_t)__popcll(m);
+            if (nb) {
+#pragma unroll
+                for (int q = 0; q < HPT; ++q) {
+                    const unsigned long long hs = htab[q * NT + tid];
+                    const bool f = (hs & CM) != 0ull;
+                    const uint64_t m = __ballot(f);
+                    if (f) {
+                        const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                        codes[o] = hib | (hs >> CB);
+                        counts[o] = (uint32_t)(hs & CM);
+                        if constexpr (POS) firsts[o] = hmin[q * NT + tid];
+                    }
+                    run += (uint32_t)__popcll(m);
+                }
+            }
         }
-    }
-    KMH_PT(6)
-    if (tid == 0) nbig = bad = 0u;
-    lds_barrier();   // sorted / nbig are reused by the next item
-    KMH_PT(7)
+        if (nb) {   // cleared behind its last reads (this thread's); the next inserts follow barriers
+#pragma unroll
+            for (int q = 0; q < HPT; ++q) htab[q * NT + tid] = 0ull;
+            if constexpr (POS) {
+#pragma unroll
+                for (int q = 0; q < HPT; ++q) hmin[q * NT + tid] = 0xFFFFFFFFu;
+            }
+        }
+        KMH_PT(6)
+        if (!has_n) break;
+        item = nitem;
+        cur = nxt;
+        ntot = ntot_n;
+        nitem = nnitem;
+        has_n = has_nn;
+        nxt = nn;
+        bn = bnn;
+        nnitem = nnnitem;
+        has_nn = has_nnn;
+        nn = nnn;
     }
 #ifdef KMH_EXPERIMENTS
     if (lane == 0)
@@ -1668,8 +1781,8 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             KMH_HIP(ctx, hipStreamSynchronize(s));
             KMH_HIP(ctx, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sp_prof), sizeof(h)));
             const double w = (double)h[8] * kNW;   // waves
-            std::fprintf(stderr, "k_sp_count per wave over %zu items on %u WGs: load+hist %.0f | bar %.0f | scan %.0f | "
-                         "scatter %.0f | big %.0f | count %.0f | write %.0f | bar %.0f Mcyc\n", nci, (unsigned)h[8],
+            std::fprintf(stderr, "k_sp_count per wave over %zu items on %u WGs: scan %.0f | scatter %.0f | issue next %.0f | "
+                         "big+emission %.0f | totals+clear %.0f | next hist %.0f | stores %.0f | - %.0f Mcyc\n", nci, (unsigned)h[8],
                          h[0] / w / 1e6, h[1] / w / 1e6, h[2] / w / 1e6, h[3] / w / 1e6, h[4] / w / 1e6,
                          h[5] / w / 1e6, h[6] / w / 1e6, h[7] / w / 1e6);
             const unsigned long long z[16] = {};
