@@ -254,12 +254,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
 
         // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
         const uint32_t n0 = cnt[tid];
-        uint32_t incl = n0;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(incl, d);
-            if (lane >= d) incl += t;
-        }
+        const uint32_t incl = scan64(n0);   // DPP: no LDS-pipe shuffles
         if (lane == 63) wsum[wave] = incl;
         lds_barrier();
         uint32_t pre = 0u, total = 0u;
@@ -1213,11 +1208,15 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             lds_barrier();
             KMH_PT(0)
             if (nseg(cur) <= 64u) {
+                // all the returning adds first, then the stores (a store right behind its add
+                // waited for each add in turn)
+                uint32_t slot[KPL];
+#pragma unroll
+                for (int u = 0; u < KPL; ++u)
+                    slot[u] = atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], np) : kDummy], 0x10000u);
 #pragma unroll
                 for (int u = 0; u < KPL; ++u) {
-                    const bool ok = (uint32_t)u < kn;
-                    const uint32_t slot = atomicAdd(&hist[ok ? bin_of(kr[u], np) : kDummy], 0x10000u) >> 16;
-                    const uint32_t at = ok ? slot : (uint32_t)C + (uint32_t)lane;
+                    const uint32_t at = (uint32_t)u < kn ? slot[u] >> 16 : (uint32_t)C + (uint32_t)lane;
                     sorted[at] = kr[u];
                     if constexpr (POS) spos[at] = kp[u];
                 }
@@ -1294,40 +1293,72 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         for (int q = 0; q < ECW; ++q) ecw[q] = 0u;
         uint32_t wmine = 0u;   // the wave's emitted keys
         if (!over) {
+            // In phases over a group of HB positions, so that every phase's LDS reads are
+            // independent and issue back to back (position by position, each read waited for the
+            // one before: ~100 serial LDS round trips per item): (a) the keys, (b) their bins'
+            // ranges, (c) four rounds of one read per position -- the bin's key t, at an address
+            // clamped into the bin (most bins hold 1-3 keys), (d) bins of 5..kBig keys, rare, one
+            // by one.  Count of position jj (1 + equal keys after it): byte jj % 4 of ecw[jj / 4];
+            // first: bit jj of fm.  Groups of 4 positions (their 4 rounds' 16 reads in flight
+            // together) and sched_barriers between groups keep one group's values in registers
+            // (8-position groups, or all 16 positions hoisted together, spilled the next item's
+            // keys in flight).
+            constexpr int HB = KPL < 4 ? KPL : 4;
 #pragma unroll
-            for (int jj = 0; jj < KPL; ++jj) {
-                const uint32_t i = (uint32_t)(jj * NT + tid);
-                const uint32_t ic = i < ntot ? i : 0u;
-                const E key = sorted[ic];
-                const uint32_t b = bin_of(key, np);
-                const uint32_t hb = hist[b], bs = hb & 0xFFFFu, be = hb >> 16;
-                bool first = i < ntot && be - bs <= (uint32_t)kBig;
-                uint32_t c = 1u;
-                uint32_t fp = POS ? spos[ic] : 0u;
-                // bins of up to 4 keys (all but a fraction of a percent): four independent
-                // reads, so the positions of a thread overlap their LDS round trips; a lane
-                // reads only its bin's other keys (most bins hold one key: few lanes per read)
+            for (int q = 0; q < ECW; ++q) ecw[q] = 0x01010101u;
+#pragma unroll
+            for (int h0 = 0; h0 < KPL; h0 += HB) {
+                __builtin_amdgcn_sched_barrier(0);
+                E key[HB];
+                uint32_t rng[HB];   // bs | be << 16
+#pragma unroll
+                for (int x = 0; x < HB; ++x) {
+                    const uint32_t i = (uint32_t)((h0 + x) * NT + tid);
+                    key[x] = sorted[i < ntot ? i : 0u];
+                }
+#pragma unroll
+                for (int x = 0; x < HB; ++x) rng[x] = hist[bin_of(key[x], np)];
+#pragma unroll
+                for (int x = 0; x < HB; ++x) {
+                    const int jj = h0 + x;
+                    const uint32_t i = (uint32_t)(jj * NT + tid), bs = rng[x] & 0xFFFFu, be = rng[x] >> 16;
+                    fm |= (uint32_t)(i < ntot && be - bs <= (uint32_t)kBig) << jj;   // (shifts of 0/1:
+                    if constexpr (POS) ef[jj] = spos[i < ntot ? i : 0u];             //  no mask constants)
+                }
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const uint32_t y = bs + (uint32_t)t;
-                    if (y < be && y != i) {
-                        const E o = sorted[y];
-                        first = first && !(y < i && o == key);
-                        c += (y > i && o == key) ? 1u : 0u;
-                        if constexpr (POS) fp = (y > i && o == key) ? min(fp, spos[y]) : fp;
+                    E o[HB];
+#pragma unroll
+                    for (int x = 0; x < HB; ++x) {
+                        const uint32_t bs = rng[x] & 0xFFFFu, be = rng[x] >> 16, y = bs + (uint32_t)t;
+                        o[x] = sorted[y < be ? y : bs];
+                    }
+#pragma unroll
+                    for (int x = 0; x < HB; ++x) {
+                        const int jj = h0 + x;
+                        const uint32_t i = (uint32_t)(jj * NT + tid), be = rng[x] >> 16, y = (rng[x] & 0xFFFFu) + (uint32_t)t;
+                        const bool eq = y < be && o[x] == key[x];
+                        fm &= ~((uint32_t)(eq && y < i) << jj);
+                        ecw[jj / 4] += (uint32_t)(eq && y > i) << (8 * (jj % 4));
+                        if constexpr (POS) ef[jj] = (eq && y > i) ? min(ef[jj], spos[y]) : ef[jj];
                     }
                 }
-                if (first && be - bs > 4u) {
-                    for (uint32_t y = bs + 4u; y < be; ++y) {
-                        const E o = sorted[y];
-                        first = first && !(y < i && o == key);
-                        c += (y > i && o == key) ? 1u : 0u;
-                        if constexpr (POS) fp = (y > i && o == key) ? min(fp, spos[y]) : fp;
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int x = 0; x < HB; ++x) {
+                    const int jj = h0 + x;
+                    const uint32_t i = (uint32_t)(jj * NT + tid), bs = rng[x] & 0xFFFFu, be = rng[x] >> 16;
+                    if (((fm >> jj) & 1u) && be - bs > 4u) {
+                        bool first = true;
+                        for (uint32_t y = bs + 4u; y < be; ++y) {
+                            const E o = sorted[y];
+                            first = first && !(y < i && o == key[x]);
+                            ecw[jj / 4] += (uint32_t)(y > i && o == key[x]) << (8 * (jj % 4));
+                            if constexpr (POS) ef[jj] = (y > i && o == key[x]) ? min(ef[jj], spos[y]) : ef[jj];
+                        }
+                        fm &= ~((uint32_t)!first << jj);
                     }
                 }
-                ecw[jj / 4] |= c << (8 * (jj % 4));
-                if constexpr (POS) ef[jj] = fp;
-                fm |= first ? (1u << jj) : 0u;
             }
 #pragma unroll
             for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
@@ -1390,17 +1421,26 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint64_t hib = (uint64_t)cur.c.b << R;
             const uint64_t below = (1ull << lane) - 1ull;
             uint32_t run = 0u;
+            constexpr int SB = KPL < 8 ? KPL : 8;   // keys re-read 8 at a time (one round trip)
 #pragma unroll
-            for (int jj = 0; jj < KPL; ++jj) {
-                const bool f = (fm >> jj) & 1u;
-                const uint64_t m = __ballot(f);
-                if (f) {
-                    const uint64_t o = at + run + (uint32_t)__popcll(m & below);
-                    out_store(codes + o, hib | (uint64_t)sorted[jj * NT + tid]);
-                    out_store(counts + o, (ecw[jj / 4] >> (8 * (jj % 4))) & 0xFFu);
-                    if constexpr (POS) firsts[o] = ef[jj];
+            for (int j0 = 0; j0 < KPL; j0 += SB) {
+                __builtin_amdgcn_sched_barrier(0);
+                E sk[SB];
+#pragma unroll
+                for (int x = 0; x < SB; ++x) sk[x] = sorted[(j0 + x) * NT + tid];
+#pragma unroll
+                for (int x = 0; x < SB; ++x) {
+                    const int jj = j0 + x;
+                    const bool f = (fm >> jj) & 1u;
+                    const uint64_t m = __ballot(f);
+                    if (f) {
+                        const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                        out_store(codes + o, hib | (uint64_t)sk[x]);
+                        out_store(counts + o, (ecw[jj / 4] >> (8 * (jj % 4))) & 0xFFu);
+                        if constexpr (POS) firsts[o] = ef[jj];
+                    }
+                    run += (uint32_t)__popcll(m);
                 }
-                run += (uint32_t)__popcll(m);
             }
             if (nb) {
 #pragma unroll
