@@ -312,6 +312,9 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
 
     // 2b. bucket starts: exclusive scan of the chunk-padded bucket sizes, the invalid-window
     //     row last (unpadded)
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
+    uint32_t pad_lo = 0u, pad_hi = 0u;   // this bucket's padding slots, filled with spread values
+#endif
     {
         const uint32_t n = tid <= NBK ? start[tid] : 0u;
         const uint32_t p = tid < NBK ? (n + 7u) & ~7u : n;
@@ -323,8 +326,15 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
         for (int q = 0; q < NW; ++q) pre += q < wave ? wsum[q] : 0u;
         const uint32_t ex = pre + incl - p;
         if (tid <= NBK) start[tid] = ex;
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
+        // A/B only (counts wrong): segments listed at KMH_EXCH_COMPACT / 4 of their chunks,
+        // contiguous -- the bytes and the access pattern of a denser exchange code
+        if (tid <= NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)(((ex >> 3) * KMH_EXCH_COMPACT) >> 2);
+        if (tid < NBK) { pad_lo = ex + n; pad_hi = ex + p; }
+#else
         if (tid < NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)((ex >> 3) | ((p - n) << 12));
         if (tid == NBK) toff[(uint64_t)NBK * ldt + lt] = (uint16_t)(ex >> 3);
+#endif
     }
     lds_barrier();
     const uint32_t total = start[NBK];   // entries to write: the padded buckets
@@ -342,6 +352,9 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     }
     lds_barrier();
 
+#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
+    for (uint32_t i = pad_lo; i < pad_hi; ++i) stage[i] = (uint16_t)(i * 40503u);   // no hot bin
+#endif
     // 3. scatter the suffixes: a returning add on the (bucket, replica) start gives each k-mer
     //    its slot (groups of 8: eight adds in flight, then eight stores); the order inside a
     //    segment is arbitrary, the count kernel only adds.  The codes are laundered so that the
@@ -367,6 +380,8 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
 #if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_PLAIN)
     // A/B only: plain stores (the lines may stay in the Infinity Cache for the count kernel)
     for (uint32_t c = tid; c < (total >> 3); c += kPThreads) dst[c] = src[c];
+#elif defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
+    for (uint32_t c = tid; c < (((total >> 3) * KMH_EXCH_COMPACT) >> 2); c += kPThreads) store_nt(&dst[c], src[c]);
 #else
     for (uint32_t c = tid; c < (total >> 3); c += kPThreads) store_nt(&dst[c], src[c]);
 #endif
@@ -474,8 +489,8 @@ constexpr int batch_tiles(int qmax) {
 // queue (chunk index relative to the batch, entries used in the chunk) and streams the queue
 // with all 64 lanes active: U loads in flight per lane, 8 LDS adds per load.  A batch whose
 // chunks overflow the queue (skewed input) is walked lane by lane instead.
-#ifdef KMH_EXPERIMENTS
-// KMH_DENSE_PROF: per-phase clocks of k_bucket_count summed over its waves (lane 0 of each)
+#if defined(KMH_EXPERIMENTS) && defined(KMH_DP_CLOCKS)
+// KMH_DENSE_PROF: per-phase clocks (a clocks build: its same-address atomics slow the kernel) of k_bucket_count summed over its waves (lane 0 of each)
 __device__ unsigned long long g_dense_prof[8];
 #define KMH_DP(i) if ((threadIdx.x & 63) == 0) { const unsigned long long t_ = clock64(); atomicAdd(&g_dense_prof[i], t_ - tl_); tl_ = t_; }
 #else
@@ -512,7 +527,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     const uint4* chunks = reinterpret_cast<const uint4*>(suf);
     const uint64_t row0 = (uint64_t)g * (1ull << (2 * K)) + (uint64_t)b * kCBins;
 
-#ifdef KMH_EXPERIMENTS
+#if defined(KMH_EXPERIMENTS) && defined(KMH_DP_CLOCKS)
     unsigned long long tl_ = clock64();
 #endif
     uint4* tbl4 = reinterpret_cast<uint4*>(tbl);
@@ -656,14 +671,14 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     // make it a k_reencode bucket) and widens again.  With split rows (S > 1, added with
     // atomics) the table is checked before it is widened.  One call site of each walk (a
     // third inlined copy made the compiler spill to scratch).
-#if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
+#if defined(KMH_EXPERIMENTS) && (defined(KMH_EXCH_CUT) || defined(KMH_EXCH_COMPACT))
     constexpr bool kCheck = false;   // A/B only: no exactness check (the cut exchange counts garbage)
 #else
     constexpr bool kCheck = true;
 #endif
     const bool post = S == 1;   // uniform
     bool exact = false, enc = false;
-#ifdef KMH_EXPERIMENTS
+#if defined(KMH_EXPERIMENTS) && defined(KMH_DP_CLOCKS)
     __syncthreads();
     KMH_DP(2)
 #endif
@@ -962,7 +977,7 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
                                s, suf, toff, ldt, m, S, d_out, fl, U4Out{});
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
-#ifdef KMH_EXPERIMENTS
+#if defined(KMH_EXPERIMENTS) && defined(KMH_DP_CLOCKS)
         if (env_long("KMH_DENSE_PROF", 0)) {
             unsigned long long hp[8];
             KMH_HIP(ctx, hipStreamSynchronize(s));
