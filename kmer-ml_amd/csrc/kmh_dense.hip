@@ -220,18 +220,19 @@ __device__ __forceinline__ void visit_raw(uint4 a, uint4 b, uint4 n, uint32_t tm
     constexpr uint32_t KM = (1u << (2 * K)) - 1u;
     constexpr uint32_t VM = (1u << K) - 1u;
     const uint64_t wAB = ((uint64_t)cA << 32) | cB;
-    const uint32_t vAB = (iA << 16) | iB;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t code = (uint32_t)(wAB >> (64 - 2 * (j + K))) & KM;
-        km[j] = (((vAB >> (32 - (j + K))) & VM) == 0u) ? code : INV;
-    }
     const uint64_t wBN = ((uint64_t)cB << 32) | cN;
-    const uint32_t vBN = (iB << 16) | iN;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t code = (uint32_t)(wBN >> (64 - 2 * (j + K))) & KM;
-        km[16 + j] = (((vBN >> (32 - (j + K))) & VM) == 0u) ? code : INV;
+    for (int j = 0; j < 16; ++j) km[j] = (uint32_t)(wAB >> (64 - 2 * (j + K))) & KM;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) km[16 + j] = (uint32_t)(wBN >> (64 - 2 * (j + K))) & KM;
+    // only a wave whose 48-byte spans hold a non-base byte (in a synthetic genome: the wave at
+    // its end) applies the per-window validity selects: 3 of the ~18 VALU instructions per k-mer
+    if (__builtin_amdgcn_ballot_w64((iA | iB | iN) != 0u) != 0ull) {
+        const uint32_t vAB = (iA << 16) | iB, vBN = (iB << 16) | iN;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) km[j] = ((vAB >> (32 - (j + K))) & VM) == 0u ? km[j] : INV;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) km[16 + j] = ((vBN >> (32 - (j + K))) & VM) == 0u ? km[16 + j] : INV;
     }
 }
 
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     constexpr int NW = kPThreads / 64;
     constexpr int CAP = tile_cap<K>();
     static_assert(NBK + 1 <= kPThreads && CAP / 8 < 4096, "scan layout / 12-bit chunk offsets");
-    static_assert(NROW + NW <= CAP / 2 && CAP <= 65535 - kPTile, "starts alias the stage; u16 counters");
+    static_assert(NROW + NW <= CAP / 2 && 2 * CAP <= 65535, "starts alias the stage; u16 byte counters");
     constexpr uint32_t kInv = (uint32_t)NBK << kCBits;   // invalid windows: bucket NBK, suffix 0
     static_assert(kCBits == 16, "counter word = code >> 17, half = bit 16 of the code");
     // counters as u16 halves: bucket b, replica r in half b & 1 of word (b >> 1) * 32 + r
@@ -290,15 +291,18 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     }
     lds_barrier();
 
-    // 1. histogram of (bucket, replica): adds whose results nobody waits for
+    // 1. histogram of (bucket, replica): adds whose results nobody waits for.  Counters,
+    //    starts and slots are kept in bytes (2 per k-mer, every value below 2 * CAP < 65536),
+    //    so the scatter's returned start is the stage address itself.
 #pragma unroll
     for (int j = 0; j < kTileBpt; ++j) {
-        __hip_atomic_fetch_add(ctr(km[j]), 1u << half(km[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(ctr(km[j]), 2u << half(km[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     lds_barrier();
 
     // 2a. row totals: one 16-byte read per lane, 8 lanes per word row (two buckets, summed as
-    //     packed halves: a bucket holds at most kPTile < 65536), 8 word rows per wave instruction
+    //     packed halves: a bucket holds at most 2 * kPTile < 65536 bytes), 8 word rows per wave
+    //     instruction
     for (int i = wave; i < NROW / 16; i += NW) {
         const int wr = i * 8 + (lane >> 3);
         const uint4 v = rep4[wr * (kRep / 4) + (lane & 7)];
@@ -316,8 +320,8 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     uint32_t pad_lo = 0u, pad_hi = 0u;   // this bucket's padding slots, filled with spread values
 #endif
     {
-        const uint32_t n = tid <= NBK ? start[tid] : 0u;
-        const uint32_t p = tid < NBK ? (n + 7u) & ~7u : n;
+        const uint32_t n = tid <= NBK ? start[tid] : 0u;          // bytes: 2 per k-mer
+        const uint32_t p = tid < NBK ? (n + 15u) & ~15u : n;       // padded to a 16-byte chunk
         const uint32_t incl = scan64(p);
         if (lane == 63) wsum[wave] = incl;
         lds_barrier();
@@ -329,18 +333,18 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
 #if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
         // A/B only (counts wrong): segments listed at KMH_EXCH_COMPACT / 4 of their chunks,
         // contiguous -- the bytes and the access pattern of a denser exchange code
-        if (tid <= NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)(((ex >> 3) * KMH_EXCH_COMPACT) >> 2);
+        if (tid <= NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)(((ex >> 4) * KMH_EXCH_COMPACT) >> 2);
         if (tid < NBK) { pad_lo = ex + n; pad_hi = ex + p; }
 #else
-        if (tid < NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)((ex >> 3) | ((p - n) << 12));
-        if (tid == NBK) toff[(uint64_t)NBK * ldt + lt] = (uint16_t)(ex >> 3);
+        if (tid < NBK) toff[(uint64_t)tid * ldt + lt] = (uint16_t)((ex >> 4) | ((p - n) << 11));
+        if (tid == NBK) toff[(uint64_t)NBK * ldt + lt] = (uint16_t)(ex >> 4);
 #endif
     }
     lds_barrier();
-    const uint32_t total = start[NBK];   // entries to write: the padded buckets
+    const uint32_t total = start[NBK];   // bytes to write: the padded buckets
 
     // 2c. segment start of every (bucket, replica), in place
-    //     (packed halves: every start stays below CAP + kPTile < 65536)
+    //     (packed halves: every start stays below 2 * CAP < 65536)
     for (int i = wave; i < NROW / 16; i += NW) {
         const int wr = i * 8 + (lane >> 3);
         uint4* pr = &rep4[wr * (kRep / 4) + (lane & 7)];
@@ -353,7 +357,7 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     lds_barrier();
 
 #if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
-    for (uint32_t i = pad_lo; i < pad_hi; ++i) stage[i] = (uint16_t)(i * 40503u);   // no hot bin
+    for (uint32_t i = pad_lo; i < pad_hi; i += 2) stage[i >> 1] = (uint16_t)(i * 40503u);   // no hot bin
 #endif
     // 3. scatter the suffixes: a returning add on the (bucket, replica) start gives each k-mer
     //    its slot (groups of 8: eight adds in flight, then eight stores); the order inside a
@@ -367,10 +371,10 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint32_t h = half(km[j0 + j]);
-            pos[j] = __builtin_amdgcn_ubfe(atomicAdd(ctr(km[j0 + j]), 1u << h), h, 16);
+            pos[j] = __builtin_amdgcn_ubfe(atomicAdd(ctr(km[j0 + j]), 2u << h), h, 16);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) stage[pos[j]] = (uint16_t)km[j0 + j];
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(stage) + pos[j]) = (uint16_t)km[j0 + j];
     }
     lds_barrier();
 
@@ -379,11 +383,11 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     const uint4* src = reinterpret_cast<const uint4*>(stage);
 #if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_PLAIN)
     // A/B only: plain stores (the lines may stay in the Infinity Cache for the count kernel)
-    for (uint32_t c = tid; c < (total >> 3); c += kPThreads) dst[c] = src[c];
+    for (uint32_t c = tid; c < (total >> 4); c += kPThreads) dst[c] = src[c];
 #elif defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_COMPACT)
-    for (uint32_t c = tid; c < (((total >> 3) * KMH_EXCH_COMPACT) >> 2); c += kPThreads) store_nt(&dst[c], src[c]);
+    for (uint32_t c = tid; c < (((total >> 4) * KMH_EXCH_COMPACT) >> 2); c += kPThreads) store_nt(&dst[c], src[c]);
 #else
-    for (uint32_t c = tid; c < (total >> 3); c += kPThreads) store_nt(&dst[c], src[c]);
+    for (uint32_t c = tid; c < (total >> 4); c += kPThreads) store_nt(&dst[c], src[c]);
 #endif
 }
 
@@ -438,6 +442,7 @@ template <bool EXACT>
 __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv, const FixLog& L,
                                             uint64_t row0, uint32_t* wrapped) {
     const uint32_t wd[4] = {q.x, q.y, q.z, q.w};
+    const uint32_t used = (1u << nv) - 1u;   // slots 0 .. nv - 1 add 1 (one bfe per slot)
     uint32_t old[8], off[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -445,7 +450,7 @@ __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv,
         // entry v = the low / high half of w: word (v >> 1) * 4 bytes, half (v & 1) * 16 bits
         const uint32_t addr = (i & 1) ? (w >> 15) & 0x1FFFCu : (w << 1) & 0x1FFFCu;
         off[i] = (i & 1) ? (w >> 12) & 16u : (w << 4) & 16u;
-        const uint32_t add = (uint32_t)i < nv ? 1u : 0u;
+        const uint32_t add = __builtin_amdgcn_ubfe(used, (uint32_t)i, 1);
         old[i] = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(tbl) + addr),
                                         add << off[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
