@@ -160,17 +160,24 @@ __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
         rhi = revcomp<32>(lo);
         rlo = revcomp<32>(hi);
     }
-#pragma unroll
-    for (int j = 0; j < WPT; ++j) {
-        if (((b.inv << j) >> (64 - K)) == 0ull) {
-            uint64_t c = window<K>(hi, lo, j);
-            if constexpr (CANON != 0) {
-                const uint64_t r = window<K>(rhi, rlo, 64 - j - K);
-                c = r < c ? r : c;
-            }
-            f(c, j);
+    auto code = [&](int j) {
+        uint64_t c = window<K>(hi, lo, j);
+        if constexpr (CANON != 0) {
+            const uint64_t r = window<K>(rhi, rlo, 64 - j - K);
+            c = r < c ? r : c;
         }
+        return c;
+    };
+    // a wave whose 64-byte spans hold no non-base byte (every wave of a synthetic genome but the
+    // one at its end) takes every window without the per-window validity test and branch
+    if (__builtin_amdgcn_ballot_w64(b.inv != 0ull) == 0ull) {
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) f(code(j), j);
+        return;
     }
+#pragma unroll
+    for (int j = 0; j < WPT; ++j)
+        if (((b.inv << j) >> (64 - K)) == 0ull) f(code(j), j);
 }
 
 // Persistent, one workgroup per CU (132 KiB of LDS).  XCD x (= blockIdx % 8) takes a contiguous
