@@ -67,11 +67,14 @@ def parse():
     p.add_argument("--no-config5", action="store_true",
                    help="dense N = 1: skip the config-5 measurement (16 x 250 Mbp, k = 21 canonical, "
                         "3 timed steps) that the default run appends to its JSON line as \"config5\"")
+    p.add_argument("--no-e2e", action="store_true",
+                   help="dense N = 1: skip the drop-in end-to-end leg (the reference CLI's call pattern on "
+                        "synthetic FASTA files, per-stage clocks) that the default run appends as \"e2e\"")
     p.add_argument("--simulate-ranks", type=int, default=0,
                    help="one process on one GPU doing what ONE rank of N does per step at config 4 "
                         "(count G/N genomes, encode u4, and the all-gather's writes modelled as N "
                         "device copies of the slot; no xGMI): a projection, labelled as such")
-    p.add_argument("--cpu-sample", type=int, default=16_000_000,
+    p.add_argument("--cpu-sample", type=int, default=8_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
     p.add_argument("--kernel-events", choices=["roofline", "all"], default="roofline",
                    help="HIP event pairs around the kernels the roofline names only (default), or all")
@@ -97,7 +100,7 @@ def parse():
     return a
 
 
-CONFIG5_CPU_SAMPLE = 12_000_000   # ~10 s of the k = 21 loop on one EPYC 9575F core
+CONFIG5_CPU_SAMPLE = 6_000_000    # ~5 s of the k = 21 loop on one EPYC 9575F core + ~10 s of its writer
 
 
 def cpu_baseline(sample, k, strand=None):
@@ -106,18 +109,30 @@ def cpu_baseline(sample, k, strand=None):
     sys.path.insert(0, HERE)
     from oracle import kmers as okmers
     from oracle import synth as osynth
+    import tempfile
     seq = osynth.synth_bases(sample, osynth.genome_seed(0)).tobytes().decode()
     t0 = time.perf_counter()
     table = okmers.count_sequence(seq, k)
     dt = time.perf_counter() - t0
     assert sum(table.values()) == sample - k + 1
+    # the save phase (generate.py:68-91, compress=False as the CLI's default) on the same table:
+    # SURVEY 8(d) times it separately because it scales with the distinct k-mers, not the bases
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, f"k{k}.txt")
+        t1 = time.perf_counter()
+        okmers.save_kmers(table, path)
+        ds = time.perf_counter() - t1
+        save_bytes = os.path.getsize(path)
     note = (" (forward strand: the reference counts no canonical k-mers, so this is its loop on "
             "the config's genomes, not a canonical count)") if strand == "forward" else ""
     return {"value": sample / dt, "unit": "bases/s", "cores": 1, "kind": "port",
             "sample": f"first {sample} bases of synthetic genome 0, k={k}: the count loop of "
                       f"generate.py:49-58 restated in pure Python (oracle/kmers.py), "
-                      f"{dt:.2f} s on one core{note}",
-            "seconds": dt, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
+                      f"{dt:.2f} s on one core{note}; then its k{k}.txt writer (generate.py:68-91, "
+                      f"oracle/kmers.py save_kmers) over the {len(table)} distinct k-mers, {ds:.2f} s",
+            "k": k, "seconds": dt, "save_seconds": ds, "save_lines": len(table), "save_bytes": save_bytes,
+            "value_e2e": sample / (dt + ds),
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
 
 
 def cpu_threads_baseline(k, bases_per_thread=25_000_000, threads=16):
@@ -655,6 +670,12 @@ def main():
                 out["config5"] = run_sparse(sa, 1, 0, dev, dev_index, emit=False)
             except Exception as e:   # never lose the config-3 line over the extra measurement
                 out["config5"] = {"error": f"{type(e).__name__}: {e}"}
+        if world == 1 and not sim and not a.no_e2e and G == 64 and L == 100_000_000 and k == 12:
+            torch.cuda.empty_cache()
+            try:
+                out["e2e"] = run_e2e(dev, dev_index, {12: cpu, 21: cpu5})
+            except Exception as e:
+                out["e2e"] = {"error": f"{type(e).__name__}: {e}"}
         if sim:
             out["config"]["workload"] = (f"projection: ONE rank of config 4 at N = {sim} on one GPU (its {g_local} of "
                                          f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k}, u4 encode, the all-gather "
@@ -669,6 +690,88 @@ def main():
         dist.destroy_process_group()
     if not ok:
         raise SystemExit("row-sum check failed")
+
+
+YEAST_LENGTHS = [230218, 813184, 316620, 1531933, 576874, 270161, 1090940, 562643, 439888, 745751, 666816,
+                 1078177, 924431, 784333, 1091291, 948066, 85779]   # config 1's 17 records
+
+
+def _write_synth_fasta(ctx, dev, path, lengths, prefix):
+    """A FASTA of synthetic genome 0 (generated on the device) cut into records of
+    `lengths` bases, 80-column lines."""
+    L = sum(lengths)
+    d = torch.empty(L, dtype=torch.uint8, device=dev)
+    ctx.synth_dev(d.data_ptr(), L, L, 1, SEED_BASE, torch.cuda.current_stream(dev).cuda_stream)
+    seq = d.cpu().numpy()
+    with open(path, "wb") as f:
+        pos = 0
+        for i, n in enumerate(lengths):
+            body = seq[pos:pos + n]
+            pos += n
+            f.write(f">{prefix}{i + 1:02d}\n".encode())
+            full = n // 80
+            lines = np.empty((full, 81), np.uint8)
+            lines[:, :80] = body[:full * 80].reshape(full, 80)
+            lines[:, 80] = ord("\n")
+            f.write(lines.tobytes())
+            if n % 80:
+                f.write(body[full * 80:].tobytes() + b"\n")
+
+
+def run_e2e(dev, dev_index, cpu):
+    """The drop-in end to end: the reference CLI's call pattern
+    (scripts/extract_kmers.py:55-61: KmerExtractor(output_dir, compress=False) then
+    extract_kmers_from_fasta(path, k_values) per genome) on synthetic FASTA files, with the
+    drop-in's stage clocks (kmerml.kmers.generate.PROFILE: parse, pack, h2d, count = kernels +
+    first-occurrence order + D2H, format, write, trim).  Beside it the reference's loop and
+    writer (cpu_baseline: count seconds per base and save seconds per line measured on its
+    sample) projected onto the same files.  Each case runs once untimed, then timed."""
+    import contextlib
+    import io
+    import tempfile
+    from kmerml.kmers import generate as kgen
+    ctx = _native.context(dev_index)
+    cases = [("yeast_standin_12.16Mbp", YEAST_LENGTHS, [8, 9, 10, 11, 12]),
+             ("synthetic_100Mbp", [100_000_000], [8, 9, 10, 11, 12]),
+             ("yeast_standin_12.16Mbp", YEAST_LENGTHS, [21])]
+    out = {"call": "KmerExtractor(output_dir, compress=False).extract_kmers_from_fasta(fasta, k_values) "
+                   "(scripts/extract_kmers.py:55-61 defaults: -k 8,9,10,11,12, no --compress)",
+           "cases": []}
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, lengths, ks in cases:
+            fa = os.path.join(tmp, f"{name}.fa")
+            if not os.path.exists(fa):
+                _write_synth_fasta(ctx, dev, fa, lengths, "SYN_chr" if len(lengths) > 1 else "SYN_")
+            L = sum(lengths)
+            ex = kgen.KmerExtractor(output_dir=os.path.join(tmp, "out"), compress=False)
+            for timed in (False, True):
+                kgen.PROFILE = {}
+                t0 = time.perf_counter()
+                with contextlib.redirect_stdout(io.StringIO()):
+                    ex.extract_kmers_from_fasta(fa, ks, organism_id=name)
+                dt = time.perf_counter() - t0
+            stages = {k: round(v, 4) for k, v in kgen.PROFILE.items()}
+            kgen.PROFILE = None
+            odir = os.path.join(tmp, "out", name)
+            lines = sum(sum(1 for _ in open(os.path.join(odir, f"k{k}.txt"), "rb")) for k in ks)
+            nbytes = sum(os.path.getsize(os.path.join(odir, f"k{k}.txt")) for k in ks)
+            case = {"input": f"{name}: {len(lengths)} record(s), {L} bases, 80-column FASTA", "k_values": ks,
+                    "seconds": round(dt, 4), "bases_per_s": L / dt, "bases_x_k_per_s": L * len(ks) / dt,
+                    "stages_s": stages, "lines_written": lines, "bytes_written": nbytes}
+            ref = (cpu or {}).get(21 if ks == [21] else 12)
+            if ref:   # the reference's loop + writer at the rates measured on its sample
+                est = len(ks) * L / ref["value"] + lines * ref["save_seconds"] / ref["save_lines"]
+                case["reference_projection"] = {
+                    "seconds": round(est, 1), "bases_per_s": L / est,
+                    "basis": f"cpu_baseline k={ref['k']}: count {ref['value']:.3g} bases/s per k, save "
+                             f"{ref['save_seconds'] / ref['save_lines'] * 1e6:.2f} us per line (one core)",
+                    "speedup": round(est / dt, 1)}
+            out["cases"].append(case)
+            for k in ks:
+                os.remove(os.path.join(odir, f"k{k}.txt"))
+            if name.startswith("synthetic"):
+                os.remove(fa)
+    return out
 
 
 def run_sparse(a, world, rank, dev, dev_index, emit=True):
@@ -790,4 +893,5 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
 
 
 if __name__ == "__main__":
-    main()
+    from kmerml.utils.devmem import run_guarded
+    run_guarded(main)

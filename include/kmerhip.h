@@ -43,7 +43,7 @@ extern "C" {
 #define KMH_ERR_IO          -5  /* file could not be read               */
 
 #define KMH_MAX_DENSE_K  12     /* dense 4^k tables: 1 <= k <= 12        */
-#define KMH_MAX_SPARSE_K 32     /* sorted sparse path: 13 <= k <= 32     */
+#define KMH_MAX_SPARSE_K 32     /* device hash pipeline: 13 <= k <= 32   */
 #define KMH_MAX_LONG_K   1024   /* long k-mers (forward strand): 33 <= k <= 1024, sorted by
                                    ceil(k / 32) code words                      */
 
@@ -70,6 +70,13 @@ void kmh_ctx_destroy(kmh_ctx* ctx);
  * stream and the context stream; the next call allocates again.  For long-lived processes
  * that hand the device to other work.  Replaces nothing in the reference. */
 int kmh_ctx_release(kmh_ctx* ctx);
+/* Bytes the context holds now (cached device workspace + pinned staging). */
+uint64_t kmh_ctx_workspace_bytes(const kmh_ctx* ctx);
+/* Workspace policy of a long-lived process: kmh_ctx_release if the context holds more than
+ * keep_bytes, else nothing.  The drop-in calls it after every organism, so the serial loop of
+ * /root/reference/kmerml/kmers/generate.py:116-126 (extract_from_genome_list) does not keep a
+ * config-5-sized workspace (tens of GB) between genomes. */
+int kmh_ctx_trim(kmh_ctx* ctx, uint64_t keep_bytes);
 
 /* Last error message of `ctx`, or of the calling thread's context-free calls when
  * ctx == NULL.  Never NULL; "" when there was no error. */
@@ -107,7 +114,9 @@ void kmh_fasta_free(kmh_fasta* f);
  * `seq` whose k bytes are all bases.  Result = distinct k-mers in FIRST-OCCURRENCE
  * order (the insertion order of the reference's dict, which fixes the line order of
  * k{k}.txt, generate.py:89-91), with exact counts and the first window start.
- * 1 <= k <= 12: dense 4^k table on the GPU; 13 <= k <= 32: GPU sort + run-length;
+ * 1 <= k <= 12: dense 4^k table on the GPU; 13 <= k <= 32: the device hash pipeline of
+ * kmh_count_sparse_dev with every window's position carried (the minimum per k-mer), then a
+ * radix sort of the first positions;
  * 33 <= k <= KMH_MAX_LONG_K: GPU sort of ceil(k / 32) code words per window + run-length,
  * and codes[i] then holds only the k-mer's first 32 bases (the whole k-mer is
  * seq[first[i] .. first[i] + k); kmh_format_lines_seq writes its text).
@@ -115,6 +124,14 @@ void kmh_fasta_free(kmh_fasta* f);
  * which is forward-strand only; used for BASELINE config 5; k <= 32 only). */
 int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int canonical,
                    kmh_kmers** out);
+/* kmh_count_host in two steps, so that an organism crosses PCIe once for all its k (the
+ * reference loops `for k in k_values` over the same record, generate.py:49): kmh_stage_host
+ * copies seq to the context's device staging (it returns once the host buffer may change);
+ * kmh_count_staged counts it at k like kmh_count_host.  The staging stays valid until the next
+ * host-buffer call of any kind on the context or kmh_ctx_release / kmh_ctx_trim
+ * (KMH_ERR_INVALID then). */
+int kmh_stage_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n);
+int kmh_count_staged(kmh_ctx* ctx, int k, int canonical, kmh_kmers** out);
 uint64_t kmh_kmers_size(const kmh_kmers* r);
 /* Copy the result out; any pointer may be NULL.  codes/counts/first: size() entries. */
 int kmh_kmers_export(const kmh_kmers* r, uint64_t* codes, uint32_t* counts, uint64_t* first);

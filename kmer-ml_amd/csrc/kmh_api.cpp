@@ -56,6 +56,17 @@ int ensure(Ctx* ctx, DevBuf& b, size_t bytes) {
     return KMH_OK;
 }
 
+int drop(Ctx* ctx, DevBuf& b) {
+    if (!b.ptr) return KMH_OK;
+    KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    KMH_HIP(ctx, hipDeviceSynchronize());
+    KMH_HIP(ctx, hipFree(b.ptr));
+    if (&b == &ctx->seq) ctx->staged_ok = false;
+    b.ptr = nullptr;
+    b.bytes = 0;
+    return KMH_OK;
+}
+
 int upload(Ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s) {
     if (ctx->pinned_ready) KMH_HIP(ctx, hipEventSynchronize(ctx->pinned_ready));
     if (bytes > ctx->pinned_bytes) {
@@ -163,6 +174,16 @@ static void free_workspace(kmh_ctx* ctx) {
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     ctx->pinned = nullptr;
     ctx->pinned_bytes = 0;
+    ctx->staged_ok = false;
+}
+
+static uint64_t workspace_bytes(const kmh_ctx* ctx) {
+    uint64_t t = ctx->pinned_bytes;
+    for (const kmh::DevBuf* b : {&ctx->seq, &ctx->suf, &ctx->toff, &ctx->meta, &ctx->out, &ctx->out2, &ctx->fix,
+                                 &ctx->redo, &ctx->order, &ctx->sort_tmp, &ctx->scan_tmp, &ctx->first})
+        t += b->bytes;
+    for (const auto& b : ctx->sparse) t += b.bytes;
+    return t;
 }
 
 int kmh_ctx_release(kmh_ctx* ctx) {
@@ -170,6 +191,19 @@ int kmh_ctx_release(kmh_ctx* ctx) {
         kmh::set_thread_error("kmh_ctx_release: ctx is NULL");
         return KMH_ERR_INVALID;
     }
+    KMH_HIP(ctx, hipSetDevice(ctx->device));
+    free_workspace(ctx);
+    return KMH_OK;
+}
+
+uint64_t kmh_ctx_workspace_bytes(const kmh_ctx* ctx) { return ctx ? workspace_bytes(ctx) : 0; }
+
+int kmh_ctx_trim(kmh_ctx* ctx, uint64_t keep_bytes) {
+    if (!ctx) {
+        kmh::set_thread_error("kmh_ctx_trim: ctx is NULL");
+        return KMH_ERR_INVALID;
+    }
+    if (workspace_bytes(ctx) <= keep_bytes) return KMH_OK;
     KMH_HIP(ctx, hipSetDevice(ctx->device));
     free_workspace(ctx);
     return KMH_OK;
@@ -346,6 +380,7 @@ int kmh_feature_columns_dev(kmh_ctx* ctx, const uint64_t* d_codes, uint64_t n, i
 
 // Host sequence -> device (padded with one non-base byte so loads past the end are safe).
 static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t** d_seq) {
+    ctx->staged_ok = false;
     int rc = kmh::ensure(ctx, ctx->seq, (size_t)n + 64);
     if (rc) return rc;
     uint8_t* d = static_cast<uint8_t*>(ctx->seq.ptr);
@@ -354,6 +389,10 @@ static int stage_sequence(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, uint8_t*
     *d_seq = d;
     return KMH_OK;
 }
+
+// The counting dispatch of kmh_count_host / kmh_count_staged on a sequence already in
+// ctx->seq (n bytes + 64 zero bytes).
+static int count_staged_impl(kmh_ctx* ctx, uint8_t* d_seq, uint64_t n, int k, int canonical, kmh_kmers** out);
 
 int kmh_count_dense_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, uint32_t* counts) {
     if (!ctx) return KMH_ERR_INVALID;
@@ -375,26 +414,68 @@ int kmh_count_dense_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, ui
     return KMH_OK;
 }
 
+// Checks of every host-buffer count call, before any byte is read or staged.
+static int check_count_args(kmh_ctx* ctx, uint64_t n, int k, int canonical) {
+    if (k < 1 || k > KMH_MAX_LONG_K)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "k must be in [1, 1024] (k = " + std::to_string(k) + ")");
+    if (canonical && k > KMH_MAX_SPARSE_K)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "canonical counting needs k <= 32 (k = " + std::to_string(k) + ")");
+    // Size limit ("Limits"): every path takes sequences below 2^32 - 1 bytes (u32
+    // positions and counts; item counts are 64-bit).
+    if (n >= 0xFFFFFFFFull)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "sequence must be shorter than 2^32 - 1 bytes (one call)");
+    return KMH_OK;
+}
+
 int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int canonical,
                    kmh_kmers** out) {
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (!out || (n && !seq)) return fail(ctx, KMH_ERR_INVALID, "NULL argument");
     *out = nullptr;
-    if (k < 1 || k > KMH_MAX_LONG_K)
-        return fail(ctx, KMH_ERR_UNSUPPORTED, "k must be in [1, 1024] (k = " + std::to_string(k) + ")");
-    if (canonical && k > KMH_MAX_SPARSE_K)
-        return fail(ctx, KMH_ERR_UNSUPPORTED, "canonical counting needs k <= 32 (k = " + std::to_string(k) + ")");
-    // Size limit, checked before any byte is read or staged ("Limits"): every path
-    // takes sequences below 2^32 - 1 bytes (u32 positions and counts; item counts are 64-bit).
+    int rc = check_count_args(ctx, n, k, canonical);
+    if (rc) return rc;
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    uint8_t* d_seq = nullptr;
+    if ((rc = stage_sequence(ctx, seq, n, &d_seq))) return rc;
+    return count_staged_impl(ctx, d_seq, n, k, canonical, out);
+}
+
+int kmh_stage_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (n && !seq) return fail(ctx, KMH_ERR_INVALID, "NULL argument");
     if (n >= 0xFFFFFFFFull)
         return fail(ctx, KMH_ERR_UNSUPPORTED, "sequence must be shorter than 2^32 - 1 bytes (one call)");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    std::unique_ptr<kmh_kmers> r(new (std::nothrow) kmh_kmers);
-    if (!r) return fail(ctx, KMH_ERR_NOMEM, "out of host memory");
     uint8_t* d_seq = nullptr;
     int rc = stage_sequence(ctx, seq, n, &d_seq);
     if (rc) return rc;
+    // the host buffer may change after return: the copy from pageable memory completes first
+    KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->staged_n = n;
+    ctx->staged_ok = true;
+    return KMH_OK;
+}
+
+int kmh_count_staged(kmh_ctx* ctx, int k, int canonical, kmh_kmers** out) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (!out) return fail(ctx, KMH_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (!ctx->staged_ok || !ctx->seq.ptr)
+        return fail(ctx, KMH_ERR_INVALID, "kmh_count_staged: no staged sequence (kmh_stage_host first; another "
+                                          "host-buffer call or kmh_ctx_release/trim replaces or frees it)");
+    int rc = check_count_args(ctx, ctx->staged_n, k, canonical);
+    if (rc) return rc;
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return count_staged_impl(ctx, static_cast<uint8_t*>(ctx->seq.ptr), ctx->staged_n, k, canonical, out);
+}
+
+static int count_staged_impl(kmh_ctx* ctx, uint8_t* d_seq, uint64_t n, int k, int canonical, kmh_kmers** out) {
+    std::unique_ptr<kmh_kmers> r(new (std::nothrow) kmh_kmers);
+    if (!r) return fail(ctx, KMH_ERR_NOMEM, "out of host memory");
+    int rc = KMH_OK;
     try {
         if (k <= KMH_MAX_DENSE_K && !canonical) {
             const size_t bins = (size_t)1 << (2 * k);

@@ -11,9 +11,11 @@
 //                     (u32 residues for k <= 21, u64 for 22 <= k <= 32 on half-size tiles),
 //                     one coalesced store of the tile's entries and an exact
 //                     bucket-major offset table toff[bucket][tile] (u16 entry indices).
-//  2. k_sp_sizes      entries per (genome, bucket).  The host splits every bucket into
-//                     P = ceil(entries / 7680) passes over equal residue ranges (one count
-//                     item each) and into split items of ~12K entries (ranges of tiles).
+//  2. k_sp_sizes      entries per (genome, bucket); k_sp_plan (one workgroup, on the device)
+//     k_sp_plan       splits every bucket into P = ceil(entries / 7680) passes over equal
+//     k_sp_fill       residue ranges (one count item each) and into split items of ~12K
+//                     entries (ranges of tiles); k_sp_fill writes the items.  The host reads
+//                     back only the two item totals.
 //  3. k_sp_split      one workgroup per split item: gathers the bucket's segments of its
 //                     tiles (16-byte chunk loads, entries outside the segment masked by
 //                     position), partitions them by pass (LDS histogram, scan, scatter) and
@@ -26,8 +28,9 @@
 //                     bins of repeated keys go through a small LDS hash table.
 //  5. fallback        a split item whose entries exceed its staging, or an item the count
 //                     kernel cannot hold, emits nothing; those passes are counted by
-//                     gather + hipCUB radix sort + run-length encode from the step-1 entries
-//                     (keys of different passes are disjoint, so nothing is counted twice).
+//                     gather + the hand-written radix sort of kmh_sort.hip + run-length
+//                     encode from the step-1 entries (keys of different passes are
+//                     disjoint, so nothing is counted twice).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -293,7 +296,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
         cnt[tid] = 0u;   // (the cursors are dead; the next histogram starts after a barrier)
 
         E* dst = ent + (uint64_t)lt * kSpTile;
+#if defined(KMH_EXPERIMENTS) && KMH_SP_PART_EXP == 1
+        const uint32_t n4 = total == 0xFFFFFFFFu ? total / EPC : 0u;   // what-if: no entries stored
+#else
         const uint32_t n4 = total / EPC;
+#endif
         for (uint32_t i = tid; i < n4; i += kSpThreads)
             store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
         if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
@@ -732,7 +739,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next item starts after a barrier
 
         // (D) this item's stores
+#if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 1
+        if (fits && total == 0xFFFFFFFFu) {   // what-if: no split output (timing of the split only)
+#else
         if (fits) {
+#endif
             E* dst = out + (uint64_t)item * kCaps;
             const uint32_t n4 = total / EPC;
             for (uint32_t i = tid; i < n4; i += kSpThreads)
@@ -1442,8 +1453,17 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const uint64_t m = __ballot(f);
                     if (f) {
                         const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+#if defined(KMH_EXPERIMENTS) && KMH_SP_OUT_EXP == 1
+                        // what-if: a compact row (u32 residue + u8 count), same positions
+                        out_store(reinterpret_cast<uint32_t*>(codes) + o, (uint32_t)sk[x]);
+                        out_store(reinterpret_cast<uint8_t*>(counts) + o, (uint8_t)(ecw[jj / 4] >> (8 * (jj % 4))));
+#elif defined(KMH_EXPERIMENTS) && KMH_SP_OUT_EXP == 2
+                        // what-if: no output bytes at all (counts wrong; timing only)
+                        if (sk[x] == (E)0x5A5A5A5Au && o == 0ull) codes[0] = hib;
+#else
                         out_store(codes + o, hib | (uint64_t)sk[x]);
                         out_store(counts + o, (ecw[jj / 4] >> (8 * (jj % 4))) & 0xFFu);
+#endif
                         if constexpr (POS) firsts[o] = ef[jj];
                     }
                     run += (uint32_t)__popcll(m);
@@ -1851,6 +1871,13 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         }
         bool any_gbf = false;
         for (uint32_t f : gbf) any_gbf |= f != 0u;
+#ifdef KMH_EXPERIMENTS
+        if (env_long("KMH_SP_NO_FALLBACK", 0)) {   // what-if builds whose counts are wrong by design
+            nfail = 0;
+            ids.clear();
+            any_gbf = false;
+        }
+#endif
         std::vector<CountItem> citems;
         if (nfail || any_gbf) {  // items are only needed on the host to recount failed passes
             citems.resize(nci);

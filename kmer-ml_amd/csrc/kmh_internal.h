@@ -40,6 +40,9 @@ struct Ctx {
     std::string err;
     // device workspace
     DevBuf seq, suf, toff, meta, out, out2, fix, redo, sparse[8], order, sort_tmp, scan_tmp, first;
+    // kmh_stage_host: bytes of the host sequence staged in `seq` (valid while staged_ok)
+    uint64_t staged_n = 0;
+    bool staged_ok = false;
     // pinned staging for small host->device tables
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
@@ -66,6 +69,8 @@ void set_thread_error(const std::string& msg);
 
 // Grow-only device buffer.
 int ensure(Ctx* ctx, DevBuf& b, size_t bytes);
+// Free one cached buffer after the queued work that may read it (workspace policy).
+int drop(Ctx* ctx, DevBuf& b);
 // Copy a small host table to device through the pinned staging buffer (async on s).
 int upload(Ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s);
 

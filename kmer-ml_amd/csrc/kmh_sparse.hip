@@ -323,6 +323,12 @@ int sparse_count_first(Ctx* ctx, const uint8_t* d_seq, uint64_t n, int k, int ca
     KMH_HIP(ctx, hipMemcpyAsync(&m, d_nk, 8, hipMemcpyDeviceToHost, s));
     KMH_HIP(ctx, hipStreamSynchronize(s));
     if (m > nwin) return fail(ctx, KMH_ERR_HIP, "sparse count: more distinct k-mers than windows");
+    // The hash pipeline's entries, positions and pass staging (12-16 B per window) are dead:
+    // free them before order_by_first allocates, when they are large (a 3 Gbp organism at
+    // k >= 22 would otherwise peak near 200 GB of device memory).
+    if (ctx->sparse[2].bytes + ctx->sparse[6].bytes + ctx->sparse[7].bytes > ((size_t)4 << 30))
+        for (int i : {2, 6, 7})
+            if ((rc = drop(ctx, ctx->sparse[i]))) return rc;
     return order_by_first(ctx, d_codes, d_counts, d_first, m, n, codes, counts, first, s);
 }
 

@@ -35,6 +35,8 @@ SIGNATURES = [
     ("kmh_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_vp)]),
     ("kmh_ctx_destroy", None, [_vp]),
     ("kmh_ctx_release", _c.c_int, [_vp]),
+    ("kmh_ctx_workspace_bytes", _u64, [_vp]),
+    ("kmh_ctx_trim", _c.c_int, [_vp, _u64]),
     ("kmh_last_error", _c.c_char_p, [_vp]),
     ("kmh_timing_enable", _c.c_int, [_vp, _c.c_int]),
     ("kmh_timing_report", _c.c_int, [_vp, _c.POINTER(_c.c_char_p), _u64p,
@@ -46,6 +48,8 @@ SIGNATURES = [
     ("kmh_fasta_pack", _c.c_int, [_vp, _u64, _vp, _u64, _u64p, _vp]),
     ("kmh_fasta_free", None, [_vp]),
     ("kmh_count_host", _c.c_int, [_vp, _vp, _u64, _c.c_int, _c.c_int, _c.POINTER(_vp)]),
+    ("kmh_stage_host", _c.c_int, [_vp, _vp, _u64]),
+    ("kmh_count_staged", _c.c_int, [_vp, _c.c_int, _c.c_int, _c.POINTER(_vp)]),
     ("kmh_kmers_size", _u64, [_vp]),
     ("kmh_kmers_export", _c.c_int, [_vp, _vp, _vp, _vp]),
     ("kmh_kmers_data", _c.c_int, [_vp, _vp, _vp, _vp]),
@@ -137,11 +141,23 @@ def _ptr(a):
     return ctypes.c_void_p(a.ctypes.data) if a is not None else None
 
 
+def _locked(fn):
+    """Run a Context method under the context's lock: the C ABI serialises nothing itself, and
+    release() / trim() free buffers that a call in flight on another thread would still use."""
+    def wrapper(self, *args, **kwargs):
+        with self.lock:
+            return fn(self, *args, **kwargs)
+    wrapper.__name__, wrapper.__doc__ = fn.__name__, fn.__doc__
+    return wrapper
+
+
 class Context:
-    """A libkmerhip context bound to one HIP device (kmh_ctx_create)."""
+    """A libkmerhip context bound to one HIP device (kmh_ctx_create).  Every call takes
+    ``self.lock`` (re-entrant; hold it across kmh_stage_host + kmh_count_staged)."""
 
     def __init__(self, device=0):
         self.device = int(device)
+        self.lock = threading.RLock()
         h = ctypes.c_void_p()
         _check(lib().kmh_ctx_create(self.device, ctypes.byref(h)))
         self._h = h
@@ -150,15 +166,28 @@ class Context:
     def handle(self):
         return self._h
 
+    @_locked
     def close(self):
         if self._h:
             lib().kmh_ctx_destroy(self._h)
             self._h = None
 
+    @_locked
     def release(self):
         """Free the cached device workspace (kmh_ctx_release); the next call allocates again."""
         if self._h:
             _check(lib().kmh_ctx_release(self._h), self._h)
+
+    @_locked
+    def workspace_bytes(self):
+        """Device workspace + pinned staging the context holds now (kmh_ctx_workspace_bytes)."""
+        return int(lib().kmh_ctx_workspace_bytes(self._h)) if self._h else 0
+
+    @_locked
+    def trim(self, keep_bytes):
+        """kmh_ctx_trim: release the workspace if it holds more than keep_bytes."""
+        if self._h:
+            _check(lib().kmh_ctx_trim(self._h, int(keep_bytes)), self._h)
 
     def __del__(self):
         try:
@@ -167,6 +196,7 @@ class Context:
             pass
 
     # -- host-buffer counting (the drop-in path) --
+    @_locked
     def count(self, seq, k, canonical=False):
         """Distinct k-mers of ``seq`` in first-occurrence order.
 
@@ -177,29 +207,38 @@ class Context:
         r = ctypes.c_void_p()
         _check(lib().kmh_count_host(self._h, _ptr(buf), buf.size, int(k), int(bool(canonical)),
                                     ctypes.byref(r)), self._h)
-        # numpy views of the result's own arrays (no copy); they keep it alive
-        owner = _Kmers(r)
-        n = lib().kmh_kmers_size(r)
-        if n == 0:
-            return np.empty(0, np.uint64), np.empty(0, np.uint32), np.empty(0, np.uint64)
-        pc, pn, pf = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
-        _check(lib().kmh_kmers_data(r, ctypes.byref(pc), ctypes.byref(pn), ctypes.byref(pf)))
-        return (owner.view(pc, n, ctypes.c_uint64), owner.view(pn, n, ctypes.c_uint32),
-                owner.view(pf, n, ctypes.c_uint64))
+        return _kmers_arrays(r)
 
+    @_locked
+    def stage(self, seq):
+        """kmh_stage_host: copy ``seq`` to the device once for several count_staged calls."""
+        buf = _as_u8(seq)
+        _check(lib().kmh_stage_host(self._h, _ptr(buf), buf.size), self._h)
+
+    @_locked
+    def count_staged(self, k, canonical=False):
+        """count() of the sequence given to stage() (no second host-to-device copy)."""
+        r = ctypes.c_void_p()
+        _check(lib().kmh_count_staged(self._h, int(k), int(bool(canonical)), ctypes.byref(r)), self._h)
+        return _kmers_arrays(r)
+
+    @_locked
     def count_dense(self, seq, k):
         buf = _as_u8(seq)
         out = np.empty(1 << (2 * int(k)), np.uint32)
         _check(lib().kmh_count_dense_host(self._h, _ptr(buf), buf.size, int(k), _ptr(out)), self._h)
         return out
 
+
     # -- device-resident batch (pointers are device addresses, e.g. tensor.data_ptr()) --
+    @_locked
     def count_dense_dev(self, d_seq, offsets, k, d_matrix, stream=None):
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         _check(lib().kmh_count_dense_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1,
                                          int(k), ctypes.c_void_p(d_matrix),
                                          ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def count_dense_u4_dev(self, d_seq, offsets, k, d_matrix, d_u4, d_esc, cap, d_esc_n, stream=None):
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         _check(lib().kmh_count_dense_u4_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1,
@@ -207,18 +246,21 @@ class Context:
                                             ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def first_dense_dev(self, d_seq, offsets, k, d_first, stream=None):
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         _check(lib().kmh_first_dense_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1,
                                          int(k), ctypes.c_void_p(d_first),
                                          ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def synth_dev(self, d_seq, length, stride, n_genomes, seed0, stream=None):
         _check(lib().kmh_synth_dev(self._h, ctypes.c_void_p(d_seq), int(length), int(stride),
                                    int(n_genomes), int(seed0),
                                    ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- sparse counting, device-resident (BASELINE config 5) --
+    @_locked
     def count_sparse_dev(self, d_seq, offsets, k, canonical, d_codes, d_counts, d_nkmers, stream=None):
         """Distinct k-mers of G device-resident genomes (13 <= k <= 32); genome g's entries
         start at sparse_out_offsets(offsets, k)[g].  Synchronises the stream."""
@@ -229,12 +271,14 @@ class Context:
                                           ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- matrix assembly encoding (device pointers) --
+    @_locked
     def rows_encode_u8(self, d_rows, rows, cols, d_u8, d_esc, cap, d_esc_n, stream=None):
         _check(lib().kmh_rows_encode_u8_dev(self._h, ctypes.c_void_p(d_rows), int(rows), int(cols),
                                             ctypes.c_void_p(d_u8), ctypes.c_void_p(d_esc), int(cap),
                                             ctypes.c_void_p(d_esc_n),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def rows_decode_u8(self, d_u8, rows, cols, d_esc, cap, d_esc_n, ranks, rows_per_rank, d_rows,
                        stream=None):
         _check(lib().kmh_rows_decode_u8_dev(self._h, ctypes.c_void_p(d_u8), int(rows), int(cols),
@@ -242,18 +286,21 @@ class Context:
                                             int(ranks), int(rows_per_rank), ctypes.c_void_p(d_rows),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def rows_encode_u4(self, d_rows, rows, cols, d_u4, d_esc, cap, d_esc_n, stream=None):
         _check(lib().kmh_rows_encode_u4_dev(self._h, ctypes.c_void_p(d_rows), int(rows), int(cols),
                                             ctypes.c_void_p(d_u4), ctypes.c_void_p(d_esc), int(cap),
                                             ctypes.c_void_p(d_esc_n),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def rows_decode_u4(self, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, stream=None):
         _check(lib().kmh_rows_decode_u4_dev(self._h, ctypes.c_void_p(d_u4), int(rows), int(cols),
                                             ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
                                             ctypes.c_void_p(d_rows),
                                             ctypes.c_void_p(stream) if stream else None), self._h)
 
+    @_locked
     def rows_decode_u4_range(self, d_u4, rows, cols, d_esc, cap, d_esc_n, row0, nrows, d_rows, stream=None):
         _check(lib().kmh_rows_decode_u4_range_dev(self._h, ctypes.c_void_p(d_u4), int(rows), int(cols),
                                                   ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
@@ -261,6 +308,7 @@ class Context:
                                                   ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- feature columns (device pointers; statistics.py:188-238) --
+    @_locked
     def feature_columns_dev(self, d_codes, n, k, d_order, d_lg, d_cnt, d_cpg, d_rep, d_gc, d_oe, d_ent, stream=None):
         _check(lib().kmh_feature_columns_dev(self._h, ctypes.c_void_p(d_codes) if d_codes else None, int(n), int(k),
                                              ctypes.c_void_p(d_order), ctypes.c_void_p(d_lg), ctypes.c_void_p(d_cnt),
@@ -269,9 +317,11 @@ class Context:
                                              ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- kernel timing --
+    @_locked
     def timing(self, enable):
         _check(lib().kmh_timing_enable(self._h, int(bool(enable))), self._h)
 
+    @_locked
     def timing_report(self):
         cap = 64
         names = (ctypes.c_char_p * cap)()
@@ -305,6 +355,19 @@ def _as_u8(seq):
     if isinstance(seq, np.ndarray):
         return np.ascontiguousarray(seq, dtype=np.uint8)
     return np.frombuffer(bytes(seq), dtype=np.uint8)
+
+
+def _kmers_arrays(r):
+    """(codes u64, counts u32, first u64) numpy views of a kmh_kmers result (no copy; the views
+    keep the result alive)."""
+    owner = _Kmers(r)
+    n = lib().kmh_kmers_size(r)
+    if n == 0:
+        return np.empty(0, np.uint64), np.empty(0, np.uint32), np.empty(0, np.uint64)
+    pc, pn, pf = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    _check(lib().kmh_kmers_data(r, ctypes.byref(pc), ctypes.byref(pn), ctypes.byref(pf)))
+    return (owner.view(pc, n, ctypes.c_uint64), owner.view(pn, n, ctypes.c_uint32),
+            owner.view(pf, n, ctypes.c_uint64))
 
 
 class _Kmers:

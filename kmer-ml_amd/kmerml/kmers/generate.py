@@ -29,15 +29,23 @@ the reference itself, tests/golden/):
 Differences (DESIGN.md): k <= 1024 is supported (k > 1024 raises NotImplementedError;
 k >= 33 is counted by sorting ceil(k / 32) code words per window
 and its lines are written from the sequence); counting never falls back to the CPU --
-without the HIP library or a device it raises.  Size limits per organism (its kept records
-joined): below 2^32 - 1 bytes for every k, and fewer than 2^31 windows for k >= 13 (a
-3.1 Gbp human genome fits the first and not the second: it raises NotImplementedError for
-k >= 13, which extract_from_genome_list reports as "Error processing <id>" like any other
-failure).  The reference's dict has no such limit but needs tens of bytes per distinct
-k-mer of host memory.
+without the HIP library or a device it raises.  Size limit per organism (its kept records
+joined): below 2^32 - 1 bytes for every k (u32 positions and counts; a 3.1 Gbp human genome
+fits, 2^31 windows and more are counted at every k).  Larger organisms raise
+NotImplementedError, which extract_from_genome_list reports as "Error processing <id>" like
+any other failure.  The reference's dict has no such limit but needs tens of bytes per
+distinct k-mer of host memory.
+
+Device memory: the organism crosses PCIe once for all its k (kmh_stage_host, then one
+kmh_count_staged per k), and after each organism the context's cached workspace is released
+if it holds more than KMERML_WORKSPACE_MB (default 4096 MiB; kmh_ctx_trim), so a long
+extract_from_genome_list loop (generate.py:116-126) does not keep the tens of GB a large
+organism needed.
 """
+import contextlib
 import operator
 import os
+import time
 from pathlib import Path
 
 import numpy as np
@@ -46,6 +54,22 @@ from kmerml import _native
 from kmerml.utils.path_utils import ensure_directory_exists
 
 _DIGITS = {"A": "0", "T": "1", "C": "2", "G": "3"}
+
+# Stage clocks of the drop-in (bench.py's "e2e" object): set to a dict and every
+# extract_kmers_from_fasta call adds its wall seconds per stage to it.
+PROFILE = None
+
+
+@contextlib.contextmanager
+def _stage(name):
+    if PROFILE is None:
+        yield
+        return
+    t0 = time.perf_counter()
+    try:
+        yield
+    finally:
+        PROFILE[name] = PROFILE.get(name, 0.0) + time.perf_counter() - t0
 
 
 def _device():
@@ -67,7 +91,8 @@ class KmerExtractor:
         multiplicity = {k: 0 for k in k_order}
         for k in k_values:                            # the loop of generate.py:49
             multiplicity[k] += 1
-        fasta = _native.FastaFile(fasta_file)
+        with _stage("parse"):
+            fasta = _native.FastaFile(fasta_file)
         results = {}
         packed = np.zeros(0, np.uint8)
         if len(fasta):
@@ -75,18 +100,9 @@ class KmerExtractor:
             if not all(_is_index(k) for k in k_values):
                 _raise_like_reference(fasta, k_values, longest)
                 longest = float("inf")                # no record is kept: nothing to count
-            packed, kept = fasta.pack(_min_len(longest))
-            ctx = None
-            for k in k_order:
-                if not kept.any():
-                    break
-                kv = operator.index(k)                # True / False count as k = 1 / 0
-                if kv >= 1:
-                    ctx = ctx or _native.context(_device())
-                    results[k] = ctx.count(packed, kv)
-                else:
-                    bodies = bytes(packed).split(b"\n")[:int(kept.sum())]
-                    results[k] = _count_degenerate(bodies, kv)
+            with _stage("pack"):
+                packed, kept = fasta.pack(_min_len(longest))
+            results = _count_all(packed, kept, k_order)
             for rid, keep in zip(fasta.ids, kept):
                 if keep:
                     print(f"Processed chromosome/contig: {rid}")
@@ -105,10 +121,13 @@ class KmerExtractor:
             codes, counts, first = res
             kv = operator.index(k)
             counts = np.multiply(counts, np.uint64(multiplicity[k]), dtype=np.uint64)
-            if kv > 32:   # a code holds 32 bases: the line digits come from the sequence
-                self._write_bytes(path, _native.format_lines_seq(kv, packed, first, counts))
-            else:
-                self._write_bytes(path, _native.format_lines_array(kv, codes, counts))
+            with _stage("format"):
+                if kv > 32:   # a code holds 32 bases: the line digits come from the sequence
+                    text = _native.format_lines_seq(kv, packed, first, counts)
+                else:
+                    text = _native.format_lines_array(kv, codes, counts)
+            with _stage("write"):
+                self._write_bytes(path, text)
         return organism_id
 
     def _kmer_path(self, organism_id, k):
@@ -143,6 +162,42 @@ class KmerExtractor:
                 print(f"Error processing {org_id}: {str(e)}")
         print(f"Completed processing {len(processed_ids)} out of {total} genomes")
         return processed_ids
+
+
+def _count_all(packed, kept, k_order):
+    """{k: result} for the kept records joined in ``packed``: the GPU counts every k >= 1 from one
+    device copy of the organism; k <= 0 is counted on the host."""
+    results = {}
+    if not kept.any():
+        return results
+    ctx = None
+    try:
+        for k in k_order:
+            kv = operator.index(k)                # True / False count as k = 1 / 0
+            if kv >= 1:
+                if ctx is None:                   # one host-to-device copy for every k
+                    ctx = _native.context(_device())
+                    ctx.lock.acquire()
+                    with _stage("h2d"):
+                        ctx.stage(packed)
+                with _stage("count"):             # kernels, first-occurrence order, D2H
+                    results[k] = ctx.count_staged(kv)
+            else:
+                bodies = bytes(packed).split(b"\n")[:int(kept.sum())]
+                results[k] = _count_degenerate(bodies, kv)
+    finally:
+        if ctx is not None:
+            try:
+                with _stage("trim"):
+                    ctx.trim(_workspace_limit())
+            finally:
+                ctx.lock.release()
+    return results
+
+
+def _workspace_limit():
+    """Bytes of device workspace a context may keep between organisms (KMERML_WORKSPACE_MB)."""
+    return int(os.environ.get("KMERML_WORKSPACE_MB", "4096")) << 20
 
 
 def _is_index(k):

@@ -399,6 +399,17 @@ def _code_features_hip(k, codes):
             'cpg_obs_exp': oe.cpu().numpy(), 'shannon_entropy': ent.cpu().numpy()}
 
 
+def _hip_library_loads():
+    """True if libkmerhip.so loads (the feature kernel needs it); a host with a GPU but no HIP
+    build keeps the torch path of this CPU-side consumer."""
+    from kmerml import _native
+    try:
+        _native.lib()
+        return True
+    except (ImportError, OSError):
+        return False
+
+
 def _code_features(k, codes):
     """statistics.py:188-238 for the compat labels of `codes` (None: all 4^k codes).  Same
     IEEE operations as the reference, per value: gc = (g + c) / L * 100; expected =
@@ -408,7 +419,7 @@ def _code_features(k, codes):
     the CPU (this consumer of the k-mer files is a CPU program in the reference)."""
     import torch
 
-    if torch.cuda.is_available():
+    if torch.cuda.is_available() and torch.version.hip and _hip_library_loads():
         return _code_features_hip(k, codes)
     dev = torch.device("cpu")
     i64 = torch.int64

@@ -63,6 +63,17 @@ def kmer_text(kmers):
     return "".join(out)
 
 
+def save_kmers(kmers, path):
+    """_save_kmers_to_file's write loop (generate.py:84-91) for compress=False (the CLI default,
+    scripts/extract_kmers.py:19-20): text mode, one f.write per k-mer, digits built by the same
+    per-base generator expression.  bench.py times it as the reference's save phase."""
+    encoding = {'A': 0, 'T': 1, 'C': 2, 'G': 3}
+    with open(path, "w") as f:
+        for kmer, count in kmers.items():
+            numeric_kmer = ''.join(str(encoding.get(base, 'X')) for base in kmer)
+            f.write(f"{numeric_kmer}\t{count}\n")
+
+
 _CODE = {"A": 0, "C": 1, "G": 2, "T": 3}
 
 

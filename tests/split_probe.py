@@ -34,4 +34,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    from kmerml.utils.devmem import run_guarded
+    run_guarded(main)

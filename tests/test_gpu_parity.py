@@ -732,7 +732,7 @@ def test_sparse_dev_rejects_k(ctx, dev, k):
 
 
 # ---------------------------------------------------------------- RCCL code paths, one GPU
-def _torchrun(args, timeout=600, nproc=1, env=None):
+def _torchrun(args, timeout=600, nproc=1, env=None, gib_per_rank=4):
     import gc
     import socket
     import subprocess
@@ -743,6 +743,12 @@ def _torchrun(args, timeout=600, nproc=1, env=None):
     _native.release_all()
     gc.collect()
     torch.cuda.empty_cache()
+    # ... and refuse to start ranks that cannot fit (a rank that still runs out reports its own
+    # allocation failure and hipMemGetInfo: kmerml.utils.devmem.run_guarded)
+    free, total = torch.cuda.mem_get_info()
+    need = nproc * gib_per_rank * 2**30
+    assert free >= need, (f"{nproc} ranks need ~{nproc * gib_per_rank} GiB of device memory; "
+                          f"free {free / 2**30:.1f} of {total / 2**30:.1f} GiB before launch")
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -1017,7 +1023,7 @@ def test_config4_per_rank_workload_eight_ranks(tmp_path, oracle_lib, wire):
     (reference anchor: the organisms x k-mers matrix of features.py:85-117)."""
     r = _torchrun(["bench.py", "--gpus", "8", "--backend", "gloo", "--single-device", "--assemble", wire,
                    "--steps", "2", "--warmup", "1", "--cpu-sample", "0", "--check-dir", str(tmp_path)],
-                  nproc=8, timeout=800)
+                  nproc=8, timeout=800, gib_per_rank=24)
     assert r.returncode == 0, _failure(r)
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["rows_checked"] is True and d["assembly_checked"] is True
@@ -1041,7 +1047,7 @@ def test_config4_assembly_fallbacks_full_size(tmp_path, oracle_lib, caps, wire):
     env = dict(os.environ, **caps)
     here = os.path.dirname(os.path.abspath(__file__))
     r = _torchrun([os.path.join(here, "assembly_probe.py"), str(tmp_path), "64", "100000000", "12", "gloo",
-                   "--single-device"], nproc=8, timeout=800, env=env)
+                   "--single-device"], nproc=8, timeout=800, env=env, gib_per_rank=24)
     assert r.returncode == 0, _failure(r)
     res = json.load(open(tmp_path / "result.json"))
     assert res == {"wire": wire, "assembly_checked": True, "world": 8}
@@ -1116,3 +1122,33 @@ def test_sparse_rows_from_fasta(tmp_path, oracle_lib, k, canonical):
     for (codes, counts), seq in zip(rows, seqs):
         wc, wn, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), k, canonical=canonical)
         assert np.array_equal(codes, wc) and np.array_equal(counts, wn)
+
+
+def test_dropin_workspace_trim_and_staging(ctx, oracle_lib, monkeypatch):
+    """The drop-in's device-memory policy: one 250 Mbp organism
+    counted at k = 21 and k = 12 through the drop-in's counting core (generate._count_all: one
+    kmh_stage_host, one kmh_count_staged per k, then kmh_ctx_trim).  With a high mark the context
+    keeps its workspace (tens of GB after k = 21); with the default-style mark it is released
+    after the organism, so the serial loop of generate.py:116-126 does not hold it between
+    genomes.  Counts are checked by their sums (every window of an all-ACGT genome)."""
+    from kmerml.kmers import generate as kgen
+    L = 250_000_000
+    packed = oracle_lib.synth(L, osynth.genome_seed(3))
+    kept = np.ones(1, bool)
+    c = _native.context(0)
+    c.release()
+    monkeypatch.setenv("KMERML_WORKSPACE_MB", str(1 << 20))      # 1 TiB: nothing is released
+    res = kgen._count_all(packed, kept, [21, 12])
+    held = c.workspace_bytes()
+    assert held > (4 << 30), held
+    for k in (21, 12):
+        codes, counts, first = res[k]
+        assert int(counts.sum(dtype=np.uint64)) == L - k + 1
+        assert first[0] == 0 and np.all(np.diff(first.astype(np.int64)) > 0)
+    monkeypatch.setenv("KMERML_WORKSPACE_MB", "2048")
+    res2 = kgen._count_all(packed, kept, [21])
+    assert c.workspace_bytes() <= (2048 << 20)
+    assert np.array_equal(res2[21][0], res[21][0]) and np.array_equal(res2[21][1], res[21][1])
+    # the staging is gone with the workspace: counting it again must fail loudly, not read freed memory
+    with pytest.raises(ValueError):
+        c.count_staged(21)
