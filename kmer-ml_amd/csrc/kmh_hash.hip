@@ -19,13 +19,15 @@
 //  3. k_sp_split      one workgroup per split item: gathers the bucket's segments of its
 //                     tiles (16-byte chunk loads, entries outside the segment masked by
 //                     position), partitions them by pass (LDS histogram, scan, scatter) and
-//                     stores them contiguously with per-pass offsets toff2[item][pass].
+//                     appends each pass's run to that pass's own region (one count item's
+//                     keys, contiguous), at an offset reserved by one atomic per (item, pass).
 //  4. k_sp_count      one item per (genome, bucket, pass), two persistent workgroups per CU:
-//                     reads that pass's segment of every split item of the bucket into
-//                     registers and deduplicates it by an LDS counting sort on the key's
-//                     position inside the pass (8192 bins of about one key; equal keys share
-//                     a bin), then emits each distinct key with its count, position-parallel;
-//                     bins of repeated keys go through a small LDS hash table.
+//                     reads its region (contiguous: no segment lookup) into registers and
+//                     deduplicates it by an LDS counting sort on the key's position inside the
+//                     pass (8192 bins of about one key; equal keys share a bin); each thread
+//                     then resolves 16 consecutive sorted positions from registers (neighbours
+//                     +-3 compared, +-4 binned) and the rare bins that reach further by their
+//                     exact range; bins of repeated keys go through a small LDS hash table.
 //  5. fallback        a split item whose entries exceed its staging, or an item the count
 //                     kernel cannot hold, emits nothing; those passes are counted by
 //                     gather + the hand-written radix sort of kmh_sort.hip + run-length
@@ -50,6 +52,10 @@ constexpr int kQueue = 512;                // per-wave chunk queue of the split 
 #define KMH_SP_QU 4
 #endif
 constexpr int kQU = KMH_SP_QU;             // chunk loads in flight per lane (split kernel)
+
+#ifndef KMH_SP_SPLIT_V4
+#define KMH_SP_SPLIT_V4 0   // split: 16-byte stores into the count items' regions (A/B)
+#endif
 
 // Entry width: u32 residues (k <= 21) or u64 (22 <= k <= 32).  A u64 tile holds half the windows,
 // so a tile's entries (128 KiB) and a split item's staging (80 KiB) keep their LDS size.
@@ -77,6 +83,13 @@ template <> struct Sp<uint64_t, true> {
     static constexpr int TILE = kSpThreads * WPT;  // 8192 (96 KiB)
     static constexpr int CAPS = 5120;              // 60 KiB
 };
+// Keys of one count item (one pass of a bucket): the capacity of its region and of the count
+// kernel's LDS staging (the bin sort of k_sp_count); half with positions.
+template <typename E, bool POS> struct Cnt;
+template <> struct Cnt<uint32_t, false> { static constexpr int CAP = 8192; };
+template <> struct Cnt<uint64_t, false> { static constexpr int CAP = 4096; };
+template <> struct Cnt<uint32_t, true> { static constexpr int CAP = 4096; };    // + positions
+template <> struct Cnt<uint64_t, true> { static constexpr int CAP = 2048; };
 template <typename E> constexpr int epc() { return 16 / (int)sizeof(E); }   // entries per chunk
 // 16-byte chunks of a tile's entries (8192, or 4096 with positions) and the bits of a queue
 // entry that hold the chunk (the rest hold the tile within the batch)
@@ -92,8 +105,10 @@ __host__ __device__ __forceinline__ uint32_t split_bt(uint32_t per, uint32_t epc
     return bt < 1u ? 1u : (bt > 64u ? 64u : bt);
 }
 
-constexpr int kMaxPasses = 1024;           // passes of one bucket (a 2^32-window genome needs ~512)
-constexpr int kT2 = kMaxPasses + 1;        // toff2 row stride
+// Passes of one bucket.  With positions (the drop-in) a pass holds 1920-3840 keys, so a bucket of
+// a 2^32-window organism needs ~2200 passes; the split keeps a pass's staging start and region
+// offset as u16 halves of one LDS word (4096 words).
+constexpr int kMaxPasses = 4096;
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
 
 // 2-bit-group reversal of the low 2K bits of ~x: the reverse complement of a K-mer code.
@@ -200,7 +215,6 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     constexpr uint64_t RM = (1ull << R) - 1ull;
     constexpr int WPT = Sp<E, POS>::WPT, kSpTile = Sp<E, POS>::TILE, EPC = epc<E>();
     static_assert(kSpBuckets == kSpThreads, "one bucket per thread in the scan");
-    static_assert(kMaxPasses <= kSpThreads, "one pass per thread in the split scan");
     static_assert(R <= 8 * (int)sizeof(E), "residues fit the entry");
     __shared__ __attribute__((aligned(16))) E sorted[kSpTile];
     __shared__ __attribute__((aligned(16))) uint32_t spos[POS ? kSpTile : 4];
@@ -356,6 +370,9 @@ struct SplitItem {
     uint32_t b, t0, t1, np;
     uint32_t gb;       // (genome, bucket) index within the batch: failure flag slot
     uint32_t per;      // expected entries per tile of this bucket
+    uint32_t cbase;    // count item of pass 0 of this (genome, bucket): pass p's region and
+                       // fill counter are those of count item cbase + p
+    uint32_t pad;
 };
 
 // Positions of entries [4 c, 4 c + 4) (u32 entries) or [2 c, 2 c + 2) (u64) of a tile's layout.
@@ -553,8 +570,9 @@ template <typename E, bool POS>
 __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     const E* __restrict__ ent, const uint32_t* __restrict__ epos, const uint16_t* __restrict__ toff, uint32_t ldt,
     const SplitItem* __restrict__ items, uint32_t nitems, int R, E* __restrict__ out, uint32_t* __restrict__ opos,
-    uint16_t* __restrict__ toff2, uint32_t* __restrict__ gb_fail) {
-    constexpr int kCaps = Sp<E, POS>::CAPS, EPC = epc<E>();
+    uint32_t* __restrict__ pfill, uint32_t* __restrict__ gb_fail) {
+    constexpr int kCaps = Sp<E, POS>::CAPS, EPC = epc<E>(), C = Cnt<E, POS>::CAP;
+    static_assert(kCaps < 65536, "staging offsets fit 16 bits");
     __shared__ __attribute__((aligned(16))) E sorted[kCaps + 64];   // + scratch tail for out-of-segment lanes
     __shared__ __attribute__((aligned(16))) uint32_t spos[POS ? kCaps + 64 : 4];
     // pass counters: np <= kRepP passes -- every item of config 5 (~32) -- count in 32 bank
@@ -562,11 +580,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // address or a bank, where 64 lanes on ~32 plain counters collided); more passes: one
     // counter each.  Out-of-segment entries count into 32 dummies past the replicas.
     constexpr int kRepP = 128;
-    static_assert(kRepP * 32 == 4 * kSpThreads && kMaxPasses + 32 <= kRepP * 32, "counter layout");
+    static_assert(kRepP * 32 == 4 * kSpThreads && kMaxPasses <= kRepP * 32, "counter layout");
     __shared__ __attribute__((aligned(16))) uint32_t hist[kRepP * 32 + 32];
     __shared__ uint32_t q[kNW][kQueue];
     __shared__ uint32_t slo[kNW][64], shi[kNW][64];
     __shared__ uint32_t wsum[kNW], total_sh;
+    __shared__ uint32_t pst[kMaxPasses + 1];   // staging start of every pass (+ the end)
     uint4* hist4 = reinterpret_cast<uint4*>(hist);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -678,15 +697,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         KMH_ST(2)
         lds_barrier();
         KMH_ST(3)
-        // exclusive scan of the counters (pass-major): thread t owns counters 4t .. 4t + 3
-        // (replicated) or counter t; pass p starts at counter 32p (thread 8p) or p
+        // exclusive scan of the counters (pass-major): thread t owns counters 4t .. 4t + 3 (pass p's
+        // 32 replicas are counters 32p .. 32p + 31, i.e. threads 8p .. 8p + 7; without replicas
+        // counter p); counters past the item's passes are zero
         {
-            uint4 cv = make_uint4(0u, 0u, 0u, 0u);
-            if (rep) {
-                if ((uint32_t)tid < np * 8u) cv = hist4[tid];
-            } else {
-                cv.x = hist[tid];
-            }
+            const uint4 cv = hist4[tid];
             const uint32_t sm = cv.x + cv.y + cv.z + cv.w;
             const uint32_t incl = scan64(sm);
             if (lane == 63) wsum[wave] = incl;
@@ -699,18 +714,20 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                 tot += x;
             }
             const uint32_t ex = pre + incl - sm;
+            const uint32_t e1 = ex + cv.x, e2 = e1 + cv.y, e3 = e2 + cv.z;
+            hist4[tid] = make_uint4(ex, e1, e2, e3);
             if (rep) {
-                if ((uint32_t)tid < np * 8u) {
-                    hist4[tid] = make_uint4(ex, ex + cv.x, ex + cv.x + cv.y, ex + cv.x + cv.y + cv.z);
-                    if ((tid & 7) == 0) toff2[(uint64_t)item * kT2 + (uint32_t)tid / 8u] = (uint16_t)ex;
-                }
+                if ((tid & 7) == 0 && (uint32_t)tid / 8u < np) pst[tid / 8] = ex;
             } else {
-                hist[tid] = ex;
-                if ((uint32_t)tid < np) toff2[(uint64_t)item * kT2 + tid] = (uint16_t)ex;
+                const uint32_t p0 = 4u * (uint32_t)tid;
+                if (p0 < np) pst[p0] = ex;
+                if (p0 + 1u < np) pst[p0 + 1u] = e1;
+                if (p0 + 2u < np) pst[p0 + 2u] = e2;
+                if (p0 + 3u < np) pst[p0 + 3u] = e3;
             }
             if (tid == 0) {
                 total_sh = tot;
-                toff2[(uint64_t)item * kT2 + np] = (uint16_t)(tot <= (uint32_t)kCaps ? tot : 0u);
+                pst[np] = tot;
                 if (tot > (uint32_t)kCaps) gb_fail[cur.gb] = 1u;   // staging overflow: the bucket goes to the fallback
             }
         }
@@ -718,6 +735,26 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         KMH_ST(4)
         const uint32_t total = total_sh;
         const bool fits = total <= (uint32_t)kCaps;   // uniform
+        // Region offsets of this item's passes: lane j of wave w reserves pass w + 16 (64 r + j)'s
+        // run in that count item's region (one returning atomic per pass, in flight during the
+        // scatter; read by readlane in the stores)
+        constexpr int kRR = (kMaxPasses + 64 * kNW - 1) / (64 * kNW);
+        uint32_t aoff[kRR];
+#pragma unroll
+        for (int r = 0; r < kRR; ++r) {
+            aoff[r] = 0u;
+            const uint32_t p = (uint32_t)wave + (uint32_t)kNW * (64u * (uint32_t)r + (uint32_t)lane);
+            if (fits && p < np) {
+                const uint32_t c = pst[p + 1] - pst[p];
+#if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 2
+                // what-if: no returning atomic to wait for (every split item writes its run at the
+                // region's start: counts wrong; timing only)
+                if (c) atomicAdd(&pfill[cur.cbase + p], c);
+#else
+                if (c) aoff[r] = atomicAdd(&pfill[cur.cbase + p], c);
+#endif
+            }
+        }
         if (fits) {
             auto scatter = [&](E r, uint32_t p, bool ok) {
                 const uint32_t slot = atomicAdd(&hist[ctr(r, ok)], 1u);
@@ -738,22 +775,62 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         KMH_ST(7)
         hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next item starts after a barrier
 
-        // (D) this item's stores
+        // (D) this item's stores: pass p's run of the staging [pst[p], pst[p + 1]) is appended to
+        // count item cbase + p's region at the reserved offset; entries past the region's capacity
+        // are dropped (that item's fill counter then exceeds C: it goes to the fallback)
 #if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 1
         if (fits && total == 0xFFFFFFFFu) {   // what-if: no split output (timing of the split only)
 #else
         if (fits) {
 #endif
-            E* dst = out + (uint64_t)item * kCaps;
-            const uint32_t n4 = total / EPC;
-            for (uint32_t i = tid; i < n4; i += kSpThreads)
-                store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
-            if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
-            if constexpr (POS) {
-                uint32_t* pdst = opos + (uint64_t)item * kCaps;
-                for (uint32_t i = tid; i < total / 4; i += kSpThreads)
-                    store_nt(reinterpret_cast<uint4*>(pdst) + i, reinterpret_cast<const uint4*>(spos)[i]);
-                if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
+            for (uint32_t k = 0; (uint32_t)wave + (uint32_t)kNW * k < np; ++k) {   // (uniform)
+                const uint32_t p = (uint32_t)wave + (uint32_t)kNW * k;
+                const uint32_t r = k / 64u;   // (uniform; a select chain, not a dynamic register index)
+                uint32_t av = aoff[0];
+#pragma unroll
+                for (int q = 1; q < kRR; ++q) av = r == (uint32_t)q ? aoff[q] : av;
+                const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)av, (int)(k % 64u));
+                const uint32_t s0 = pst[p], n = pst[p + 1] - s0;
+                const uint32_t lim = o < (uint32_t)C ? min(n, (uint32_t)C - o) : 0u;
+                const uint64_t d = (uint64_t)(cur.cbase + p) * C + o;
+#if KMH_SP_SPLIT_V4
+                // 16-byte stores on the region's 16-byte boundaries (the run's first and last few
+                // entries one by one); the staging side is read at whatever alignment the run has
+                // there (a uniform choice per pass)
+                {
+                    const uint32_t mis = (uint32_t)(d % (uint64_t)EPC);
+                    const uint32_t head = min(((uint32_t)EPC - mis) % (uint32_t)EPC, lim);
+                    const uint32_t nb = (lim - head) / (uint32_t)EPC, tb = head + nb * (uint32_t)EPC;
+                    if ((uint32_t)lane < head) __builtin_nontemporal_store(sorted[s0 + lane], out + d + lane);
+                    const uint32_t qs = s0 + head;
+                    uint4* dst4 = reinterpret_cast<uint4*>(out + d + head);
+                    if (qs % (uint32_t)EPC == 0u) {
+                        const uint4* src4 = reinterpret_cast<const uint4*>(sorted) + qs / (uint32_t)EPC;
+                        for (uint32_t c = (uint32_t)lane; c < nb; c += 64u) store_nt(dst4 + c, src4[c]);
+                    } else if (sizeof(E) == 4 && (qs & 1u) == 0u) {
+                        const uint2* src2 = reinterpret_cast<const uint2*>(sorted) + qs / 2u;
+                        for (uint32_t c = (uint32_t)lane; c < nb; c += 64u) {
+                            const uint2 a = src2[2u * c], b = src2[2u * c + 1u];
+                            store_nt(dst4 + c, make_uint4(a.x, a.y, b.x, b.y));
+                        }
+                    } else {
+                        const uint32_t* src1 = reinterpret_cast<const uint32_t*>(sorted + qs);
+                        for (uint32_t c = (uint32_t)lane; c < nb; c += 64u)
+                            store_nt(dst4 + c, make_uint4(src1[4u * c], src1[4u * c + 1u], src1[4u * c + 2u],
+                                                          src1[4u * c + 3u]));
+                    }
+                    if ((uint32_t)lane < lim - tb)
+                        __builtin_nontemporal_store(sorted[s0 + tb + lane], out + d + tb + lane);
+                    if constexpr (POS)
+                        for (uint32_t i = (uint32_t)lane; i < lim; i += 64u)
+                            __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
+                }
+#else
+                for (uint32_t i = (uint32_t)lane; i < lim; i += 64u) {
+                    __builtin_nontemporal_store(sorted[s0 + i], out + d + i);
+                    if constexpr (POS) __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
+                }
+#endif
             }
         }
         KMH_ST(8)
@@ -780,12 +857,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
 #endif
 }
 
-// Count work item: pass p of bucket b of genome g; its entries are segment p of split items
-// [s0, s1).
+// Count work item: pass p of bucket b of genome g; its keys are the first pfill[item] entries of
+// its region (item * Cnt<E, POS>::CAP), appended by the split items of the bucket.
 struct CountItem {
     uint32_t g, b, p, np;
-    uint32_t s0, s1;
-    uint32_t gb, n;
+    uint32_t gb, n;    // (genome, bucket) index in the batch; the bucket's entries
 };
 
 // Work items of one (genome, bucket) with n entries over nt tiles: P = ceil(n / target)
@@ -877,13 +953,13 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
     const uint32_t b = (uint32_t)(gb % kSpBuckets);
     const uint32_t ta = (uint32_t)(tbase[g] - tile_lo), tb = (uint32_t)(tbase[g + 1] - tile_lo);
     const GbRule r(n, tb - ta, target, split_target, epc);
-    const uint32_t s0 = sofs[gb], s1 = s0 + r.nsplit;
+    const uint32_t s0 = sofs[gb];
     for (uint32_t i = threadIdx.x; i < r.nsplit; i += 64u) {
         const uint32_t t = ta + i * r.ts;
-        sitems[s0 + i] = SplitItem{b, t, min(t + r.ts, tb), r.np, (uint32_t)gb, r.per};
+        sitems[s0 + i] = SplitItem{b, t, min(t + r.ts, tb), r.np, (uint32_t)gb, r.per, cofs[gb], 0u};
     }
     for (uint32_t p = threadIdx.x; p < r.np; p += 64u)
-        citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, s0, s1, (uint32_t)gb, n};
+        citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, (uint32_t)gb, n};
 }
 
 // Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel).
@@ -900,21 +976,17 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // The keys of pass p of a bucket are the residues r with floor(r * np / 2^R) = p, so
 // (r * np) mod 2^R is increasing in r and spread evenly over [0, 2^R): its top 13 bits give
 // 8192 bins of about one key each (8192 keys per item).  Equal keys share a bin, so after a
-// counting sort (histogram, scan, scatter: one LDS atomic per key per pass over the keys,
-// no probing and no per-lane tail) a thread dedups its own 8 bins by comparing the few keys
-// of each.  A bin of more than kBig keys (a repeated k-mer) goes through a small LDS hash
-// table instead, so repeats cost what they cost the hash kernel before.
+// counting sort (histogram, scan, scatter: one LDS atomic per key per pass over the keys, no
+// probing and no per-lane tail) every distinct key is resolved by comparing the few keys of its
+// bin.  A bin of more than BIG keys (a repeated k-mer) goes through a small LDS hash table
+// instead, so repeats cost what they cost the hash kernel before.
 constexpr int kBinBits = 13, kBins = 1 << kBinBits;
-constexpr int kBig = 32;         // keys of a bin deduplicated by comparison
+constexpr int kBig = 32;         // positions: keys of a bin resolved by comparison (byte counts)
+constexpr int kBigN = 14;        // no positions: the same, counts kept as nibbles
 constexpr int kHSlots = 1024;    // hash table of the big bins
 constexpr int kMaxBig = 256;     // big bins of one item (more: the item goes to the fallback)
-constexpr int kCntThreads = 512; // two count workgroups per CU (74 KiB of LDS each) hide each
+constexpr int kCntThreads = 512; // two count workgroups per CU (~78 KiB of LDS each) hide each
                                  // other's load latency
-template <typename E, bool POS> struct Cnt;
-template <> struct Cnt<uint32_t, false> { static constexpr int CAP = 8192; };   // keys of one item
-template <> struct Cnt<uint64_t, false> { static constexpr int CAP = 4096; };
-template <> struct Cnt<uint32_t, true> { static constexpr int CAP = 4096; };    // + positions
-template <> struct Cnt<uint64_t, true> { static constexpr int CAP = 2048; };
 
 #ifdef KMH_EXPERIMENTS
 __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks of k_sp_count
@@ -924,34 +996,46 @@ __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks 
 #endif
 
 // Persistent, two workgroups per CU; XCD x (= blockIdx % 8) takes a contiguous run of the
-// items (the passes of a bucket read neighbouring segments and the same toff2 lines, which then
-// meet in one L2) and its workgroups stride through it.  Software-pipelined over items, so that
-// no global latency is waited for inside an item: the keys of item i + 1 are loaded into
-// registers right after item i's scatter (its own keys are dead then) and land during item i's
-// emission; they are counted into the histogram (cleared behind the emission) before item i's
-// output stores are issued, so the wait for them never queues behind those stores (loads and
-// stores share one in-order counter); segment bounds are loaded one item ahead of their keys
-// and descriptors one item ahead of their bounds; the output base (one global atomic per item)
-// returns during the next item's histogram.  Item i's keys are re-read from `sorted` for its
-// stores (still intact: item i + 1's scatter comes after them), so a lane holds only the next
-// item's keys, its emission flags and its packed counts across the phases.
+// items and its workgroups stride through it.  Software-pipelined over items, so that no global
+// latency is waited for inside an item: the keys of item i + 1 are loaded into registers right
+// after item i's scatter (its own keys are dead then) and land during item i's emission; they
+// are counted into the histogram (cleared behind the emission) before item i's output stores
+// are issued, so the wait for them never queues behind those stores (loads and stores share one
+// in-order counter); descriptors (with the item's key count, pfill) are loaded two items ahead;
+// the output base (one global atomic per item) returns during the next item's histogram.  Item
+// i's keys are re-read from `sorted` for its stores (still intact: item i + 1's scatter comes
+// after them), so a lane holds only the next item's keys and its emission results across the
+// phases.
+//
+// Emission.  Without positions (config 5), thread t resolves the KPL consecutive sorted positions
+// KPL t .. KPL t + KPL - 1 from registers: it reads them and the 4 positions on each side with
+// 16-byte LDS reads; a key is first iff none of the 3 positions before it holds the same key, its
+// count is 1 + the equal keys among the 3 after it -- complete whenever its bin lies within those
+// +-3 positions, i.e. the keys 4 before and 4 after it fall in other bins (binned from the same
+// registers).  The few positions whose bin reaches further (bins of 5+ keys) or that sit within 4
+// of the item's ends are resolved by the exact bin range (hist).  Each position's result, 0 (not
+// first) or its count (<= kBigN), goes to a 4-bit LDS table that the stores (lane-consecutive
+// positions, coalesced) read.  With positions (the drop-in: every k-mer's first position is the
+// minimum over its copies), positions are resolved lane-consecutively by four rounds of reads of
+// the bin's keys 0..3 (clamped) and a loop for larger bins.
 template <typename E, bool POS>
 __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_count(
-    const E* __restrict__ split, const uint32_t* __restrict__ opos, const uint16_t* __restrict__ toff2,
+    const E* __restrict__ split, const uint32_t* __restrict__ opos, const uint32_t* __restrict__ pfill,
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
     const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ firsts, unsigned long long* __restrict__ nk,
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
     constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E, POS>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
     constexpr int BQ = BPT / 4;   // uint4 words of a thread's bins
-#ifndef KMH_SP_CU
-#define KMH_SP_CU 4
-#endif
-    constexpr int kCaps = Sp<E, POS>::CAPS, U = KMH_SP_CU;
     constexpr bool WIDE = sizeof(E) == 8;
-    constexpr int KPL = C / NT;          // keys per lane of a single-group item
-    constexpr int ECW = (KPL + 3) / 4;   // words of a lane's emission counts, 8 bits each (<= kBig)
+    constexpr int KPL = C / NT;          // keys per lane
+    constexpr int ECW = (KPL + 3) / 4;   // POS: words of a lane's emission counts, 8 bits each (<= kBig)
+    constexpr int BIG = POS ? kBig : kBigN;
+    constexpr int EPC = epc<E>();        // keys per 16-byte LDS read
+    constexpr int NW = KPL + 8;          // !POS: a thread's keys and the 4 on each side
     static_assert(BPT % 4 == 0 && HPT >= 1 && C % NT == 0 && KPL <= 32 && kBig < 256, "thread layout");
+    static_assert(POS || (KPL == 8 || KPL == 16), "nibble layout: 8 or 16 positions per thread");
+    static_assert(KPL % EPC == 0 && 4 % EPC == 0, "16-byte reads of a thread's keys");
     // + 32 dummy counters and a 64-entry scratch tail: a lane past its keys adds to a dummy and
     // scatters into the tail, so no exec-mask branch surrounds the atomics of a key
     __shared__ __attribute__((aligned(16))) uint32_t hist[kBins + 32];
@@ -961,6 +1045,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     __shared__ unsigned long long htab[kHSlots];
     __shared__ uint32_t bigl[kMaxBig];
     __shared__ uint32_t wtot[kNW];
+    __shared__ uint32_t scnt[kNW];                  // !POS: keys each storing wave emits
+    __shared__ __attribute__((aligned(16))) uint32_t nib[POS ? 4 : C / 8];   // !POS: 4 bits per position
     __shared__ uint32_t nbig, bad;
     __shared__ unsigned long long obase;
 
@@ -993,6 +1079,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         for (int q = 0; q < HPT; ++q) hmin[q * NT + tid] = 0xFFFFFFFFu;
     }
     if (tid == 0) nbig = bad = 0u;
+    if (tid < kNW) scnt[tid] = 0u;
 
     // bin = top 13 bits of (r * np) mod 2^R; u32 residues: (r << (32 - R)) * np mod 2^32 is that
     // value shifted to the top of a word (one 32-bit multiply)
@@ -1001,151 +1088,52 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         else return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
     };
 
-    // An item as loaded: its descriptor and the gb_fail flag of its bucket (a pass of a bucket
-    // whose split overflowed is left to the fallback: it counts as an item without keys).
-    // Used an item after it was loaded, so the scalar loads have landed.
+    // An item as loaded: its descriptor, the gb_fail flag of its bucket (a pass of a bucket whose
+    // split overflowed is left to the fallback: it counts as an item without keys) and its key
+    // count (the fill counter the split items appended to).  Used two items after it was loaded,
+    // so the scalar loads have landed.
     struct Desc {
         CountItem c;
-        uint32_t skip;
+        uint32_t skip, n, idx;
     };
     auto load_desc = [&](uint32_t i) {
         Desc d;
         d.c = items[i];
         d.skip = gb_fail[d.c.gb];
+        d.n = pfill[i];
+        d.idx = i;
         return d;
     };
-    // split items of the item's group (0 for a skipped item); single: at most one group of 64
-    auto nseg = [&](const Desc& d) -> uint32_t { return d.skip ? 0u : d.c.s1 - d.c.s0; };
-    // this lane's segment [lo, hi) of split item s0 + lane of a single-group item; the loads are
-    // unconditional (entry 0 for lanes past the group) and masked where they are used
-    struct Bnd {
-        uint32_t lo, hi;
-    };
-    auto load_bounds = [&](const Desc& d) {
-        const uint32_t ns = nseg(d);
-        const bool in = ns <= 64u && (uint32_t)lane < ns;
-        const uint64_t r = in ? (uint64_t)(d.c.s0 + (uint32_t)lane) * kT2 + d.c.p : 0u;
-        Bnd b;
-        b.lo = toff2[r];
-        b.hi = toff2[r + (in ? 1u : 0u)];
-        return b;
-    };
+    auto keys_of = [&](const Desc& d) -> uint32_t { return d.skip ? 0u : d.n; };
 
-    // Issues the loads of a single-group item's keys into kr / kp (every lane's share of at most
-    // KPL keys, all in flight, nobody waits for them here; segment lookup by wave-uniform
-    // shuffles) and returns the item's key count (0 for a multi-group item, which walk() counts).
-    auto issue_keys = [&](const Desc& d, const Bnd& bd, E (&kr)[KPL], uint32_t (&kp)[POS ? KPL : 1],
-                          uint32_t& kn) -> uint32_t {
+    // Issues the loads of an item's keys into kr / kp (wave w takes the keys [n w / 8, n (w + 1) / 8)
+    // of the region, 64 consecutive ones per register: coalesced, all in flight, nobody waits for
+    // them here).  Lanes past the share (and an item over capacity, whose keys the fallback counts)
+    // load entry 0 of the region, which exists.
+    auto issue_keys = [&](const Desc& d, E (&kr)[KPL], uint32_t (&kp)[POS ? KPL : 1], uint32_t& kn) {
+        const uint32_t n = keys_of(d);
+        const uint32_t m = n <= (uint32_t)C ? n : 0u;
+        const uint32_t ea = m * (uint32_t)wave / kNW, eb = m * (uint32_t)(wave + 1) / kNW;
+        const uint64_t base = (uint64_t)d.idx * C;
         kn = 0u;
-        const uint32_t ns = nseg(d);
-        if (ns > 64u) return 0u;   // uniform
-        const uint32_t in = (uint32_t)lane < ns ? 1u : 0u;
-        const uint32_t lo = in ? bd.lo : 0u, len = in ? bd.hi - bd.lo : 0u;
-        const uint32_t incl = scan64(len);
-        const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63), excl = incl - len;
-        const uint64_t sb = (uint64_t)(d.c.s0 + (uint32_t)lane) * kCaps + lo - excl;   // segment base - its start
-        const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
-        const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
-        const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
-        if (n <= (uint32_t)C && ea < eb) {
 #pragma unroll
-            for (int u = 0; u < KPL; ++u) {
-                const uint32_t e0 = ea + 64u * (uint32_t)u;
-                const uint32_t e = e0 + (uint32_t)lane;
-                kn += e < eb ? 1u : 0u;
-                // lanes past the share read a valid entry (lane 0's, or entry ea)
-                const uint32_t e1 = e0 < eb ? e0 : ea;
-                const uint32_t es = e < eb ? e : e1;
-                // the 64 entries [e0, e0 + 63] lie in segments s0 .. s1 (wave-uniform, almost
-                // always one or two): each lane takes the last of them whose start is <= its
-                // entry, with the segments' starts and bases read by v_readlane (no LDS-pipe
-                // shuffles: ds_bpermute would compete with the item's LDS atomics)
-                const uint32_t el = e0 < eb ? min(e0 + 63u, eb - 1u) : ea;
-                const int s0 = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
-                const int s1 = __popcll(__ballot((uint32_t)lane < ns && excl <= el)) - 1;
-                uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)sb_lo, s0);
-                uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)sb_hi, s0);
-                for (int sx = s0 + 1; sx <= s1; ++sx) {
-                    const uint32_t xs = (uint32_t)__builtin_amdgcn_readlane((int)excl, sx);
-                    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)sb_lo, sx);
-                    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)sb_hi, sx);
-                    blo = es >= xs ? l : blo;
-                    bhi = es >= xs ? h : bhi;
-                }
-                const uint64_t base = ((uint64_t)bhi << 32) | blo;
-                kr[u] = split[base + es];
-                if constexpr (POS) kp[u] = opos[base + es];
-            }
+        for (int u = 0; u < KPL; ++u) {
+            const uint32_t e = ea + 64u * (uint32_t)u + (uint32_t)lane;
+            kn += e < eb ? 1u : 0u;
+            const uint64_t ix = base + (e < eb ? e : 0u);
+            kr[u] = split[ix];
+            if constexpr (POS) kp[u] = opos[ix];
         }
-        return n;
     };
 
-    // f(key, position, true) for every key of a multi-group item (and f(x, p, false) for idle lanes) (a bucket of more than 64 split
-    // items: organisms of >= ~0.8 G windows), read from memory: per group of 64 split items
-    // every wave reads the segment bounds (lane j: split item g + j), scans their lengths and
-    // takes an equal share of the group's entries, U loads of 64 entries in flight.  Returns
-    // the item's key count.
-    auto walk = [&](const Desc& d, auto&& f) -> uint32_t {
-        uint32_t ntot = 0u;
-        for (uint32_t g = d.c.s0; g < d.c.s1; g += 64u) {
-            const uint32_t ns = min(64u, d.c.s1 - g);
-            const uint32_t j = g + (uint32_t)lane;
-            uint32_t lo = 0u, len = 0u;
-            if ((uint32_t)lane < ns) {
-                lo = toff2[(uint64_t)j * kT2 + d.c.p];
-                len = (uint32_t)toff2[(uint64_t)j * kT2 + d.c.p + 1] - lo;
-            }
-            const uint32_t incl = scan64(len);
-            const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63), excl = incl - len;
-            ntot += n;
-            const uint64_t sb = (uint64_t)j * kCaps + lo - excl;
-            const uint32_t sb_lo = (uint32_t)sb, sb_hi = (uint32_t)(sb >> 32);
-            const uint32_t ea = (uint32_t)((uint64_t)n * (uint32_t)wave / kNW);
-            const uint32_t eb = (uint32_t)((uint64_t)n * (uint32_t)(wave + 1) / kNW);
-            for (uint32_t c = ea; c < eb; c += 64u * U) {
-                E r[U];
-                uint32_t rp[U];
-                bool ok[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t e0 = c + 64u * (uint32_t)u;
-                    const uint32_t e = e0 + (uint32_t)lane;
-                    ok[u] = e < eb;
-                    const uint32_t e1 = e0 < eb ? e0 : c;
-                    const uint32_t es = ok[u] ? e : e1;
-                    int sj = __popcll(__ballot((uint32_t)lane < ns && excl <= e1)) - 1;
-                    for (;;) {
-                        const uint32_t nx = __shfl(excl, sj < 63 ? sj + 1 : 63);
-                        const bool adv = sj + 1 < (int)ns && nx <= es;
-                        if (!__ballot(adv)) break;
-                        sj += adv ? 1 : 0;
-                    }
-                    const uint64_t base = ((uint64_t)(uint32_t)__shfl((int)sb_hi, sj) << 32) |
-                                          (uint32_t)__shfl((int)sb_lo, sj);
-                    r[u] = split[base + es];
-                    rp[u] = POS ? opos[base + es] : 0u;
-                }
-                // every lane consumes every load (f is branch-free: ok selects a dummy), so no
-                // load of the walk is left in flight on any path
-#pragma unroll
-                for (int u = 0; u < U; ++u) f(r[u], rp[u], ok[u]);
-            }
-        }
-        return ntot;
-    };
-
-    // the histogram of an item: from the registers (single group) or walked from memory
+    // the histogram of an item, from the registers
     const uint32_t kDummy = (uint32_t)kBins + (uint32_t)(lane & 31);
     E kr[KPL];
     uint32_t kp[POS ? KPL : 1];
     uint32_t kn = 0u;   // valid keys of this lane (a prefix of kr)
-    auto count_keys = [&](const Desc& d, uint32_t n_single) -> uint32_t {
-        if (nseg(d) <= 64u) {   // uniform
+    auto count_keys = [&](const Desc& d) {
 #pragma unroll
-            for (int u = 0; u < KPL; ++u) atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], d.c.np) : kDummy], 1u);
-            return n_single;
-        }
-        return walk(d, [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ok ? bin_of(r, d.c.np) : kDummy], 1u); });
+        for (int u = 0; u < KPL; ++u) atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], d.c.np) : kDummy], 1u);
     };
 
     // makes the wave wait for the loads into kr / kp on every path (the compiler waits before
@@ -1158,8 +1146,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
     };
 
-    // prologue: descriptors of the first three items, bounds of the first two, keys and
-    // histogram of the first
+    // prologue: descriptors of the first three items, keys and histogram of the first
     Desc cur = load_desc(item);
     uint32_t nitem = item + nwx;
     bool has_n = nitem < xb;
@@ -1167,13 +1154,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t nnitem = nitem + nwx;
     bool has_nn = has_n && nnitem < xb;
     Desc nn = load_desc(has_nn ? nnitem : item);
-    Bnd bc = load_bounds(cur);
-    Bnd bn = load_bounds(nxt);
-    uint32_t ntot = issue_keys(cur, bc, kr, kp, kn);
+    issue_keys(cur, kr, kp, kn);
     lds_barrier();   // cleared state visible
-    ntot = count_keys(cur, ntot);
+    count_keys(cur);
     landed_keys();
-    asm volatile("" ::"v"(bn.lo), "v"(bn.hi));
     lds_barrier();
 #ifdef KMH_EXPERIMENTS
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = clock64();
@@ -1183,9 +1167,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     // after a barrier, or wave totals), so all threads meet the same barriers.
     for (;;) {
         const uint32_t np = cur.c.np;
+        const uint32_t ntot = keys_of(cur);
         const uint64_t obo = out_off[cur.c.g];  // (scalar; lands by the first barrier)
         const bool over = ntot > (uint32_t)C;   // more keys than the staging holds: fallback
-        // 1. exclusive scan: thread t owns bins 16t .. 16t + 15; bins of more than kBig keys are
+        // 1. exclusive scan: thread t owns bins 16t .. 16t + 15; bins of more than BIG keys are
         //    listed; bin b's counter becomes start | start << 16.  2. scatter: the returning add
         //    of 1 << 16 hands each key its slot, so hist[b] ends as start | end << 16 (one read
         //    gives a bin's range; starts and ends <= C < 2^16)
@@ -1203,7 +1188,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (lane == 63) wtot[wave] = incl;
 #pragma unroll
             for (int i = 0; i < BPT; ++i) {
-                if (v[i] > (uint32_t)kBig) {
+                if (v[i] > (uint32_t)BIG) {
                     const uint32_t at = atomicAdd(&nbig, 1u);
                     if (at < (uint32_t)kMaxBig) bigl[at] = (uint32_t)(BPT * tid + i);
                 }
@@ -1225,37 +1210,25 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
             lds_barrier();
             KMH_PT(0)
-            if (nseg(cur) <= 64u) {
-                // all the returning adds first, then the stores (a store right behind its add
-                // waited for each add in turn)
-                uint32_t slot[KPL];
+            // all the returning adds first, then the stores (a store right behind its add waited
+            // for each add in turn)
+            uint32_t slot[KPL];
 #pragma unroll
-                for (int u = 0; u < KPL; ++u)
-                    slot[u] = atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], np) : kDummy], 0x10000u);
+            for (int u = 0; u < KPL; ++u)
+                slot[u] = atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], np) : kDummy], 0x10000u);
 #pragma unroll
-                for (int u = 0; u < KPL; ++u) {
-                    const uint32_t at = (uint32_t)u < kn ? slot[u] >> 16 : (uint32_t)C + (uint32_t)lane;
-                    sorted[at] = kr[u];
-                    if constexpr (POS) spos[at] = kp[u];
-                }
-            } else {
-                walk(cur, [&](E r, uint32_t p, bool ok) {
-                    const uint32_t slot = atomicAdd(&hist[ok ? bin_of(r, np) : kDummy], 0x10000u) >> 16;
-                    const uint32_t at = ok ? slot : (uint32_t)C + (uint32_t)lane;
-                    sorted[at] = r;
-                    if constexpr (POS) spos[at] = p;
-                });
+            for (int u = 0; u < KPL; ++u) {
+                const uint32_t at = (uint32_t)u < kn ? slot[u] >> 16 : (uint32_t)C + (uint32_t)lane;
+                sorted[at] = kr[u];
+                if constexpr (POS) spos[at] = kp[u];
             }
             lds_barrier();
         }
         KMH_PT(1)
 
         // 3. this item's keys are dead: the next item's keys load behind this item's emission,
-        //    the bounds of the one after behind the next item, the descriptor after that behind
-        //    two items
-        uint32_t ntot_n = 0u;
-        if (has_n) ntot_n = issue_keys(nxt, bn, kr, kp, kn);
-        const Bnd bnn = load_bounds(nn);
+        //    the descriptor after that behind two items
+        if (has_n) issue_keys(nxt, kr, kp, kn);
         const uint32_t nnnitem = nnitem + nwx;
         const bool has_nnn = has_nn && nnnitem < xb;
         const Desc nnn = load_desc(has_nnn ? nnnitem : item);
@@ -1300,27 +1273,99 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             lds_barrier();
         }
 
-        // 5. emission flags, position-parallel: the key at sorted position i (i = j * NT + tid,
-        //    so a wave reads 64 consecutive keys) is emitted if no earlier key of its bin equals
-        //    it, with the number of equal keys of the bin as its count (bins hold about one key:
-        //    the loops run zero or one times); keys of big bins are emitted from the hash table
-        uint32_t fm = 0u;   // bit j: position j * NT + tid is emitted
+        // 5. emission
+        uint32_t fm = 0u;   // POS: bit j: position j * NT + tid is emitted
         uint32_t ecw[ECW];
         uint32_t ef[POS ? KPL : 1];   // first position of the key (POS): the minimum over its bin's copies
 #pragma unroll
         for (int q = 0; q < ECW; ++q) ecw[q] = 0u;
-        uint32_t wmine = 0u;   // the wave's emitted keys
-        if (!over) {
+        uint32_t wmine = 0u;   // POS: the wave's emitted keys
+        if constexpr (!POS) {
+            if (!over) {
+                // this thread's positions P0 .. P0 + KPL - 1 and the 4 on each side: w[j] = position
+                // P0 - 4 + j (thread 0's head and the last threads' tail read real but unrelated
+                // entries; the positions they could mislead are resolved by range below)
+                const uint32_t P0 = (uint32_t)(KPL * tid);
+                const uint4* s4 = reinterpret_cast<const uint4*>(sorted);
+                E w[NW];
+                {
+                    const uint32_t hq = tid ? (P0 - 4u) / EPC : 0u;
+#pragma unroll
+                    for (int q = 0; q < 4 / EPC; ++q) {
+                        const uint4 c = s4[hq + q];
+#pragma unroll
+                        for (int i = 0; i < EPC; ++i) w[EPC * q + i] = lane_of<E>(c, i);
+                    }
+#pragma unroll
+                    for (int q = 0; q < KPL / EPC + 4 / EPC; ++q) {
+                        const uint4 c = s4[P0 / EPC + q];
+#pragma unroll
+                        for (int i = 0; i < EPC; ++i) w[4 + EPC * q + i] = lane_of<E>(c, i);
+                    }
+                }
+                uint32_t bn[NW];
+#pragma unroll
+                for (int j = 0; j < NW; ++j) bn[j] = bin_of(w[j], np);
+                // valid positions u < rem; positions within 4 of either end of the item are resolved
+                // by range (their neighbours outside [0, ntot) hold unrelated entries)
+                const int rem = (int)ntot - (int)P0;
+                uint32_t valid = rem >= KPL ? (KPL == 32 ? 0xFFFFFFFFu : (1u << KPL) - 1u)
+                                            : (rem > 0 ? (1u << rem) - 1u : 0u);
+                uint32_t slow = tid == 0 ? 0xFu : 0u;
+                if (rem < KPL + 4) slow |= valid & ~(rem > 4 ? (1u << (rem - 4)) - 1u : 0u);
+                uint64_t nv = 0ull;   // 4 bits per position
+#pragma unroll
+                for (int u = 0; u < KPL; ++u) {
+                    const E k = w[u + 4];
+                    const uint32_t bk = bn[u + 4];
+                    const bool dup = (w[u + 3] == k) | (w[u + 2] == k) | (w[u + 1] == k);
+                    const uint32_t c = 1u + (uint32_t)(w[u + 5] == k) + (uint32_t)(w[u + 6] == k) +
+                                       (uint32_t)(w[u + 7] == k);
+                    slow |= (uint32_t)((bn[u] == bk) | (bn[u + 8] == bk)) << u;
+                    nv |= (uint64_t)(dup ? 0u : c) << (4 * u);
+                }
+                slow &= valid;
+                // positions whose bin reaches past +-3 (bins of 5+ keys), or near the item's ends:
+                // the bin's exact range [bs, be) from hist (start | end << 16)
+                while (slow) {
+                    const uint32_t u = (uint32_t)__builtin_ctz(slow);
+                    slow &= slow - 1u;
+                    const uint32_t i = P0 + u;
+                    const E k = sorted[i];
+                    const uint32_t hb = hist[bin_of(k, np)], bs = hb & 0xFFFFu, be = hb >> 16;
+                    uint32_t c = 0u;
+                    if (be - bs <= (uint32_t)BIG) {   // (bigger bins: emitted from the hash table)
+                        bool first = true;
+                        c = 1u;
+                        for (uint32_t y = bs; y < be; ++y) {
+                            const bool eq = y != i && sorted[y] == k;
+                            first = first && !(eq && y < i);
+                            c += (uint32_t)(eq && y > i);
+                        }
+                        c = first ? c : 0u;
+                    }
+                    nv = (nv & ~(0xFull << (4u * u))) | ((uint64_t)c << (4u * u));
+                }
+                // nibbles of invalid positions are 0 (dup / c of unrelated entries cleared)
+                uint64_t vm = 0ull;
+#pragma unroll
+                for (int u = 0; u < KPL; ++u) vm |= (uint64_t)((valid >> u) & 1u) * (0xFull << (4 * u));
+                nv &= vm;
+                if constexpr (KPL == 16) reinterpret_cast<uint2*>(nib)[tid] = make_uint2((uint32_t)nv, (uint32_t)(nv >> 32));
+                else nib[tid] = (uint32_t)nv;
+                // the storing wave of these positions: position P0 + u is stored by lane
+                // (P0 + u) % NT, i.e. wave (P0 % NT) / 64 for every u (KPL divides 64)
+                uint32_t e = 0u;
+#pragma unroll
+                for (int u = 0; u < KPL; ++u) e += (uint32_t)(((nv >> (4 * u)) & 0xFull) != 0ull);
+                if (e) atomicAdd(&scnt[(P0 % (uint32_t)NT) / 64u], e);
+            }
+        } else if (!over) {
             // In phases over a group of HB positions, so that every phase's LDS reads are
-            // independent and issue back to back (position by position, each read waited for the
-            // one before: ~100 serial LDS round trips per item): (a) the keys, (b) their bins'
-            // ranges, (c) four rounds of one read per position -- the bin's key t, at an address
-            // clamped into the bin (most bins hold 1-3 keys), (d) bins of 5..kBig keys, rare, one
-            // by one.  Count of position jj (1 + equal keys after it): byte jj % 4 of ecw[jj / 4];
-            // first: bit jj of fm.  Groups of 4 positions (their 4 rounds' 16 reads in flight
-            // together) and sched_barriers between groups keep one group's values in registers
-            // (8-position groups, or all 16 positions hoisted together, spilled the next item's
-            // keys in flight).
+            // independent and issue back to back: (a) the keys, (b) their bins' ranges, (c) four
+            // rounds of one read per position -- the bin's key t, at an address clamped into the
+            // bin (most bins hold 1-3 keys), (d) bins of 5..kBig keys, rare, one by one.  Count of
+            // position jj (1 + equal keys after it): byte jj % 4 of ecw[jj / 4]; first: bit jj of fm.
             constexpr int HB = KPL < 4 ? KPL : 4;
 #pragma unroll
             for (int q = 0; q < ECW; ++q) ecw[q] = 0x01010101u;
@@ -1340,8 +1385,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 for (int x = 0; x < HB; ++x) {
                     const int jj = h0 + x;
                     const uint32_t i = (uint32_t)(jj * NT + tid), bs = rng[x] & 0xFFFFu, be = rng[x] >> 16;
-                    fm |= (uint32_t)(i < ntot && be - bs <= (uint32_t)kBig) << jj;   // (shifts of 0/1:
-                    if constexpr (POS) ef[jj] = spos[i < ntot ? i : 0u];             //  no mask constants)
+                    fm |= (uint32_t)(i < ntot && be - bs <= (uint32_t)kBig) << jj;
+                    ef[jj] = spos[i < ntot ? i : 0u];
                 }
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
@@ -1358,7 +1403,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         const bool eq = y < be && o[x] == key[x];
                         fm &= ~((uint32_t)(eq && y < i) << jj);
                         ecw[jj / 4] += (uint32_t)(eq && y > i) << (8 * (jj % 4));
-                        if constexpr (POS) ef[jj] = (eq && y > i) ? min(ef[jj], spos[y]) : ef[jj];
+                        ef[jj] = (eq && y > i) ? min(ef[jj], spos[y]) : ef[jj];
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -1372,7 +1417,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                             const E o = sorted[y];
                             first = first && !(y < i && o == key[x]);
                             ecw[jj / 4] += (uint32_t)(y > i && o == key[x]) << (8 * (jj % 4));
-                            if constexpr (POS) ef[jj] = (y > i && o == key[x]) ? min(ef[jj], spos[y]) : ef[jj];
+                            ef[jj] = (y > i && o == key[x]) ? min(ef[jj], spos[y]) : ef[jj];
                         }
                         fm &= ~((uint32_t)!first << jj);
                     }
@@ -1380,18 +1425,21 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
 #pragma unroll
             for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
-            if (nb) {
+        }
+        if (!over && nb) {   // the hash table's keys are stored by the wave of their slot
+            uint32_t hk = 0u;
 #pragma unroll
-                for (int q = 0; q < HPT; ++q) wmine += (uint32_t)__popcll(__ballot((htab[q * NT + tid] & CM) != 0ull));
-            }
+            for (int q = 0; q < HPT; ++q) hk += (uint32_t)__popcll(__ballot((htab[q * NT + tid] & CM) != 0ull));
+            if constexpr (POS) wmine += hk;
+            else if (lane == 0 && hk) atomicAdd(&scnt[wave], hk);
         }
         KMH_PT(3)
-        if (lane == 0) wtot[wave] = wmine;
+        if (POS && lane == 0) wtot[wave] = wmine;
         lds_barrier();   // (also: every read of hist, and of htab for the totals, is done)
         uint32_t before = 0u, used = 0u;
 #pragma unroll
         for (int w = 0; w < kNW; ++w) {
-            const uint32_t xw = wtot[w];
+            const uint32_t xw = POS ? wtot[w] : scnt[w];
             before += w < wave ? xw : 0u;
             used += xw;
         }
@@ -1415,16 +1463,17 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
         zero_bins();
         KMH_PT(4)
-        lds_barrier();   // cleared bins visible; `bad` read by everybody
+        lds_barrier();   // cleared bins visible; `bad` read by everybody; scnt read by everybody
+        if constexpr (!POS)
+            if (tid < kNW) scnt[tid] = 0u;   // (the next item's emission adds after two more barriers)
 
         // 6. the next item's histogram (the wait for its keys), before this item's stores
-        if (has_n) ntot_n = count_keys(nxt, ntot_n);
+        if (has_n) count_keys(nxt);
         // Everything loaded so far has landed here, on every path: the next item's keys (counted
-        // above, but only by the lanes that hold keys) and the bounds after them.  A load still
-        // in flight at the stores below would be waited for behind them later (one in-order
-        // counter: vmcnt(0) at a register copy or at the scatter).
+        // above, but only by the lanes that hold keys).  A load still in flight at the stores
+        // below would be waited for behind them later (one in-order counter: vmcnt(0) at a
+        // register copy or at the scatter).
         landed_keys();
-        asm volatile("" ::"v"(bnn.lo), "v"(bnn.hi));
         if (tid == 0) {
             obase = ob + obo;
             nbig = bad = 0u;
@@ -1444,25 +1493,38 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             for (int j0 = 0; j0 < KPL; j0 += SB) {
                 __builtin_amdgcn_sched_barrier(0);
                 E sk[SB];
+                uint32_t nc[SB];   // !POS: the position's nibble (0: not emitted, else its count)
 #pragma unroll
-                for (int x = 0; x < SB; ++x) sk[x] = sorted[(j0 + x) * NT + tid];
+                for (int x = 0; x < SB; ++x) {
+                    const uint32_t i = (uint32_t)((j0 + x) * NT + tid);
+                    sk[x] = sorted[i];
+                    if constexpr (!POS) nc[x] = (nib[i >> 3] >> (4u * (i & 7u))) & 0xFu;
+                }
 #pragma unroll
                 for (int x = 0; x < SB; ++x) {
                     const int jj = j0 + x;
-                    const bool f = (fm >> jj) & 1u;
+                    bool f;
+                    uint32_t cv;
+                    if constexpr (POS) {
+                        f = (fm >> jj) & 1u;
+                        cv = (ecw[jj / 4] >> (8 * (jj % 4))) & 0xFFu;
+                    } else {
+                        f = nc[x] != 0u;
+                        cv = nc[x];
+                    }
                     const uint64_t m = __ballot(f);
                     if (f) {
                         const uint64_t o = at + run + (uint32_t)__popcll(m & below);
 #if defined(KMH_EXPERIMENTS) && KMH_SP_OUT_EXP == 1
                         // what-if: a compact row (u32 residue + u8 count), same positions
                         out_store(reinterpret_cast<uint32_t*>(codes) + o, (uint32_t)sk[x]);
-                        out_store(reinterpret_cast<uint8_t*>(counts) + o, (uint8_t)(ecw[jj / 4] >> (8 * (jj % 4))));
+                        out_store(reinterpret_cast<uint8_t*>(counts) + o, (uint8_t)cv);
 #elif defined(KMH_EXPERIMENTS) && KMH_SP_OUT_EXP == 2
                         // what-if: no output bytes at all (counts wrong; timing only)
-                        if (sk[x] == (E)0x5A5A5A5Au && o == 0ull) codes[0] = hib;
+                        if (sk[x] == (E)0x5A5A5A5Au && o == 0ull) codes[0] = hib + cv;
 #else
                         out_store(codes + o, hib | (uint64_t)sk[x]);
-                        out_store(counts + o, (ecw[jj / 4] >> (8 * (jj % 4))) & 0xFFu);
+                        out_store(counts + o, cv);
 #endif
                         if constexpr (POS) firsts[o] = ef[jj];
                     }
@@ -1497,11 +1559,9 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         if (!has_n) break;
         item = nitem;
         cur = nxt;
-        ntot = ntot_n;
         nitem = nnitem;
         has_n = has_nn;
         nxt = nn;
-        bn = bnn;
         nnitem = nnnitem;
         has_nn = has_nnn;
         nn = nnn;
@@ -1513,12 +1573,13 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #endif
 }
 
-// Fallback, step 1: the residues of bucket b, pass p of genome g (and their positions), in
-// any order.
+// Fallback, step 1: the residues of bucket b of genome g whose pass is set in the bitmap
+// `pmask` (np bits) -- every failed pass of the bucket at once -- and their positions, in any
+// order.
 template <typename E, bool POS>
 __global__ __launch_bounds__(256) void k_sp_gather(const E* __restrict__ ent, const uint32_t* __restrict__ epos,
                                                    const uint16_t* __restrict__ toff, uint32_t ldt,
-                                                   uint64_t ta, uint64_t tb, uint32_t b, uint32_t p,
+                                                   uint64_t ta, uint64_t tb, uint32_t b, const uint32_t* __restrict__ pmask,
                                                    uint32_t np, int R, E* __restrict__ out,
                                                    uint32_t* __restrict__ opos, uint32_t* __restrict__ n) {
     const uint64_t t = ta + (uint64_t)blockIdx.x;
@@ -1527,7 +1588,8 @@ __global__ __launch_bounds__(256) void k_sp_gather(const E* __restrict__ ent, co
     for (uint32_t j = lo + threadIdx.x; j < hi; j += 256) {
         const uint64_t ix = t * (uint64_t)Sp<E, POS>::TILE + j;
         const E r = ent[ix];
-        if (pass_of(r, np, R) == p) {
+        const uint32_t p = pass_of(r, np, R);
+        if ((pmask[p >> 5] >> (p & 31u)) & 1u) {
             const uint32_t at = atomicAdd(n, 1u);
             out[at] = r;
             opos[at] = POS ? epos[ix] : at;   // without positions: any value (the sort needs one)
@@ -1602,16 +1664,18 @@ void launch_partition_k(int k, int canonical, unsigned tiles, unsigned grid, hip
 #undef KMH_PK
 }
 
-// Fallback for pass p of bucket b of genome g: gather, sort (radix_sort_pairs: with positions,
+// Fallback for the failed passes `passes` of bucket b of genome g (n entries in the bucket):
+// one gather of all of them (passes hold disjoint keys), sort (radix_sort_pairs: with positions,
 // first by position and then stably by key, so a run's first entry holds its first position),
 // runs, append.  Hand-written kernels throughout (kmh_sort.hip).
 template <typename E, bool POS>
-int fallback_pass(Ctx* ctx, uint32_t g, uint32_t b, uint32_t p, uint32_t np, uint32_t n,
-                  const E* ent, const uint32_t* epos, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
-                  int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
-                  uint32_t* firsts, hipStream_t s) {
+int fallback_passes(Ctx* ctx, uint32_t g, uint32_t b, const std::vector<uint32_t>& passes, uint32_t np, uint32_t n,
+                    const E* ent, const uint32_t* epos, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
+                    int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
+                    uint32_t* firsts, hipStream_t s) {
     const size_t ne = ((size_t)n * sizeof(E) + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
-    int rc = ensure(ctx, ctx->sparse[5], 2 * ne + 7 * n4 + 1024);
+    const size_t mb = ((size_t)(np + 31) / 32 * 4 + 255) & ~(size_t)255;
+    int rc = ensure(ctx, ctx->sparse[5], 2 * ne + 7 * n4 + mb + 1024);
     if (rc) return rc;
     char* p8 = static_cast<char*>(ctx->sparse[5].ptr);
     E* ka = static_cast<E*>(carve(p8, ne));
@@ -1624,10 +1688,14 @@ int fallback_pass(Ctx* ctx, uint32_t g, uint32_t b, uint32_t p, uint32_t np, uin
     uint32_t* ex = static_cast<uint32_t*>(carve(p8, n4));
     uint32_t* starts = static_cast<uint32_t*>(carve(p8, n4));
     uint32_t* small = static_cast<uint32_t*>(carve(p8, 256));
+    uint32_t* d_mask = static_cast<uint32_t*>(carve(p8, mb));
+    std::vector<uint32_t> mask((np + 31) / 32, 0u);
+    for (uint32_t p : passes) mask[p >> 5] |= 1u << (p & 31u);
     KMH_HIP(ctx, hipMemsetAsync(small, 0, 256, s));
+    KMH_HIP(ctx, hipMemcpyAsync(d_mask, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, s));
     if (tb > ta) {
         hipLaunchKernelGGL((k_sp_gather<E, POS>), dim3((unsigned)(tb - ta)), dim3(256), 0, s, ent, epos, toff, ldt,
-                           ta, tb, b, p, np, R, ka, pa, small);
+                           ta, tb, b, d_mask, np, R, ka, pa, small);
         KMH_HIP(ctx, hipGetLastError());
     }
     uint32_t m = 0;
@@ -1788,15 +1856,18 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const size_t nsi = totals[0], nci = totals[1];
         if (nci == 0) continue;
         const double h2 = hprof ? now_ms() : 0.0;
-        // split output (+ positions) + toff2 (ctx->sparse[6]); items, out_off, failed list (ctx->sparse[1])
-        const size_t sbytes = nsi * (size_t)kCaps * sizeof(E);
-        const size_t pbytes = POS ? nsi * (size_t)kCaps * 4 : 0;
-        const size_t t2bytes = (nsi * kT2 * 2 + 255) & ~(size_t)255;
-        rc = ensure(ctx, ctx->sparse[6], sbytes + pbytes + t2bytes);
+        // count-item regions (+ positions) and their fill counters (ctx->sparse[6]); items, out_off,
+        // failed list (ctx->sparse[1])
+        constexpr int C = Cnt<E, POS>::CAP;
+        const size_t sbytes = nci * (size_t)C * sizeof(E);
+        const size_t pbytes = POS ? nci * (size_t)C * 4 : 0;
+        const size_t fillb = (nci * 4 + 255) & ~(size_t)255;
+        rc = ensure(ctx, ctx->sparse[6], sbytes + pbytes + fillb);
         if (rc) return rc;
         E* d_split = static_cast<E*>(ctx->sparse[6].ptr);
         uint32_t* d_spos = POS ? reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes) : nullptr;
-        uint16_t* d_toff2 = reinterpret_cast<uint16_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes + pbytes);
+        uint32_t* d_pfill = reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->sparse[6].ptr) + sbytes + pbytes);
+        KMH_HIP(ctx, hipMemsetAsync(d_pfill, 0, nci * 4, s));
         const size_t sib = (nsi * sizeof(SplitItem) + 255) & ~(size_t)255;
         const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
@@ -1818,7 +1889,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const long sg = env_long("KMH_SP_SPLIT_GRID", std::max(1, ctx->num_cu));
         const unsigned sgrid = (unsigned)std::min<uint64_t>(nsi, sg > 0 ? (uint64_t)sg : nsi);
         hipLaunchKernelGGL((k_sp_split<E, POS>), dim3(sgrid), dim3(kSpThreads), 0, s, ent, epos, toff, ldt,
-                           d_sitems, (uint32_t)nsi, R, d_split, d_spos, d_toff2, d_gbfail);
+                           d_sitems, (uint32_t)nsi, R, d_split, d_spos, d_pfill, d_gbfail);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 #ifdef KMH_EXPERIMENTS
@@ -1837,7 +1908,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
 #endif
         time_begin(ctx, s, "k_sp_count");
         const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
-        hipLaunchKernelGGL((k_sp_count<E, POS>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_toff2,
+        hipLaunchKernelGGL((k_sp_count<E, POS>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_pfill,
                            d_citems, (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts, d_firsts,
                            reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed);
         time_end(ctx, s);
@@ -1887,12 +1958,23 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
                 if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
         }
         const double h4 = hprof ? now_ms() : 0.0;
-        for (uint32_t id : ids) {
-            const CountItem& it = citems[id];
-            rc = fallback_pass<E, POS>(ctx, it.g, it.b, it.p, it.np, it.n, ent, epos, toff, ldt,
-                                       L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
-                                       reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts, s);
+        // the failed passes grouped by (genome, bucket): one gather + sort per bucket, however many
+        // of its passes failed (a skewed organism's largest buckets can fail every pass)
+        std::sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t c) {
+            return citems[a].gb != citems[c].gb ? citems[a].gb < citems[c].gb : citems[a].p < citems[c].p;
+        });
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        std::vector<uint32_t> passes;
+        for (size_t i = 0; i < ids.size();) {
+            const CountItem& it = citems[ids[i]];
+            passes.clear();
+            size_t j = i;
+            for (; j < ids.size() && citems[ids[j]].gb == it.gb; ++j) passes.push_back(citems[ids[j]].p);
+            rc = fallback_passes<E, POS>(ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt,
+                                         L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
+                                         reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts, s);
             if (rc) return rc;
+            i = j;
         }
         if (hprof)
             std::fprintf(stderr, "sparse batch host phases (ms): partition+sizes wait %.2f, items %.2f (%zu split, "
