@@ -697,6 +697,37 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         KMH_ST(2)
         lds_barrier();
         KMH_ST(3)
+        // Region offsets of this item's passes, reserved as soon as the pass counts exist (the
+        // returning atomics are in flight during the scan and the scatter; read by readlane in
+        // the stores): lane j of wave w reserves pass w + 16 (64 r + j)'s run in that count item's
+        // region.  An item whose entries overflow the staging (total > kCaps, its bucket goes to
+        // the fallback) reserves too; its count items are skipped, so nothing reads the regions.
+        constexpr int kRR = (kMaxPasses + 64 * kNW - 1) / (64 * kNW);
+        uint32_t aoff[kRR];
+#pragma unroll
+        for (int r = 0; r < kRR; ++r) {
+            aoff[r] = 0u;
+            const uint32_t p = (uint32_t)wave + (uint32_t)kNW * (64u * (uint32_t)r + (uint32_t)lane);
+            if (p < np) {
+                uint32_t c = 0u;
+                if (rep) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const uint4 h = hist4[8u * p + (uint32_t)q];
+                        c += h.x + h.y + h.z + h.w;
+                    }
+                } else {
+                    c = hist[p];
+                }
+#if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 2
+                // what-if: no returning atomic to wait for (every split item writes its run at the
+                // region's start: counts wrong; timing only)
+                if (c) atomicAdd(&pfill[cur.cbase + p], c);
+#else
+                if (c) aoff[r] = atomicAdd(&pfill[cur.cbase + p], c);
+#endif
+            }
+        }
         // exclusive scan of the counters (pass-major): thread t owns counters 4t .. 4t + 3 (pass p's
         // 32 replicas are counters 32p .. 32p + 31, i.e. threads 8p .. 8p + 7; without replicas
         // counter p); counters past the item's passes are zero
@@ -735,26 +766,6 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         KMH_ST(4)
         const uint32_t total = total_sh;
         const bool fits = total <= (uint32_t)kCaps;   // uniform
-        // Region offsets of this item's passes: lane j of wave w reserves pass w + 16 (64 r + j)'s
-        // run in that count item's region (one returning atomic per pass, in flight during the
-        // scatter; read by readlane in the stores)
-        constexpr int kRR = (kMaxPasses + 64 * kNW - 1) / (64 * kNW);
-        uint32_t aoff[kRR];
-#pragma unroll
-        for (int r = 0; r < kRR; ++r) {
-            aoff[r] = 0u;
-            const uint32_t p = (uint32_t)wave + (uint32_t)kNW * (64u * (uint32_t)r + (uint32_t)lane);
-            if (fits && p < np) {
-                const uint32_t c = pst[p + 1] - pst[p];
-#if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 2
-                // what-if: no returning atomic to wait for (every split item writes its run at the
-                // region's start: counts wrong; timing only)
-                if (c) atomicAdd(&pfill[cur.cbase + p], c);
-#else
-                if (c) aoff[r] = atomicAdd(&pfill[cur.cbase + p], c);
-#endif
-            }
-        }
         if (fits) {
             auto scatter = [&](E r, uint32_t p, bool ok) {
                 const uint32_t slot = atomicAdd(&hist[ctr(r, ok)], 1u);
@@ -1331,16 +1342,33 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const uint32_t u = (uint32_t)__builtin_ctz(slow);
                     slow &= slow - 1u;
                     const uint32_t i = P0 + u;
-                    const E k = sorted[i];
-                    const uint32_t hb = hist[bin_of(k, np)], bs = hb & 0xFFFFu, be = hb >> 16;
+                    E k = w[4];
+                    uint32_t bk = bn[4];
+#pragma unroll
+                    for (int q = 1; q < KPL; ++q) {   // (a select chain, not a dynamic register index)
+                        k = u == (uint32_t)q ? w[q + 4] : k;
+                        bk = u == (uint32_t)q ? bn[q + 4] : bk;
+                    }
+                    const uint32_t hb = hist[bk], bs = hb & 0xFFFFu, be = hb >> 16;
                     uint32_t c = 0u;
                     if (be - bs <= (uint32_t)BIG) {   // (bigger bins: emitted from the hash table)
+                        // the bin's keys, four reads in flight at a time (addresses clamped into the bin)
                         bool first = true;
                         c = 1u;
-                        for (uint32_t y = bs; y < be; ++y) {
-                            const bool eq = y != i && sorted[y] == k;
-                            first = first && !(eq && y < i);
-                            c += (uint32_t)(eq && y > i);
+                        for (uint32_t y0 = bs; y0 < be; y0 += 4u) {
+                            E o[4];
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                const uint32_t y = y0 + (uint32_t)t;
+                                o[t] = sorted[y < be ? y : bs];
+                            }
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                const uint32_t y = y0 + (uint32_t)t;
+                                const bool eq = y < be && y != i && o[t] == k;
+                                first = first && !(eq && y < i);
+                                c += (uint32_t)(eq && y > i);
+                            }
                         }
                         c = first ? c : 0u;
                     }
@@ -1919,8 +1947,8 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             KMH_HIP(ctx, hipStreamSynchronize(s));
             KMH_HIP(ctx, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sp_prof), sizeof(h)));
             const double w = (double)h[8] * kNW;   // waves
-            std::fprintf(stderr, "k_sp_count per wave over %zu items on %u WGs: scan %.0f | scatter %.0f | issue next %.0f | "
-                         "big+emission %.0f | totals+clear %.0f | next hist %.0f | stores %.0f | - %.0f Mcyc\n", nci, (unsigned)h[8],
+            std::fprintf(stderr, "k_sp_count per wave over %zu items on %u WGs: scan %.2f | scatter %.2f | issue next %.2f | "
+                         "big+emission %.2f | totals+clear %.2f | next hist %.2f | stores %.2f | - %.2f Mcyc\n", nci, (unsigned)h[8],
                          h[0] / w / 1e6, h[1] / w / 1e6, h[2] / w / 1e6, h[3] / w / 1e6, h[4] / w / 1e6,
                          h[5] / w / 1e6, h[6] / w / 1e6, h[7] / w / 1e6);
             const unsigned long long z[16] = {};

@@ -434,3 +434,170 @@ def count_genome_split(genome_file, k, device=None, group=None, count_fn=None):
         return host.to(row.device)
     dist.all_reduce(row, op=dist.ReduceOp.SUM, group=group)
     return row
+
+
+# ---------------------------------------------------------------- sparse matrix, column-sharded
+class ShardedSparseMatrix:
+    """One rank's column shard of the organisms x k-mers count matrix for sparse k (config 5).
+
+    The reference's matrix (features.py:85-117, ``_build_matrix``) has one column per label in
+    the sorted union of every organism's labels and a 0 wherever an organism lacks one.  At
+    k = 21 that union is ~10^10 columns over a 128-genome batch, so no rank holds it: rank q owns
+    the codes [lo_code, hi_code) (contiguous code ranges chosen to balance the entries) and holds
+    every organism's counts of those codes in CSR form:
+
+      columns  uint64 [ncols]   the sorted union of the organisms' codes in the range
+      indptr   int64  [G + 1]   organism g's entries are indptr[g] .. indptr[g + 1]
+      indices  int64  [nnz]     column index of each entry (ascending within an organism)
+      values   uint32 [nnz]     its count
+
+    Codes are 2-bit A0 C1 G2 T3, first base most significant, so code order is the string order
+    of the k-mers; for k >= 20 that is the reference's column order (its labels stay the exact
+    k-mer text, statistics.py:253-273 and the features2 fixtures), for k <= 19 the reference
+    sorts the integer-parsed labels instead (to_frame reproduces it).
+    """
+
+    def __init__(self, k, G, lo_code, hi_code, columns, indptr, indices, values, rank=0, world=1):
+        self.k, self.G = int(k), int(G)
+        self.lo_code, self.hi_code = int(lo_code), int(hi_code)
+        self.columns, self.indptr, self.indices, self.values = columns, indptr, indices, values
+        self.rank, self.world = rank, world
+
+    @property
+    def nnz(self):
+        return int(self.values.size)
+
+    def dense(self):
+        """The shard as a dense [G, ncols] int64 array (small shards only)."""
+        out = np.zeros((self.G, self.columns.size), np.int64)
+        rows = np.repeat(np.arange(self.G), np.diff(self.indptr))
+        out[rows, self.indices] = self.values
+        return out
+
+    @staticmethod
+    def labels(codes, k):
+        """The reference's column label of each code: the k-mer's letters; for k <= 19 with the
+        leading A's stripped ("A" for A...A), the integer round trip of its k{k}.txt digits
+        (statistics.py:157, 248-273)."""
+        out = []
+        for c in np.asarray(codes, dtype=np.uint64).tolist():
+            s = "".join("ACGT"[(c >> (2 * (k - 1 - i))) & 3] for i in range(k))
+            out.append((s.lstrip("A") or "A") if k <= 19 else s)
+        return out
+
+    @staticmethod
+    def to_frame(shards, organisms):
+        """Every rank's shard (in rank order, e.g. from torch.distributed.all_gather_object) as
+        the reference's DataFrame: organisms x sorted(labels), missing = 0 (small matrices:
+        tests and inspection; the distributed matrix itself never materialises densely)."""
+        import pandas as pd
+
+        k = shards[0].k
+        cols = np.concatenate([s.columns for s in shards]) if shards else np.zeros(0, np.uint64)
+        vals = np.concatenate([s.dense() for s in shards], axis=1) if shards else np.zeros((0, 0), np.int64)
+        labels = ShardedSparseMatrix.labels(cols, k)
+        order = sorted(range(len(labels)), key=labels.__getitem__)   # features.py:101
+        return pd.DataFrame(vals[:, order], index=list(organisms), columns=[labels[i] for i in order])
+
+
+def _code_splitters(rows, k, world, group):
+    """world - 1 code boundaries that cut every rank's entries into ~equal shares: a global
+    histogram of the codes' top 16 bits (all-reduced), cut at equal cumulative counts."""
+    import torch
+    import torch.distributed as dist
+
+    bits = 2 * k
+    sh = max(bits - 16, 0)
+    nb = 1 << min(bits, 16)
+    hist = np.zeros(nb, np.int64)
+    for codes, _ in rows:
+        if codes.size:
+            hist += np.bincount((codes >> np.uint64(sh)).astype(np.int64), minlength=nb)
+    t = torch.from_numpy(hist)
+    if dist.get_backend(group) != "gloo":
+        t = t.cuda()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    cum = np.cumsum(t.cpu().numpy())
+    total = int(cum[-1]) if cum.size else 0
+    bounds = [0]
+    for q in range(1, world):
+        b = int(np.searchsorted(cum, total * q / world, side="left")) + 1 if total else (nb * q) // world
+        bounds.append(max(bounds[-1], min(b, nb)) << sh)
+    bounds.append(1 << bits)
+    return bounds
+
+
+def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows_fn=None):
+    """The organisms x k-mers count matrix for sparse k, column-sharded across the ranks of a
+    torch.distributed group: every rank counts its block of genomes
+    (sparse_rows: rows sorted by code), the code space is cut into W ranges of ~equal entries,
+    and one all-to-all-v (RCCL over xGMI, or gloo) sends each rank the slices of every row that
+    fall in its range -- contiguous slices of sorted rows, no scatter.  Returns this rank's
+    ShardedSparseMatrix; its columns are the sorted union of the organisms' codes in its range,
+    i.e. its share of features.py:96-111's sorted(union of labels).  Without a process group one
+    shard holds the whole matrix.  rows_fn(files) -> [(codes uint64 ascending, counts), ...]
+    replaces the GPU counter (CPU tests)."""
+    import torch
+    import torch.distributed as dist
+
+    files = list(genome_files)
+    G = len(files)
+    if rows_fn is None:
+        lo, rows = sparse_rows(files, k, canonical=canonical, device=device, group=group)
+    else:
+        world0 = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        rank0 = dist.get_rank(group) if world0 > 1 else 0
+        lo, hi = shard_bounds(G, world0, rank0)
+        rows = rows_fn(files[lo:hi])
+    rows = [(np.ascontiguousarray(c, dtype=np.uint64), np.ascontiguousarray(n, dtype=np.uint32)) for c, n in rows]
+    if not (dist.is_available() and dist.is_initialized()):
+        return _assemble_shard(k, G, 0, 1 << (2 * k), [(lo + i, c, n) for i, (c, n) in enumerate(rows)], 0, 1)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    bounds = _code_splitters(rows, k, world, group)
+    # per destination: for each of my genomes, the slice of its sorted row in that range
+    cuts = [np.searchsorted(c, np.array(bounds, dtype=np.uint64), side="left") for c, _ in rows]
+    send_len = np.array([[int(cut[q + 1] - cut[q]) for cut in cuts] for q in range(world)], np.int64)
+    # every rank learns every (source, destination, genome) length: the layout of what it receives
+    lens = [None] * world
+    dist.all_gather_object(lens, send_len, group=group)
+    gpu = dist.get_backend(group) != "gloo"
+    codes_out = np.concatenate([rows[i][0][cuts[i][q]:cuts[i][q + 1]] for q in range(world) for i in range(len(rows))]
+                               + [np.zeros(0, np.uint64)])
+    counts_out = np.concatenate([rows[i][1][cuts[i][q]:cuts[i][q + 1]] for q in range(world) for i in range(len(rows))]
+                                + [np.zeros(0, np.uint32)])
+    in_splits = [int(send_len[q].sum()) for q in range(world)]
+    out_splits = [int(lens[src][rank].sum()) for src in range(world)]
+
+    def a2a(arr, dtype):
+        t_in = torch.from_numpy(arr.view(dtype))
+        t_out = torch.empty(sum(out_splits), dtype=t_in.dtype)
+        if gpu:
+            t_in, t_out = t_in.cuda(), t_out.cuda()
+        dist.all_to_all_single(t_out, t_in, out_splits, in_splits, group=group)
+        return t_out.cpu().numpy()
+
+    rc = a2a(codes_out, np.int64).view(np.uint64)
+    rn = a2a(counts_out, np.int32).view(np.uint32)
+    # received: source rank by source rank, each source's genomes in order
+    parts, pos = [], 0
+    for src in range(world):
+        glo, _ = shard_bounds(G, world, src)
+        for j, n in enumerate(lens[src][rank].tolist()):
+            parts.append((glo + j, rc[pos:pos + n], rn[pos:pos + n]))
+            pos += n
+    return _assemble_shard(k, G, bounds[rank], bounds[rank + 1], parts, rank, world)
+
+
+def _assemble_shard(k, G, lo_code, hi_code, parts, rank, world):
+    """CSR of one column shard from (genome, sorted codes, counts) pieces."""
+    per = [None] * G
+    for g, c, n in parts:
+        per[g] = (c, n)
+    per = [p if p is not None else (np.zeros(0, np.uint64), np.zeros(0, np.uint32)) for p in per]
+    allc = np.concatenate([c for c, _ in per]) if per else np.zeros(0, np.uint64)
+    columns = np.unique(allc)
+    indptr = np.zeros(G + 1, np.int64)
+    np.cumsum([c.size for c, _ in per], out=indptr[1:])
+    indices = np.searchsorted(columns, allc).astype(np.int64)
+    values = np.concatenate([n for _, n in per]) if per else np.zeros(0, np.uint32)
+    return ShardedSparseMatrix(k, G, lo_code, hi_code, columns, indptr, indices, values, rank, world)

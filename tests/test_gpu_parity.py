@@ -1152,3 +1152,35 @@ def test_dropin_workspace_trim_and_staging(ctx, oracle_lib, monkeypatch):
     # the staging is gone with the workspace: counting it again must fail loudly, not read freed memory
     with pytest.raises(ValueError):
         c.count_staged(21)
+
+
+@pytest.mark.parametrize("backend,nproc", [("nccl", 1), ("gloo", 2)])
+def test_sparse_matrix_sharded_on_gpu(tmp_path, oracle_lib, backend, nproc):
+    """kmerml.kmers.matrix.sparse_matrix on the GPU path: genomes counted by
+    the batched hash-table pipeline at k = 21 canonical, column shards assembled by all-to-all-v
+    (RCCL with one rank; gloo with two ranks sharing cuda:0).  The shards side by side must equal
+    the organisms x k-mers matrix of the oracle's counts (features.py:85-117's layout: sorted union
+    of k-mers, missing = 0)."""
+    files, rows = [], []
+    for i in range(3):
+        p = tmp_path / f"g{i}.fa"
+        seq = osynth.synth_bases(120_000 + 9_000 * i, osynth.genome_seed(60 + i)).tobytes()
+        if i == 2:
+            seq = seq + seq[:30_000]   # k-mers counted twice
+        osynth.write_fasta(p, [(f"SYN_{i}", seq)])
+        files.append(str(p))
+        c, n, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), 21, canonical=True)
+        rows.append((c, n))
+    here = os.path.dirname(os.path.abspath(__file__))
+    extra = ["--single-device"] if nproc > 1 else []
+    r = _torchrun([os.path.join(here, "sparse_matrix_probe.py"), str(tmp_path), "21", backend] + extra + files,
+                  nproc=nproc, timeout=300)
+    assert r.returncode == 0, _failure(r)
+    cols = np.load(tmp_path / "columns.npy")
+    vals = np.load(tmp_path / "values.npy")
+    want_cols = np.unique(np.concatenate([c for c, _ in rows]))
+    assert np.array_equal(cols, want_cols)
+    want = np.zeros((3, want_cols.size), np.int64)
+    for g, (c, n) in enumerate(rows):
+        want[g, np.searchsorted(want_cols, c)] = n
+    assert np.array_equal(vals, want) and vals.max() >= 2

@@ -128,3 +128,84 @@ def test_split_bounds_count_every_window_once():
                         else:
                             assert s + k > n
                 assert np.all(seen == 1)
+
+
+def _sparse_rows_oracle(files, k):
+    """Forward-strand sparse rows of each FASTA file from the C oracle (sorted by code)."""
+    from oracle import corac
+    from oracle import fasta as ofasta
+    rows = []
+    for f in files:
+        recs = [s for _, _, s in ofasta.parse_fasta(f) if len(s) >= k]
+        packed = "".join(s.upper() + "\n" for s in recs).encode()
+        c, n, _ = corac.count_sparse(np.frombuffer(packed, np.uint8), k, canonical=False)
+        rows.append((c, n))
+    return rows
+
+
+def _sparse_worker(rank, world, port, files, orgs, k, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "kmer-ml_amd"), os.path.dirname(here)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = kmatrix.sparse_matrix(files, k, canonical=False, rows_fn=lambda fs: _sparse_rows_oracle(fs, k))
+        shards = [None] * world
+        dist.all_gather_object(shards, m)
+        assert [s.rank for s in shards] == list(range(world))
+        assert all(shards[q].hi_code == shards[q + 1].lo_code for q in range(world - 1))
+        if rank == 0:
+            df = kmatrix.ShardedSparseMatrix.to_frame(shards, orgs)
+            df.to_csv(os.path.join(outdir, f"sharded_k{k}.csv"))
+            with open(os.path.join(outdir, f"nnz_k{k}.txt"), "w") as f:
+                f.write(" ".join(str(s.nnz) for s in shards))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k", [13, 21])
+def test_sparse_matrix_column_sharded_gloo(tmp_path, oracle_lib, k):
+    """Config 5's matrix: each of 2 ranks counts its block of genomes, the code
+    space is cut into 2 ranges of ~equal entries and one all-to-all-v (gloo here, RCCL on the
+    GPUs) gives each rank every organism's counts in its range.  The shards, put side by side,
+    equal the reference's matrix built from the per-organism files: k{k}.txt (the restated
+    generate.py writer) -> KmerFeatureExtractor CSVs -> KmerFeatureBuilder.build_from_statistics_
+    files (features.py:28-117: sorted union of labels, missing = 0; k = 13 has the integer-parsed,
+    A-stripped labels, k = 21 the exact k-mer text)."""
+    import contextlib
+    import io
+    from oracle import kmers as okmers
+    from oracle import synth as osynth
+    from kmerml.kmers.statistics import KmerFeatureExtractor
+    from kmerml.ml.features import KmerFeatureBuilder
+    from kmerml.utils.path_utils import find_files
+    kroot, fdir = tmp_path / "kmers", tmp_path / "features"
+    files, orgs = [], []
+    for i in range(3):
+        org = f"GCF_00000{i}"
+        seq = osynth.synth_bases(2500 + 700 * i, osynth.genome_seed(30 + i)).tobytes().decode()
+        if i == 1:   # shared stretch (counts > 1 across and within organisms), lowercase, N run
+            seq = seq[:600] + seq[:600].lower() + "NNNNN" + seq[600:]
+        if i == 2:
+            seq = seq + "ACGTTGCA" * 40
+        fa = tmp_path / f"{org}.fa"
+        osynth.write_fasta(fa, [(org, seq.encode()), ("short", b"ACGTA")])
+        files.append(str(fa))
+        orgs.append(org)
+        table = okmers.count_records([(org, seq), ("short", "ACGTA")], [k])[k]
+        (kroot / org).mkdir(parents=True)
+        (kroot / org / f"k{k}.txt").write_text(okmers.kmer_text(table))
+    with contextlib.redirect_stdout(io.StringIO()):
+        kf = find_files(str(kroot), patterns=["k*.txt"], recursive=True)
+        KmerFeatureExtractor(input_paths=kf, output_dir=str(fdir)).extract_features()
+        want = KmerFeatureBuilder(str(fdir)).build_from_statistics_files()
+    mp.spawn(_sparse_worker, args=(2, _free_port(), files, orgs, k, str(tmp_path)), nprocs=2, join=True)
+    got = (tmp_path / f"sharded_k{k}.csv").read_text()
+    assert list(want.index) == orgs
+    assert got == want.to_csv()
+    nnz = [int(x) for x in (tmp_path / f"nnz_k{k}.txt").read_text().split()]
+    assert min(nnz) > 0.3 * sum(nnz)   # the code ranges balance the entries
