@@ -77,6 +77,11 @@ uint64_t kmh_ctx_workspace_bytes(const kmh_ctx* ctx);
  * /root/reference/kmerml/kmers/generate.py:116-126 (extract_from_genome_list) does not keep a
  * config-5-sized workspace (tens of GB) between genomes. */
 int kmh_ctx_trim(kmh_ctx* ctx, uint64_t keep_bytes);
+/* Counters of the context since its creation, into stats[0 .. n): [0] sparse passes recounted by
+ * the exact sort fallback, [1] the (genome, bucket) groups they were recounted in (one gather +
+ * radix sort per group, however many of the bucket's passes failed), [2] workspace bytes.
+ * Returns the number of counters the library keeps (3). */
+int kmh_ctx_stats(const kmh_ctx* ctx, uint64_t* stats, int n);
 
 /* Last error message of `ctx`, or of the calling thread's context-free calls when
  * ctx == NULL.  Never NULL; "" when there was no error. */

@@ -198,6 +198,13 @@ int kmh_ctx_release(kmh_ctx* ctx) {
 
 uint64_t kmh_ctx_workspace_bytes(const kmh_ctx* ctx) { return ctx ? workspace_bytes(ctx) : 0; }
 
+int kmh_ctx_stats(const kmh_ctx* ctx, uint64_t* stats, int n) {
+    if (!ctx || (n > 0 && !stats)) return KMH_ERR_INVALID;
+    const uint64_t v[3] = {ctx->fb_passes, ctx->fb_groups, workspace_bytes(ctx)};
+    for (int i = 0; i < n && i < 3; ++i) stats[i] = v[i];
+    return 3;
+}
+
 int kmh_ctx_trim(kmh_ctx* ctx, uint64_t keep_bytes) {
     if (!ctx) {
         kmh::set_thread_error("kmh_ctx_trim: ctx is NULL");

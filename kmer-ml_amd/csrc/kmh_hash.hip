@@ -991,6 +991,24 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // probing and no per-lane tail) every distinct key is resolved by comparing the few keys of its
 // bin.  A bin of more than BIG keys (a repeated k-mer) goes through a small LDS hash table
 // instead, so repeats cost what they cost the hash kernel before.
+// A value every lane loads from the same address, as a VECTOR load (its address laundered through
+// a VGPR).  A scalar load (s_load) counts in lgkmcnt like the LDS operations, and the compiler
+// waits for it with lgkmcnt(0) at the next LDS wait (scalar loads return out of order): every
+// descriptor prefetched with s_load stalled the following LDS phase for a memory round trip.  A
+// vector load counts in vmcnt and is read (readfirstlane) where the wave waits for its vector loads
+// anyway.
+template <typename T>
+__device__ __forceinline__ T vload(const T* p) {
+    uint64_t a = reinterpret_cast<uint64_t>(p);
+    asm volatile("" : "+v"(a));
+    using gT = __attribute__((address_space(1))) const T;
+    return *reinterpret_cast<gT*>(a);
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
+
 constexpr int kBinBits = 13, kBins = 1 << kBinBits;
 constexpr int kBig = 32;         // positions: keys of a bin resolved by comparison (byte counts)
 constexpr int kBigN = 14;        // no positions: the same, counts kept as nibbles
@@ -1101,19 +1119,32 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 
     // An item as loaded: its descriptor, the gb_fail flag of its bucket (a pass of a bucket whose
     // split overflowed is left to the fallback: it counts as an item without keys) and its key
-    // count (the fill counter the split items appended to).  Used two items after it was loaded,
-    // so the scalar loads have landed.
+    // count (the fill counter the split items appended to).  In the loop, the descriptor of the
+    // item three ahead and the flag and count of the item two ahead are VECTOR loads issued behind
+    // the next item's keys and read (readfirstlane) after those keys have landed (vload).
     struct Desc {
         CountItem c;
         uint32_t skip, n, idx;
     };
-    auto load_desc = [&](uint32_t i) {
+    auto load_desc = [&](uint32_t i) {   // (prologue only: scalar loads)
         Desc d;
         d.c = items[i];
         d.skip = gb_fail[d.c.gb];
         d.n = pfill[i];
         d.idx = i;
         return d;
+    };
+    static_assert(sizeof(CountItem) == 24, "descriptor as three 8-byte loads");
+    struct RawItem {
+        uint64_t a, b, c;
+    };
+    auto vload_item = [&](uint32_t i) {
+        const uint64_t* p = reinterpret_cast<const uint64_t*>(items + i);
+        return RawItem{vload(p), vload(p + 1), vload(p + 2)};
+    };
+    auto item_of = [&](const RawItem& r) {
+        return CountItem{rfl((uint32_t)r.a), rfl((uint32_t)(r.a >> 32)), rfl((uint32_t)r.b),
+                         rfl((uint32_t)(r.b >> 32)), rfl((uint32_t)r.c), rfl((uint32_t)(r.c >> 32))};
     };
     auto keys_of = [&](const Desc& d) -> uint32_t { return d.skip ? 0u : d.n; };
 
@@ -1157,7 +1188,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         }
     };
 
-    // prologue: descriptors of the first three items, keys and histogram of the first
+    // prologue: descriptors of the first three items and the output base of the first, keys and
+    // histogram of the first
     Desc cur = load_desc(item);
     uint32_t nitem = item + nwx;
     bool has_n = nitem < xb;
@@ -1165,6 +1197,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t nnitem = nitem + nwx;
     bool has_nn = has_n && nnitem < xb;
     Desc nn = load_desc(has_nn ? nnitem : item);
+    uint64_t obo = out_off[cur.c.g];
     issue_keys(cur, kr, kp, kn);
     lds_barrier();   // cleared state visible
     count_keys(cur);
@@ -1179,7 +1212,6 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     for (;;) {
         const uint32_t np = cur.c.np;
         const uint32_t ntot = keys_of(cur);
-        const uint64_t obo = out_off[cur.c.g];  // (scalar; lands by the first barrier)
         const bool over = ntot > (uint32_t)C;   // more keys than the staging holds: fallback
         // 1. exclusive scan: thread t owns bins 16t .. 16t + 15; bins of more than BIG keys are
         //    listed; bin b's counter becomes start | start << 16.  2. scatter: the returning add
@@ -1242,7 +1274,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         if (has_n) issue_keys(nxt, kr, kp, kn);
         const uint32_t nnnitem = nnitem + nwx;
         const bool has_nnn = has_nn && nnnitem < xb;
-        const Desc nnn = load_desc(has_nnn ? nnnitem : item);
+
         KMH_PT(2)
 
         // 4. big bins: their keys into the hash table (linear probing, CAS(empty -> key|1), +1
@@ -1472,6 +1504,12 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             used += xw;
         }
         const bool fail_item = over || bad != 0u || used > cap;   // uniform
+        // (vector loads, read at step 6 once the next item's keys have landed; issued here, after
+        // the emission, so that they hold no registers through it): the descriptor three items
+        // ahead, the flag and count of the item two ahead, the output offset of the next item
+        const RawItem raw_nnn = vload_item(has_nnn ? nnnitem : item);
+        const uint32_t v_skip = vload(gb_fail + nn.c.gb), v_n = vload(pfill + nn.idx);
+        const uint64_t v_obo = vload(out_off + nxt.c.g);
         // the output base: one atomic per item, returning during the next item's histogram
         // (its value is first used there: an add here would wait for it)
         unsigned long long ob = 0ull;
@@ -1506,6 +1544,13 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             obase = ob + obo;
             nbig = bad = 0u;
         }
+        Desc nnn;
+        nnn.c = item_of(raw_nnn);
+        nnn.idx = has_nnn ? nnnitem : item;
+        nnn.skip = nnn.n = 0u;   // (loaded one iteration from now, when it is nn)
+        nn.skip = rfl(v_skip);
+        nn.n = rfl(v_n);
+        const uint64_t obo_n = rfl64(v_obo);
         KMH_PT(5)
         lds_barrier();
 
@@ -1593,6 +1638,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         nnitem = nnnitem;
         has_nn = has_nnn;
         nn = nnn;
+        obo = obo_n;
     }
 #ifdef KMH_EXPERIMENTS
     if (lane == 0)
@@ -1998,6 +2044,8 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             passes.clear();
             size_t j = i;
             for (; j < ids.size() && citems[ids[j]].gb == it.gb; ++j) passes.push_back(citems[ids[j]].p);
+            ctx->fb_passes += passes.size();
+            ctx->fb_groups += 1;
             rc = fallback_passes<E, POS>(ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt,
                                          L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
                                          reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts, s);

@@ -43,6 +43,9 @@ struct Ctx {
     // kmh_stage_host: bytes of the host sequence staged in `seq` (valid while staged_ok)
     uint64_t staged_n = 0;
     bool staged_ok = false;
+    // kmh_ctx_stats: sparse passes recounted by the exact fallback, and the (genome, bucket)
+    // groups they were recounted in (one gather + sort each), since the context was created
+    uint64_t fb_passes = 0, fb_groups = 0;
     // pinned staging for small host->device tables
     void* pinned = nullptr;
     size_t pinned_bytes = 0;

@@ -37,6 +37,7 @@ SIGNATURES = [
     ("kmh_ctx_release", _c.c_int, [_vp]),
     ("kmh_ctx_workspace_bytes", _u64, [_vp]),
     ("kmh_ctx_trim", _c.c_int, [_vp, _u64]),
+    ("kmh_ctx_stats", _c.c_int, [_vp, _vp, _c.c_int]),
     ("kmh_last_error", _c.c_char_p, [_vp]),
     ("kmh_timing_enable", _c.c_int, [_vp, _c.c_int]),
     ("kmh_timing_report", _c.c_int, [_vp, _c.POINTER(_c.c_char_p), _u64p,
@@ -182,6 +183,13 @@ class Context:
     def workspace_bytes(self):
         """Device workspace + pinned staging the context holds now (kmh_ctx_workspace_bytes)."""
         return int(lib().kmh_ctx_workspace_bytes(self._h)) if self._h else 0
+
+    @_locked
+    def stats(self):
+        """kmh_ctx_stats: {"fallback_passes", "fallback_groups", "workspace_bytes"}."""
+        out = np.zeros(3, np.uint64)
+        _check(lib().kmh_ctx_stats(self._h, _ptr(out), 3), self._h)
+        return {"fallback_passes": int(out[0]), "fallback_groups": int(out[1]), "workspace_bytes": int(out[2])}
 
     @_locked
     def trim(self, keep_bytes):

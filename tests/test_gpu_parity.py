@@ -1184,3 +1184,26 @@ def test_sparse_matrix_sharded_on_gpu(tmp_path, oracle_lib, backend, nproc):
     for g, (c, n) in enumerate(rows):
         want[g, np.searchsorted(want_cols, c)] = n
     assert np.array_equal(vals, want) and vals.max() >= 2
+
+
+def test_sparse_skewed_bucket_fallback_grouped(ctx, oracle_lib, monkeypatch):
+    """a skewed organism whose largest bucket fails many passes must not run
+    one gather + sort per failed pass.  A 1.5 Mbp A-rich stretch (90 % A) puts most of its windows
+    in bucket 0 (first five bases AAAAA) -- ~600 passes at the drop-in's k = 22 pass target -- and
+    KMH_SP_LIMIT = 64 fails every count item, so every pass goes to the exact fallback.  Failed
+    passes are recounted per (genome, bucket): at most one group per bucket, far fewer than the
+    passes, and the first-occurrence result equals the oracle's counts and first positions."""
+    rng = np.random.default_rng(23)
+    rich = np.where(rng.random(1_500_000) < 0.9, ord("A"), np.frombuffer(b"CGT", np.uint8)[rng.integers(0, 3, 1_500_000)])
+    seq = np.concatenate([osynth.synth_bases(2_000_000, osynth.genome_seed(81)), rich.astype(np.uint8)])
+    monkeypatch.setenv("KMH_SP_LIMIT", "64")
+    before = ctx.stats()
+    codes, counts, first = ctx.count(seq, 22)
+    after = ctx.stats()
+    passes = after["fallback_passes"] - before["fallback_passes"]
+    groups = after["fallback_groups"] - before["fallback_groups"]
+    assert 0 < groups <= 1024 and passes >= 400 + groups, (passes, groups)
+    wc, wn, wf = oracle_lib.count_sparse(seq, 22, canonical=False)
+    o = np.argsort(codes, kind="stable")
+    assert np.array_equal(codes[o], wc) and np.array_equal(counts[o], wn) and np.array_equal(first[o], wf)
+    assert np.all(np.diff(first.astype(np.int64)) > 0)
