@@ -74,6 +74,9 @@ def parse():
                    help="one process on one GPU doing what ONE rank of N does per step at config 4 "
                         "(count G/N genomes, encode u4, and the all-gather's writes modelled as N "
                         "device copies of the slot; no xGMI): a projection, labelled as such")
+    p.add_argument("--sim-copy", choices=("torch", "none"), default="torch",
+                   help="--simulate-ranks: model the all-gather's writes by device copies (torch), or "
+                        "leave them out (none: isolates the copies' contention with the count)")
     p.add_argument("--cpu-sample", type=int, default=8_000_000,
                    help="bases of genome 0 timed with the reference-algorithm CPU loop (0 = skip)")
     p.add_argument("--kernel-events", choices=["roofline", "all"], default="roofline",
@@ -428,7 +431,7 @@ def main():
             if sim:   # the gather's HBM side: every slot of recv written from this rank's slot
                 side.wait_stream(stream)
                 with torch.cuda.stream(side):
-                    for q in range(span):
+                    for q in range(span if a.sim_copy == "torch" else 0):
                         recv[b][q * P:(q + 1) * P].copy_(sb)
                     ev = torch.cuda.Event()
                     ev.record(side)
@@ -681,6 +684,7 @@ def main():
                                          f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k}, u4 encode, the all-gather "
                                          f"modelled as {sim} device copies of its slot; no xGMI traffic, no other ranks)")
             out["simulated_ranks"] = sim
+            out["simulated_copies"] = a.sim_copy
             out["projected_value_at_n"] = G * L / (elapsed / a.steps)
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)

@@ -1009,8 +1009,25 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
     return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
 }
 
+// k_sp_count's `sorted` / `spos` and `hist` are stored with their 16-byte slots XOR-swizzled:
+// slot c lives at c ^ ((c >> 4) & 3).  A ds_read_b128 is serviced in lane groups of 16 (e.g.
+// lanes 0-3, 12-15, 20-27) whose lane numbers are distinct mod 16; a thread reading slot 4t + q
+// (its consecutive keys or bins, t = its thread) then hits 16 distinct slots of a 256-byte bank
+// row instead of 4 (a 4-way conflict unswizzled).  An aligned run of 16 slots is permuted within
+// itself, so lane-consecutive reads keep one bank per lane.  EPS = elements per slot.
+#ifndef KMH_SWZ
+#define KMH_SWZ 3
+#endif
+__device__ __forceinline__ uint32_t swz_slot(uint32_t c) { return (KMH_SWZ & 2) ? c ^ ((c >> 4) & 3u) : c; }
+template <int EPS>
+__device__ __forceinline__ uint32_t swz(uint32_t a) {
+    return (KMH_SWZ & 2) ? a ^ ((((a / (uint32_t)EPS) >> 4) & 3u) * (uint32_t)EPS) : a;
+}
+__device__ __forceinline__ uint32_t swzh_slot(uint32_t c) { return (KMH_SWZ & 1) ? c ^ ((c >> 4) & 3u) : c; }
+__device__ __forceinline__ uint32_t swzh(uint32_t a) { return (KMH_SWZ & 1) ? a ^ (((a >> 6) & 3u) << 2) : a; }
+
 constexpr int kBinBits = 13, kBins = 1 << kBinBits;
-constexpr int kBig = 32;         // positions: keys of a bin resolved by comparison (byte counts)
+constexpr int kBig = 32;        // positions: keys of a bin resolved by comparison (byte counts)
 constexpr int kBigN = 14;        // no positions: the same, counts kept as nibbles
 constexpr int kHSlots = 1024;    // hash table of the big bins
 constexpr int kMaxBig = 256;     // big bins of one item (more: the item goes to the fallback)
@@ -1098,7 +1115,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint4* h4 = reinterpret_cast<uint4*>(hist);
     auto zero_bins = [&] {
 #pragma unroll
-        for (int q = 0; q < BQ; ++q) h4[BQ * tid + q] = make_uint4(0u, 0u, 0u, 0u);
+        for (int q = 0; q < BQ; ++q) h4[q * NT + tid] = make_uint4(0u, 0u, 0u, 0u);
     };
     zero_bins();
 #pragma unroll
@@ -1175,7 +1192,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t kn = 0u;   // valid keys of this lane (a prefix of kr)
     auto count_keys = [&](const Desc& d) {
 #pragma unroll
-        for (int u = 0; u < KPL; ++u) atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], d.c.np) : kDummy], 1u);
+        for (int u = 0; u < KPL; ++u) atomicAdd(&hist[swzh((uint32_t)u < kn ? bin_of(kr[u], d.c.np) : kDummy)], 1u);
     };
 
     // makes the wave wait for the loads into kr / kp on every path (the compiler waits before
@@ -1221,7 +1238,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             uint32_t v[BPT];
 #pragma unroll
             for (int q = 0; q < BQ; ++q) {
-                const uint4 a = h4[BQ * tid + q];
+                const uint4 a = h4[swzh_slot(BQ * tid + q)];
                 v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
             }
             uint32_t tsum = 0u;
@@ -1248,7 +1265,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 }
 #pragma unroll
                 for (int q = 0; q < BQ; ++q)
-                    h4[BQ * tid + q] = make_uint4(o[4 * q] * 0x10001u, o[4 * q + 1] * 0x10001u, o[4 * q + 2] * 0x10001u,
+                    h4[swzh_slot(BQ * tid + q)] = make_uint4(o[4 * q] * 0x10001u, o[4 * q + 1] * 0x10001u, o[4 * q + 2] * 0x10001u,
                                                   o[4 * q + 3] * 0x10001u);
             }
             lds_barrier();
@@ -1258,10 +1275,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             uint32_t slot[KPL];
 #pragma unroll
             for (int u = 0; u < KPL; ++u)
-                slot[u] = atomicAdd(&hist[(uint32_t)u < kn ? bin_of(kr[u], np) : kDummy], 0x10000u);
+                slot[u] = atomicAdd(&hist[swzh((uint32_t)u < kn ? bin_of(kr[u], np) : kDummy)], 0x10000u);
 #pragma unroll
             for (int u = 0; u < KPL; ++u) {
-                const uint32_t at = (uint32_t)u < kn ? slot[u] >> 16 : (uint32_t)C + (uint32_t)lane;
+                const uint32_t at = swz<EPC>((uint32_t)u < kn ? slot[u] >> 16 : (uint32_t)C + (uint32_t)lane);
                 sorted[at] = kr[u];
                 if constexpr (POS) spos[at] = kp[u];
             }
@@ -1286,9 +1303,9 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             } else {
                 for (uint32_t xb2 = 0; xb2 < nb; ++xb2) {
                     const uint32_t b = bigl[xb2];
-                    const uint32_t hb = hist[b], s = hb & 0xFFFFu, e = hb >> 16;
+                    const uint32_t hb = hist[swzh(b)], s = hb & 0xFFFFu, e = hb >> 16;
                     for (uint32_t i = s + (uint32_t)tid; i < e; i += NT) {
-                        const E key = sorted[i];
+                        const E key = sorted[swz<EPC>(i)];
                         uint32_t h = (uint32_t)key ^ (uint32_t)((uint64_t)key >> 29) * 0x9E3779B1u;
                         h = (uint32_t)__umul24(h ^ (h >> 15), 0x9E3779u) >> (32 - 10);
                         for (uint32_t probe = 0;; ++probe) {
@@ -1299,13 +1316,13 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                             unsigned long long* slot = &htab[h];
                             const unsigned long long old = atomicCAS(slot, 0ull, ((unsigned long long)key << CB) | 1ull);
                             if (old == 0ull) {
-                                if constexpr (POS) atomicMin(&hmin[h], spos[i]);
+                                if constexpr (POS) atomicMin(&hmin[h], spos[swz<EPC>(i)]);
                                 break;
                             }
                             if ((E)(old >> CB) == key) {
                                 const unsigned long long prev = atomicAdd(slot, 1ull);
                                 if (WIDE && (prev & CM) == CM) bad = 1u;   // count field full
-                                if constexpr (POS) atomicMin(&hmin[h], spos[i]);
+                                if constexpr (POS) atomicMin(&hmin[h], spos[swz<EPC>(i)]);
                                 break;
                             }
                             h = (h + 1u) & (uint32_t)(kHSlots - 1);
@@ -1335,13 +1352,13 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const uint32_t hq = tid ? (P0 - 4u) / EPC : 0u;
 #pragma unroll
                     for (int q = 0; q < 4 / EPC; ++q) {
-                        const uint4 c = s4[hq + q];
+                        const uint4 c = s4[swz_slot(hq + q)];
 #pragma unroll
                         for (int i = 0; i < EPC; ++i) w[EPC * q + i] = lane_of<E>(c, i);
                     }
 #pragma unroll
                     for (int q = 0; q < KPL / EPC + 4 / EPC; ++q) {
-                        const uint4 c = s4[P0 / EPC + q];
+                        const uint4 c = s4[swz_slot(P0 / EPC + q)];
 #pragma unroll
                         for (int i = 0; i < EPC; ++i) w[4 + EPC * q + i] = lane_of<E>(c, i);
                     }
@@ -1381,7 +1398,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         k = u == (uint32_t)q ? w[q + 4] : k;
                         bk = u == (uint32_t)q ? bn[q + 4] : bk;
                     }
-                    const uint32_t hb = hist[bk], bs = hb & 0xFFFFu, be = hb >> 16;
+                    const uint32_t hb = hist[swzh(bk)], bs = hb & 0xFFFFu, be = hb >> 16;
                     uint32_t c = 0u;
                     if (be - bs <= (uint32_t)BIG) {   // (bigger bins: emitted from the hash table)
                         // the bin's keys, four reads in flight at a time (addresses clamped into the bin)
@@ -1392,7 +1409,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
                             for (int t = 0; t < 4; ++t) {
                                 const uint32_t y = y0 + (uint32_t)t;
-                                o[t] = sorted[y < be ? y : bs];
+                                o[t] = sorted[swz<EPC>(y < be ? y : bs)];
                             }
 #pragma unroll
                             for (int t = 0; t < 4; ++t) {
@@ -1437,16 +1454,16 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
                 for (int x = 0; x < HB; ++x) {
                     const uint32_t i = (uint32_t)((h0 + x) * NT + tid);
-                    key[x] = sorted[i < ntot ? i : 0u];
+                    key[x] = sorted[swz<EPC>(i < ntot ? i : 0u)];
                 }
 #pragma unroll
-                for (int x = 0; x < HB; ++x) rng[x] = hist[bin_of(key[x], np)];
+                for (int x = 0; x < HB; ++x) rng[x] = hist[swzh(bin_of(key[x], np))];
 #pragma unroll
                 for (int x = 0; x < HB; ++x) {
                     const int jj = h0 + x;
                     const uint32_t i = (uint32_t)(jj * NT + tid), bs = rng[x] & 0xFFFFu, be = rng[x] >> 16;
                     fm |= (uint32_t)(i < ntot && be - bs <= (uint32_t)kBig) << jj;
-                    ef[jj] = spos[i < ntot ? i : 0u];
+                    ef[jj] = spos[swz<EPC>(i < ntot ? i : 0u)];
                 }
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
@@ -1454,7 +1471,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
                     for (int x = 0; x < HB; ++x) {
                         const uint32_t bs = rng[x] & 0xFFFFu, be = rng[x] >> 16, y = bs + (uint32_t)t;
-                        o[x] = sorted[y < be ? y : bs];
+                        o[x] = sorted[swz<EPC>(y < be ? y : bs)];
                     }
 #pragma unroll
                     for (int x = 0; x < HB; ++x) {
@@ -1463,7 +1480,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         const bool eq = y < be && o[x] == key[x];
                         fm &= ~((uint32_t)(eq && y < i) << jj);
                         ecw[jj / 4] += (uint32_t)(eq && y > i) << (8 * (jj % 4));
-                        ef[jj] = (eq && y > i) ? min(ef[jj], spos[y]) : ef[jj];
+                        ef[jj] = (eq && y > i) ? min(ef[jj], spos[swz<EPC>(y)]) : ef[jj];
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -1474,10 +1491,10 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     if (((fm >> jj) & 1u) && be - bs > 4u) {
                         bool first = true;
                         for (uint32_t y = bs + 4u; y < be; ++y) {
-                            const E o = sorted[y];
+                            const E o = sorted[swz<EPC>(y)];
                             first = first && !(y < i && o == key[x]);
                             ecw[jj / 4] += (uint32_t)(y > i && o == key[x]) << (8 * (jj % 4));
-                            ef[jj] = (y > i && o == key[x]) ? min(ef[jj], spos[y]) : ef[jj];
+                            ef[jj] = (y > i && o == key[x]) ? min(ef[jj], spos[swz<EPC>(y)]) : ef[jj];
                         }
                         fm &= ~((uint32_t)!first << jj);
                     }
@@ -1561,6 +1578,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             const uint64_t hib = (uint64_t)cur.c.b << R;
             const uint64_t below = (1ull << lane) - 1ull;
             uint32_t run = 0u;
+            const uint32_t stid = swz<EPC>((uint32_t)tid);
             constexpr int SB = KPL < 8 ? KPL : 8;   // keys re-read 8 at a time (one round trip)
 #pragma unroll
             for (int j0 = 0; j0 < KPL; j0 += SB) {
@@ -1570,7 +1588,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
                 for (int x = 0; x < SB; ++x) {
                     const uint32_t i = (uint32_t)((j0 + x) * NT + tid);
-                    sk[x] = sorted[i];
+                    sk[x] = sorted[(uint32_t)((j0 + x) * NT) + stid];   // (= swz(i): NT is a multiple of 64 slots)
                     if constexpr (!POS) nc[x] = (nib[i >> 3] >> (4u * (i & 7u))) & 0xFu;
                 }
 #pragma unroll
