@@ -48,6 +48,15 @@ constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
+#ifndef KMH_SP_BIN_MUL
+#define KMH_SP_BIN_MUL 0
+#endif
+#ifndef KMH_SP_SPLIT_STB
+#define KMH_SP_SPLIT_STB 1
+#endif
+#ifndef KMH_SP_RESERVE_EARLY
+#define KMH_SP_RESERVE_EARLY 1
+#endif
 #ifndef KMH_SP_QU
 #define KMH_SP_QU 4
 #endif
@@ -375,6 +384,17 @@ struct SplitItem {
     uint32_t pad;
 };
 
+// add + the rank of this lane among the lanes set in ballot m (v_mbcnt_lo / v_mbcnt_hi, which
+// add their second operand)
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m, uint32_t add = 0u) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, add));
+}
+// base + a 32-bit byte offset: with a uniform base the compiler addresses it as SGPR base + VGPR
+// offset (global_* saddr form)
+template <typename T>
+__device__ __forceinline__ T* at_byte(T* base, uint32_t bytes) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + bytes);
+}
 // Positions of entries [4 c, 4 c + 4) (u32 entries) or [2 c, 2 c + 2) (u64) of a tile's layout.
 template <typename E>
 __device__ __forceinline__ PosChunk load_pos(const uint32_t* __restrict__ epos, uint64_t chunk) {
@@ -654,6 +674,62 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // passes (spread over banks by lane) and its scatter store goes to a 64-entry scratch
     // tail of `sorted`, so no exec-mask branch surrounds an atomic.
     const uint32_t rl = (uint32_t)(lane & 31);
+    // pass counter of entry r in an item of np passes (replicated for np <= kRepP)
+    auto ctr = [&](uint32_t np, E r, bool ok) {   // branch-free: the dummy is a select
+        const bool rep = np <= (uint32_t)kRepP;   // uniform
+        const uint32_t c = (pass_of<E>(r, np, R) << (rep ? 5u : 0u)) | (rep ? rl : 0u);
+        return ok ? c : (uint32_t)(kRepP * 32) + rl;
+    };
+    // the pass histogram of an item (its chunks held in h, or walked from memory)
+    auto histogram = [&](const SplitItem& it, const Held<POS>& h) {
+        auto count_pass = [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ctr(it.np, r, ok)], 1u); };
+        if (h.kept) each_held<E, POS>(h, count_pass);   // wave-uniform
+        else walk_bucket<POS>(ent, epos, toff, ldt, it.b, it.t0, it.t1, split_bt(it.per, (uint32_t)EPC), q[wave],
+                              slo[wave], shi[wave], count_pass);
+    };
+    // Region offsets of an item's passes, reserved once its pass counts exist (read by readlane
+    // in its stores): lane j of wave w reserves pass w + 16 (64 r + j)'s run in that count item's
+    // region.  An item whose entries overflow the staging (total > kCaps, its bucket goes to the
+    // fallback) reserves too; its count items are skipped, so nothing reads the regions.  These
+    // returning adds go to memory (device scope) and take microseconds under the kernel's own
+    // traffic, so without positions they are issued one item early: right after the previous
+    // item's scatter, a whole store phase before their results are read.
+    constexpr int kRR = (kMaxPasses + 64 * kNW - 1) / (64 * kNW);
+    auto reserve = [&](const SplitItem& it, uint32_t (&ao)[kRR]) {
+        const bool rep = it.np <= (uint32_t)kRepP;   // uniform
+#pragma unroll
+        for (int r = 0; r < kRR; ++r) {
+            ao[r] = 0u;
+            const uint32_t p = (uint32_t)wave + (uint32_t)kNW * (64u * (uint32_t)r + (uint32_t)lane);
+            if (p < it.np) {
+                uint32_t c = 0u;
+                if (rep) {
+#pragma unroll
+                    for (int qq = 0; qq < 8; ++qq) {
+                        const uint4 hv = hist4[8u * p + (uint32_t)qq];
+                        c += hv.x + hv.y + hv.z + hv.w;
+                    }
+                } else {
+                    c = hist[p];
+                }
+#if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 2
+                // what-if: no returning atomic to wait for (every split item writes its run at the
+                // region's start: counts wrong; timing only)
+                if (c) atomicAdd(&pfill[it.cbase + p], c);
+#else
+                if (c) ao[r] = atomicAdd(&pfill[it.cbase + p], c);
+#endif
+            }
+        }
+    };
+    // (KMH_SP_RESERVE_EARLY=0: the round-4 A/B baseline, reservations after the item's own histogram)
+    constexpr bool kEarly = kPipe && KMH_SP_RESERVE_EARLY;
+    uint32_t aoff[kRR];
+    if constexpr (kEarly) {   // the first item's histogram and reservations
+        histogram(cur, hc);
+        lds_barrier();
+        reserve(cur, aoff);
+    }
 #ifdef KMH_EXPERIMENTS
     unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stl_ = clock64();
 #endif
@@ -682,55 +758,22 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             KMH_ST(1)
         }
 
-        // (C) this item: pass histogram, scan, scatter
+        // (C) this item: pass histogram and reservations (with positions; without, they were
+        //     done one item earlier), scan, scatter
         const uint32_t np = cur.np;
         const bool rep = np <= (uint32_t)kRepP;   // uniform
-        const uint32_t csh = rep ? 5u : 0u, crl = rep ? rl : 0u, cdum = (uint32_t)(kRepP * 32) + rl;
-        auto ctr = [&](E r, bool ok) {   // branch-free: the dummy is a select
-            const uint32_t c = (pass_of<E>(r, np, R) << csh) | crl;
-            return ok ? c : cdum;
-        };
-        auto count_pass = [&](E r, uint32_t, bool ok) { atomicAdd(&hist[ctr(r, ok)], 1u); };
         const uint32_t bt = split_bt(cur.per, (uint32_t)EPC);
-        if (hc.kept) each_held<E, POS>(hc, count_pass);   // wave-uniform
-        else walk_bucket<POS>(ent, epos, toff, ldt, cur.b, cur.t0, cur.t1, bt, q[wave], slo[wave], shi[wave], count_pass);
-        KMH_ST(2)
-        lds_barrier();
-        KMH_ST(3)
-        // Region offsets of this item's passes, reserved as soon as the pass counts exist (the
-        // returning atomics are in flight during the scan and the scatter; read by readlane in
-        // the stores): lane j of wave w reserves pass w + 16 (64 r + j)'s run in that count item's
-        // region.  An item whose entries overflow the staging (total > kCaps, its bucket goes to
-        // the fallback) reserves too; its count items are skipped, so nothing reads the regions.
-        constexpr int kRR = (kMaxPasses + 64 * kNW - 1) / (64 * kNW);
-        uint32_t aoff[kRR];
-#pragma unroll
-        for (int r = 0; r < kRR; ++r) {
-            aoff[r] = 0u;
-            const uint32_t p = (uint32_t)wave + (uint32_t)kNW * (64u * (uint32_t)r + (uint32_t)lane);
-            if (p < np) {
-                uint32_t c = 0u;
-                if (rep) {
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) {
-                        const uint4 h = hist4[8u * p + (uint32_t)q];
-                        c += h.x + h.y + h.z + h.w;
-                    }
-                } else {
-                    c = hist[p];
-                }
-#if defined(KMH_EXPERIMENTS) && KMH_SP_SPLIT_EXP == 2
-                // what-if: no returning atomic to wait for (every split item writes its run at the
-                // region's start: counts wrong; timing only)
-                if (c) atomicAdd(&pfill[cur.cbase + p], c);
-#else
-                if (c) aoff[r] = atomicAdd(&pfill[cur.cbase + p], c);
-#endif
-            }
+        if constexpr (!kEarly) {
+            histogram(cur, hc);
+            KMH_ST(2)
+            lds_barrier();
+            KMH_ST(3)
+            reserve(cur, aoff);
         }
         // exclusive scan of the counters (pass-major): thread t owns counters 4t .. 4t + 3 (pass p's
         // 32 replicas are counters 32p .. 32p + 31, i.e. threads 8p .. 8p + 7; without replicas
-        // counter p); counters past the item's passes are zero
+        // counter p); counters past the item's passes are zero.  (Its barrier also orders the
+        // previous item's reads of pst and of the staging before the writes below.)
         {
             const uint4 cv = hist4[tid];
             const uint32_t sm = cv.x + cv.y + cv.z + cv.w;
@@ -768,7 +811,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         const bool fits = total <= (uint32_t)kCaps;   // uniform
         if (fits) {
             auto scatter = [&](E r, uint32_t p, bool ok) {
-                const uint32_t slot = atomicAdd(&hist[ctr(r, ok)], 1u);
+                const uint32_t slot = atomicAdd(&hist[ctr(np, r, ok)], 1u);
                 const uint32_t at = ok ? slot : (uint32_t)kCaps + (uint32_t)lane;
                 sorted[at] = r;
                 if constexpr (POS) spos[at] = p;
@@ -784,7 +827,20 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         if constexpr (kPipe) landed(hn);
         asm volatile("" ::"v"(lo_nn), "v"(hi_nn));
         KMH_ST(7)
-        hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next item starts after a barrier
+        hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next histogram follows a barrier
+
+        // the next item's histogram and reservations, ahead of this item's stores (see reserve)
+        uint32_t aoff_n[kRR];
+#pragma unroll
+        for (int r = 0; r < kRR; ++r) aoff_n[r] = 0u;
+        if constexpr (kEarly) {
+            if (has_n) {   // uniform
+                lds_barrier();   // zeroed counters visible
+                histogram(nxt, hn);
+                lds_barrier();
+                reserve(nxt, aoff_n);
+            }
+        }
 
         // (D) this item's stores: pass p's run of the staging [pst[p], pst[p + 1]) is appended to
         // count item cbase + p's region at the reserved offset; entries past the region's capacity
@@ -799,7 +855,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                 const uint32_t r = k / 64u;   // (uniform; a select chain, not a dynamic register index)
                 uint32_t av = aoff[0];
 #pragma unroll
-                for (int q = 1; q < kRR; ++q) av = r == (uint32_t)q ? aoff[q] : av;
+                for (int qq = 1; qq < kRR; ++qq) av = r == (uint32_t)qq ? aoff[qq] : av;
                 const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)av, (int)(k % 64u));
                 const uint32_t s0 = pst[p], n = pst[p + 1] - s0;
                 const uint32_t lim = o < (uint32_t)C ? min(n, (uint32_t)C - o) : 0u;
@@ -836,6 +892,30 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                         for (uint32_t i = (uint32_t)lane; i < lim; i += 64u)
                             __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
                 }
+#elif KMH_SP_SPLIT_STB
+                // four staging reads in flight per lane (addresses clamped into the run), then their
+                // stores, each at the pass's uniform base + a 32-bit offset
+                E* const ob = out + d;
+                uint32_t* const pb = POS ? opos + d : nullptr;
+                for (uint32_t i0 = 0; i0 < lim; i0 += 256u) {   // (uniform)
+                    E v[4];
+                    uint32_t vp[POS ? 4 : 1];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t i = i0 + 64u * (uint32_t)t + (uint32_t)lane;
+                        const uint32_t ic = i < lim ? i : lim - 1u;
+                        v[t] = sorted[s0 + ic];
+                        if constexpr (POS) vp[t] = spos[s0 + ic];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t i = i0 + 64u * (uint32_t)t + (uint32_t)lane;
+                        if (i < lim) {
+                            __builtin_nontemporal_store(v[t], at_byte(ob, (uint32_t)sizeof(E) * i));
+                            if constexpr (POS) __builtin_nontemporal_store(vp[t], at_byte(pb, 4u * i));
+                        }
+                    }
+                }
 #else
                 for (uint32_t i = (uint32_t)lane; i < lim; i += 64u) {
                     __builtin_nontemporal_store(sorted[s0 + i], out + d + i);
@@ -846,11 +926,15 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         }
         KMH_ST(8)
         if (!has_n) break;
-        lds_barrier();   // zeroed histogram visible; the staging's reads done before the next scatter
+        // with positions: the zeroed counters visible before the next histogram (without, the
+        // next scan's barrier orders this item's reads of pst and the staging before its writes)
+        if constexpr (!kEarly) lds_barrier();
         KMH_ST(9)
         item = nitem;
         cur = nxt;
         if constexpr (kPipe) hc = hn;
+#pragma unroll
+        for (int r = 0; r < kRR; ++r) aoff[r] = aoff_n[r];
         nitem = nnitem;
         has_n = has_nn;
         nxt = nn;
@@ -983,10 +1067,10 @@ __device__ __forceinline__ void out_store(T* p, T v) {
     else *p = v;
 }
 
-// Count work item: deduplication by a counting sort on the key's position inside its pass.
-// The keys of pass p of a bucket are the residues r with floor(r * np / 2^R) = p, so
-// (r * np) mod 2^R is increasing in r and spread evenly over [0, 2^R): its top 13 bits give
-// 8192 bins of about one key each (8192 keys per item).  Equal keys share a bin, so after a
+// Count work item: deduplication by a counting sort on 13 bits of the key.  The keys of pass p
+// of a bucket are the residues r with floor(r * np / 2^R) = p, a contiguous range; 13 bits of
+// the residue (bin_of) spread them over 8192 bins of about one key each (8192 keys per item).
+// Equal keys share a bin, so after a
 // counting sort (histogram, scan, scatter: one LDS atomic per key per pass over the keys, no
 // probing and no per-lane tail) every distinct key is resolved by comparing the few keys of its
 // bin.  A bin of more than BIG keys (a repeated k-mer) goes through a small LDS hash table
@@ -1127,10 +1211,14 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (tid == 0) nbig = bad = 0u;
     if (tid < kNW) scnt[tid] = 0u;
 
-    // bin = top 13 bits of (r * np) mod 2^R; u32 residues: (r << (32 - R)) * np mod 2^32 is that
-    // value shifted to the top of a word (one 32-bit multiply)
+    // bin = the residue's low 13 bits (one AND).  The counting sort needs only that equal keys
+    // share a bin and that a pass's keys spread evenly: a pass is a contiguous residue range
+    // (2^R / np wide, ~2^27 at config 5) whose low bits are as even as any other 13 of its bits.
+    // KMH_SP_BIN_MUL (A/B): the top 13 bits of (r * np) mod 2^R, ascending in r within the pass
+    // (a shift, a 32-bit multiply and a shift).
     auto bin_of = [&](E r, uint32_t np) -> uint32_t {
-        if constexpr (sizeof(E) == 4) return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
+        if constexpr (!KMH_SP_BIN_MUL) return (uint32_t)r & (uint32_t)(kBins - 1);
+        else if constexpr (sizeof(E) == 4) return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
         else return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
     };
 
@@ -1169,19 +1257,23 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     // of the region, 64 consecutive ones per register: coalesced, all in flight, nobody waits for
     // them here).  Lanes past the share (and an item over capacity, whose keys the fallback counts)
     // load entry 0 of the region, which exists.
+    //   The loads are not clamped: a wave's share starts at ea <= 7 C / 8 and its KPL * 64 = C / 8
+    //   loads stay inside the item's own region [0, C), so one lane offset + immediate offsets
+    //   address them all; a lane's valid keys are the prefix u < kn.
     auto issue_keys = [&](const Desc& d, E (&kr)[KPL], uint32_t (&kp)[POS ? KPL : 1], uint32_t& kn) {
+        static_assert(KPL * 64 * kNW == C, "a wave's loads stay in the region");
         const uint32_t n = keys_of(d);
         const uint32_t m = n <= (uint32_t)C ? n : 0u;
         const uint32_t ea = m * (uint32_t)wave / kNW, eb = m * (uint32_t)(wave + 1) / kNW;
-        const uint64_t base = (uint64_t)d.idx * C;
-        kn = 0u;
+        const uint64_t base = (uint64_t)d.idx * C + ea;   // (uniform)
+        const E* const kb = split + base;
+        const uint32_t span = eb - ea;
+        kn = span > (uint32_t)lane ? min((span - (uint32_t)lane + 63u) / 64u, (uint32_t)KPL) : 0u;
 #pragma unroll
         for (int u = 0; u < KPL; ++u) {
-            const uint32_t e = ea + 64u * (uint32_t)u + (uint32_t)lane;
-            kn += e < eb ? 1u : 0u;
-            const uint64_t ix = base + (e < eb ? e : 0u);
-            kr[u] = split[ix];
-            if constexpr (POS) kp[u] = opos[ix];
+            const uint32_t e = 64u * (uint32_t)u + (uint32_t)lane;
+            kr[u] = kb[e];
+            if constexpr (POS) kp[u] = opos[base + e];
         }
     };
 
@@ -1574,9 +1666,12 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         // 7. this item's stores, compacted per wave with ballot + mbcnt so that they are
         //    coalesced; keys re-read from `sorted` (the next scatter comes after a barrier)
         if (!fail_item && used) {   // uniform
-            const uint64_t at = obase + before;
+            // the wave's output base, made scalar (readfirstlane): every store below is that base
+            // plus a 32-bit byte offset (no 64-bit address arithmetic per key)
+            const uint64_t at = rfl64(obase + before);
+            uint64_t* const cw = codes + at;
+            uint32_t* const nw = counts + at;
             const uint64_t hib = (uint64_t)cur.c.b << R;
-            const uint64_t below = (1ull << lane) - 1ull;
             uint32_t run = 0u;
             const uint32_t stid = swz<EPC>((uint32_t)tid);
             constexpr int SB = KPL < 8 ? KPL : 8;   // keys re-read 8 at a time (one round trip)
@@ -1605,7 +1700,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     }
                     const uint64_t m = __ballot(f);
                     if (f) {
-                        const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                        const uint32_t ow = lane_rank(m, run);   // < C: offset within the wave's output
+                        const uint64_t o = at + ow;
 #if defined(KMH_EXPERIMENTS) && KMH_SP_OUT_EXP == 1
                         // what-if: a compact row (u32 residue + u8 count), same positions
                         out_store(reinterpret_cast<uint32_t*>(codes) + o, (uint32_t)sk[x]);
@@ -1614,8 +1710,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         // what-if: no output bytes at all (counts wrong; timing only)
                         if (sk[x] == (E)0x5A5A5A5Au && o == 0ull) codes[0] = hib + cv;
 #else
-                        out_store(codes + o, hib | (uint64_t)sk[x]);
-                        out_store(counts + o, cv);
+                        out_store(at_byte(cw, 8u * ow), hib | (uint64_t)sk[x]);
+                        out_store(at_byte(nw, 4u * ow), cv);
 #endif
                         if constexpr (POS) firsts[o] = ef[jj];
                     }
@@ -1629,7 +1725,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const bool f = (hs & CM) != 0ull;
                     const uint64_t m = __ballot(f);
                     if (f) {
-                        const uint64_t o = at + run + (uint32_t)__popcll(m & below);
+                        const uint64_t o = at + run + lane_rank(m);
                         codes[o] = hib | (hs >> CB);
                         counts[o] = (uint32_t)(hs & CM);
                         if constexpr (POS) firsts[o] = hmin[q * NT + tid];
