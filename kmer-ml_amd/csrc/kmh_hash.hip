@@ -52,10 +52,10 @@ constexpr int kQueue = 512;                // per-wave chunk queue of the split 
 #define KMH_SP_BIN_MUL 0
 #endif
 #ifndef KMH_SP_SPLIT_STB
-#define KMH_SP_SPLIT_STB 1
+#define KMH_SP_SPLIT_STB 0
 #endif
 #ifndef KMH_SP_RESERVE_EARLY
-#define KMH_SP_RESERVE_EARLY 1
+#define KMH_SP_RESERVE_EARLY 0
 #endif
 #ifndef KMH_SP_QU
 #define KMH_SP_QU 4
@@ -692,8 +692,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
     // region.  An item whose entries overflow the staging (total > kCaps, its bucket goes to the
     // fallback) reserves too; its count items are skipped, so nothing reads the regions.  These
     // returning adds go to memory (device scope) and take microseconds under the kernel's own
-    // traffic, so without positions they are issued one item early: right after the previous
-    // item's scatter, a whole store phase before their results are read.
+    // traffic; they are issued right after the pass histogram, before the scan.
     constexpr int kRR = (kMaxPasses + 64 * kNW - 1) / (64 * kNW);
     auto reserve = [&](const SplitItem& it, uint32_t (&ao)[kRR]) {
         const bool rep = it.np <= (uint32_t)kRepP;   // uniform
@@ -722,7 +721,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             }
         }
     };
-    // (KMH_SP_RESERVE_EARLY=0: the round-4 A/B baseline, reservations after the item's own histogram)
+    // (KMH_SP_RESERVE_EARLY=1, A/B: the next item's histogram and reservations ahead of this item's
+    // stores, without positions.  Measured slower: split 12.3-12.6 vs 11.7 ms at config 5, the
+    // stores issued a histogram later drain less behind the next item, profiles/r04/r04k/ab)
     constexpr bool kEarly = kPipe && KMH_SP_RESERVE_EARLY;
     uint32_t aoff[kRR];
     if constexpr (kEarly) {   // the first item's histogram and reservations
@@ -893,8 +894,8 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                             __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
                 }
 #elif KMH_SP_SPLIT_STB
-                // four staging reads in flight per lane (addresses clamped into the run), then their
-                // stores, each at the pass's uniform base + a 32-bit offset
+                // (A/B, not faster: 12.4 vs 12.4 ms) four staging reads in flight per lane (addresses
+                // clamped into the run), then their stores, each at the pass's base + a 32-bit offset
                 E* const ob = out + d;
                 uint32_t* const pb = POS ? opos + d : nullptr;
                 for (uint32_t i0 = 0; i0 < lim; i0 += 256u) {   // (uniform)
@@ -1068,8 +1069,9 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 }
 
 // Count work item: deduplication by a counting sort on 13 bits of the key.  The keys of pass p
-// of a bucket are the residues r with floor(r * np / 2^R) = p, a contiguous range; 13 bits of
-// the residue (bin_of) spread them over 8192 bins of about one key each (8192 keys per item).
+// of a bucket are the residues r with floor(r * np / 2^R) = p, a contiguous range; 13 middle
+// bits of the residue (bin_of) spread them over 8192 bins of about one key each (8192 keys per
+// item).
 // Equal keys share a bin, so after a
 // counting sort (histogram, scan, scatter: one LDS atomic per key per pass over the keys, no
 // probing and no per-lane tail) every distinct key is resolved by comparing the few keys of its
@@ -1211,15 +1213,26 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     if (tid == 0) nbig = bad = 0u;
     if (tid < kNW) scnt[tid] = 0u;
 
-    // bin = the residue's low 13 bits (one AND).  The counting sort needs only that equal keys
-    // share a bin and that a pass's keys spread evenly: a pass is a contiguous residue range
-    // (2^R / np wide, ~2^27 at config 5) whose low bits are as even as any other 13 of its bits.
-    // KMH_SP_BIN_MUL (A/B): the top 13 bits of (r * np) mod 2^R, ascending in r within the pass
-    // (a shift, a 32-bit multiply and a shift).
+    // bin = 13 bits of the residue, bits [s, s + 13) with s = R - ceil(log2 np) - 16 (>= 0): one
+    // bit-field extract at a per-item scalar shift.  The counting sort needs only that equal keys
+    // share a bin and that a pass's keys spread evenly.  A pass is a contiguous residue range of
+    // 2^R / np >= 2^(R - ceil(log2 np)) values, i.e. at least 8 periods of the field (<= 12.5 %
+    // uneven), and the field stays clear of the residue's lowest bits: a canonical code is <= its
+    // reverse complement, so its last bases are constrained by its first ones (the bucket), and
+    // the low 13 bits put ~7x more keys into bins of 5+ (bins >= 5 per item: 122 vs 18 in a 50 Mbp
+    // simulation; the lowest-bits version ran config 5's count at 145 ms instead of 16).
+    // KMH_SP_BIN_MUL (A/B): the top 13 bits of (r * np) mod 2^R (a 32-bit multiply).
     auto bin_of = [&](E r, uint32_t np) -> uint32_t {
-        if constexpr (!KMH_SP_BIN_MUL) return (uint32_t)r & (uint32_t)(kBins - 1);
-        else if constexpr (sizeof(E) == 4) return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
-        else return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
+        if constexpr (!KMH_SP_BIN_MUL) {
+            const int lg = np > 1u ? 32 - __builtin_clz(np - 1u) : 0;   // (scalar)
+            const int sh = R - lg - 16 > 0 ? R - lg - 16 : 0;
+            if constexpr (sizeof(E) == 4) return __builtin_amdgcn_ubfe((uint32_t)r, (uint32_t)sh, (uint32_t)kBinBits);
+            else return (uint32_t)((uint64_t)r >> sh) & (uint32_t)(kBins - 1);
+        } else if constexpr (sizeof(E) == 4) {
+            return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
+        } else {
+            return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
+        }
     };
 
     // An item as loaded: its descriptor, the gb_fail flag of its bucket (a pass of a bucket whose
