@@ -48,6 +48,9 @@ constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
+#ifndef KMH_SP_SPLIT_VDESC
+#define KMH_SP_SPLIT_VDESC 0
+#endif
 #ifndef KMH_SP_BIN_MUL
 #define KMH_SP_BIN_MUL 0
 #endif
@@ -375,6 +378,24 @@ __device__ __forceinline__ E lane_of(const uint4& v, int i) {
 }
 
 // Split work item: tiles [t0, t1) (batch-relative) of bucket b of one genome.
+// A value every lane loads from the same address, as a VECTOR load (its address laundered through
+// a VGPR).  A scalar load (s_load) counts in lgkmcnt like the LDS operations, and the compiler
+// waits for it with lgkmcnt(0) at the next LDS wait (scalar loads return out of order): every
+// descriptor prefetched with s_load stalled the following LDS phase for a memory round trip.  A
+// vector load counts in vmcnt and is read (readfirstlane) where the wave waits for its vector loads
+// anyway.
+template <typename T>
+__device__ __forceinline__ T vload(const T* p) {
+    uint64_t a = reinterpret_cast<uint64_t>(p);
+    asm volatile("" : "+v"(a));
+    using gT = __attribute__((address_space(1))) const T;
+    return *reinterpret_cast<gT*>(a);
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
+
 struct SplitItem {
     uint32_t b, t0, t1, np;
     uint32_t gb;       // (genome, bucket) index within the batch: failure flag slot
@@ -743,6 +764,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         const bool has_nn = has_n && nnitem < xb;   // uniform
         uint32_t lo_nn = 0u, hi_nn = 0u;
         SplitItem nnn;
+#if KMH_SP_SPLIT_VDESC
+        uint64_t rawn[4];   // the descriptor of item nnitem + nwx (see B)
+#endif
         {   // on every path (after the last item: a copy of the current one, never used)
             uint64_t tw;
             bool single;
@@ -755,7 +779,18 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             }
             KMH_ST(0)
             bounds(nn, lo_nn, hi_nn);
-            nnn = items[has_nn && nnitem + nwx < xb ? nnitem + nwx : item];
+            // the descriptor two items ahead.  KMH_SP_SPLIT_VDESC (A/B): as vector loads read
+            // (readfirstlane) below where the wave waits for its loads anyway, since a scalar load
+            // is waited for by the histogram's barrier (lgkmcnt(0) covers LDS and scalar loads)
+            const uint32_t inn = has_nn && nnitem + nwx < xb ? nnitem + nwx : item;
+#if KMH_SP_SPLIT_VDESC
+            const uint64_t* ip = reinterpret_cast<const uint64_t*>(items + inn);
+            static_assert(sizeof(SplitItem) == 32, "descriptor as four 8-byte loads");
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) rawn[qq] = vload(ip + qq);
+#else
+            nnn = items[inn];
+#endif
             KMH_ST(1)
         }
 
@@ -826,7 +861,19 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
 
         // A and B have landed by now (waited for here, not behind D's stores)
         if constexpr (kPipe) landed(hn);
+#if KMH_SP_SPLIT_VDESC
+        asm volatile("" ::"v"(lo_nn), "v"(hi_nn), "v"(rawn[0]), "v"(rawn[1]), "v"(rawn[2]), "v"(rawn[3]));
+        nnn.b = rfl((uint32_t)rawn[0]);
+        nnn.t0 = rfl((uint32_t)(rawn[0] >> 32));
+        nnn.t1 = rfl((uint32_t)rawn[1]);
+        nnn.np = rfl((uint32_t)(rawn[1] >> 32));
+        nnn.gb = rfl((uint32_t)rawn[2]);
+        nnn.per = rfl((uint32_t)(rawn[2] >> 32));
+        nnn.cbase = rfl((uint32_t)rawn[3]);
+        nnn.pad = 0u;
+#else
         asm volatile("" ::"v"(lo_nn), "v"(hi_nn));
+#endif
         KMH_ST(7)
         hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next histogram follows a barrier
 
@@ -1071,30 +1118,11 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // Count work item: deduplication by a counting sort on 13 bits of the key.  The keys of pass p
 // of a bucket are the residues r with floor(r * np / 2^R) = p, a contiguous range; 13 middle
 // bits of the residue (bin_of) spread them over 8192 bins of about one key each (8192 keys per
-// item).
-// Equal keys share a bin, so after a
-// counting sort (histogram, scan, scatter: one LDS atomic per key per pass over the keys, no
+// item).  Equal keys share a bin, so after a counting sort (histogram, scan, scatter: one LDS
+// atomic per key per pass over the keys, no
 // probing and no per-lane tail) every distinct key is resolved by comparing the few keys of its
 // bin.  A bin of more than BIG keys (a repeated k-mer) goes through a small LDS hash table
 // instead, so repeats cost what they cost the hash kernel before.
-// A value every lane loads from the same address, as a VECTOR load (its address laundered through
-// a VGPR).  A scalar load (s_load) counts in lgkmcnt like the LDS operations, and the compiler
-// waits for it with lgkmcnt(0) at the next LDS wait (scalar loads return out of order): every
-// descriptor prefetched with s_load stalled the following LDS phase for a memory round trip.  A
-// vector load counts in vmcnt and is read (readfirstlane) where the wave waits for its vector loads
-// anyway.
-template <typename T>
-__device__ __forceinline__ T vload(const T* p) {
-    uint64_t a = reinterpret_cast<uint64_t>(p);
-    asm volatile("" : "+v"(a));
-    using gT = __attribute__((address_space(1))) const T;
-    return *reinterpret_cast<gT*>(a);
-}
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
-}
-
 // k_sp_count's `sorted` / `spos` and `hist` are stored with their 16-byte slots XOR-swizzled:
 // slot c lives at c ^ ((c >> 4) & 3).  A ds_read_b128 is serviced in lane groups of 16 (e.g.
 // lanes 0-3, 12-15, 20-27) whose lane numbers are distinct mod 16; a thread reading slot 4t + q
