@@ -765,7 +765,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         uint32_t lo_nn = 0u, hi_nn = 0u;
         SplitItem nnn;
 #if KMH_SP_SPLIT_VDESC
-        uint64_t rawn[4];   // the descriptor of item nnitem + nwx (see B)
+        uint32_t rawn;   // word lane % 8 of the descriptor of item nnitem + nwx (see B)
 #endif
         {   // on every path (after the last item: a copy of the current one, never used)
             uint64_t tw;
@@ -779,15 +779,14 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             }
             KMH_ST(0)
             bounds(nn, lo_nn, hi_nn);
-            // the descriptor two items ahead.  KMH_SP_SPLIT_VDESC (A/B): as vector loads read
-            // (readfirstlane) below where the wave waits for its loads anyway, since a scalar load
-            // is waited for by the histogram's barrier (lgkmcnt(0) covers LDS and scalar loads)
+            // the descriptor two items ahead.  KMH_SP_SPLIT_VDESC (A/B): one vector load, word
+            // lane % 8 per lane (one VGPR, one cache line), read by readlane below where the wave
+            // waits for its loads anyway, since a scalar load is waited for by the histogram's
+            // barrier (lgkmcnt(0) covers LDS and scalar loads alike)
             const uint32_t inn = has_nn && nnitem + nwx < xb ? nnitem + nwx : item;
 #if KMH_SP_SPLIT_VDESC
-            const uint64_t* ip = reinterpret_cast<const uint64_t*>(items + inn);
-            static_assert(sizeof(SplitItem) == 32, "descriptor as four 8-byte loads");
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) rawn[qq] = vload(ip + qq);
+            static_assert(sizeof(SplitItem) == 32, "descriptor as eight words");
+            rawn = reinterpret_cast<const uint32_t*>(items + inn)[lane & 7];
 #else
             nnn = items[inn];
 #endif
@@ -862,14 +861,14 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         // A and B have landed by now (waited for here, not behind D's stores)
         if constexpr (kPipe) landed(hn);
 #if KMH_SP_SPLIT_VDESC
-        asm volatile("" ::"v"(lo_nn), "v"(hi_nn), "v"(rawn[0]), "v"(rawn[1]), "v"(rawn[2]), "v"(rawn[3]));
-        nnn.b = rfl((uint32_t)rawn[0]);
-        nnn.t0 = rfl((uint32_t)(rawn[0] >> 32));
-        nnn.t1 = rfl((uint32_t)rawn[1]);
-        nnn.np = rfl((uint32_t)(rawn[1] >> 32));
-        nnn.gb = rfl((uint32_t)rawn[2]);
-        nnn.per = rfl((uint32_t)(rawn[2] >> 32));
-        nnn.cbase = rfl((uint32_t)rawn[3]);
+        asm volatile("" ::"v"(lo_nn), "v"(hi_nn), "v"(rawn));
+        nnn.b = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 0);
+        nnn.t0 = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 1);
+        nnn.t1 = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 2);
+        nnn.np = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 3);
+        nnn.gb = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 4);
+        nnn.per = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 5);
+        nnn.cbase = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 6);
         nnn.pad = 0u;
 #else
         asm volatile("" ::"v"(lo_nn), "v"(hi_nn));

@@ -13,8 +13,8 @@ if [ -z "$2" ]; then
 fi
 timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 11
 timeout -k 10 300 python3 -u bench.py > $OUT/bench.log 2>&1 || exit 12
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 > $OUT/trace.log 2>&1 || exit 13
-B="bench.py --steps 2 --warmup 1 --cpu-sample 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 --no-e2e > $OUT/trace.log 2>&1 || exit 13
+B="bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-e2e"   # (the e2e cases launch the same kernels on small genomes)
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/f -o f -- python3 $B > $OUT/f.log 2>&1 || exit 14
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/w -o w -- python3 $B > $OUT/w.log 2>&1 || exit 15
 echo done > $OUT/done
