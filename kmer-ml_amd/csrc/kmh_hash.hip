@@ -48,6 +48,9 @@ constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
+#ifndef KMH_SP_SPLIT_NT
+#define KMH_SP_SPLIT_NT 1
+#endif
 #ifndef KMH_SP_SPLIT_VDESC
 #define KMH_SP_SPLIT_VDESC 0
 #endif
@@ -965,8 +968,13 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                 }
 #else
                 for (uint32_t i = (uint32_t)lane; i < lim; i += 64u) {
-                    __builtin_nontemporal_store(sorted[s0 + i], out + d + i);
-                    if constexpr (POS) __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
+                    if constexpr (KMH_SP_SPLIT_NT) {
+                        __builtin_nontemporal_store(sorted[s0 + i], out + d + i);
+                        if constexpr (POS) __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
+                    } else {   // (A/B) plain stores: the L2 completes the runs' partial lines
+                        out[d + i] = sorted[s0 + i];
+                        if constexpr (POS) opos[d + i] = spos[s0 + i];
+                    }
                 }
 #endif
             }
