@@ -1114,7 +1114,13 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
 
 // Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel).
 #ifndef KMH_SP_NT_OUT
-#define KMH_SP_NT_OUT 1   // non-temporal: 42.9 -> 42.5 ms per config-5 step (profiles/r03/r03c_ab_nt.txt)
+// Count output stores: plain since round 4.  Non-temporal stores helped in round 3 (42.9 -> 42.5 ms,
+// profiles/r03/r03c_ab_nt.txt), but with the round-4 stores (a wave's run at a scalar base) they
+// write each run's partial 128-byte lines to HBM unmerged: 54.4 GB for 48 GB of output, count
+// 16.5-16.7 ms vs 14.6 ms with plain stores, which the L2 completes into full lines (48.0 GB;
+// profiles/r04/r04n).  The split keeps non-temporal stores (KMH_SP_SPLIT_NT: plain ones wrote
+// 16.7 instead of 18.7 GB but ran 11.9 vs 11.2 ms).
+#define KMH_SP_NT_OUT 0
 #endif
 template <typename T>
 __device__ __forceinline__ void out_store(T* p, T v) {
