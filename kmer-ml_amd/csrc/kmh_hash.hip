@@ -48,6 +48,9 @@ constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
+#ifndef KMH_SP_SPLIT_ORDER
+#define KMH_SP_SPLIT_ORDER 0
+#endif
 #ifndef KMH_SP_SPLIT_NT
 #define KMH_SP_SPLIT_NT 1
 #endif
@@ -1112,14 +1115,33 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
         citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, (uint32_t)gb, n};
 }
 
+// Split items in tile order (KMH_SP_SPLIT_ORDER): key = (genome in batch, first tile, bucket).  A
+// (tile, bucket) segment is ~128 bytes at an arbitrary offset of its tile's entries, so the lines
+// at its ends hold the neighbouring buckets' segments; with the items of neighbouring buckets of
+// one tile range adjacent, an XCD's workgroups read those lines together (its L2 serves the
+// second read) instead of one item after the other bucket's items have run.
+__global__ __launch_bounds__(256) void k_sp_order_keys(const SplitItem* __restrict__ it, uint32_t n,
+                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const SplitItem x = it[i];
+    keys[i] = ((uint64_t)(x.gb / (uint32_t)kSpBuckets) << 44) | ((uint64_t)x.t0 << 10) | (uint64_t)x.b;
+    vals[i] = i;
+}
+__global__ __launch_bounds__(256) void k_sp_permute(const SplitItem* __restrict__ in, const uint32_t* __restrict__ idx,
+                                                    uint32_t n, SplitItem* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) out[i] = in[idx[i]];
+}
+
 // Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel).
 #ifndef KMH_SP_NT_OUT
 // Count output stores: plain since round 4.  Non-temporal stores helped in round 3 (42.9 -> 42.5 ms,
 // profiles/r03/r03c_ab_nt.txt), but with the round-4 stores (a wave's run at a scalar base) they
-// write each run's partial 128-byte lines to HBM unmerged: 54.4 GB for 48 GB of output, count
+// write each run's partial 128-byte lines to HBM unmerged: 55.7 GB for 48 GB of output, count
 // 16.5-16.7 ms vs 14.6 ms with plain stores, which the L2 completes into full lines (48.0 GB;
 // profiles/r04/r04n).  The split keeps non-temporal stores (KMH_SP_SPLIT_NT: plain ones wrote
-// 16.7 instead of 18.7 GB but ran 11.9 vs 11.2 ms).
+// 16.7 instead of 19.2 GB but ran 11.9 vs 11.2 ms).
 #define KMH_SP_NT_OUT 0
 #endif
 template <typename T>
@@ -2113,8 +2135,10 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const size_t sib = (nsi * sizeof(SplitItem) + 255) & ~(size_t)255;
         const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
-        const size_t fb = (nci + 1) * 4;
-        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb);
+        const size_t fb = ((nci + 1) * 4 + 255) & ~(size_t)255;
+        // (KMH_SP_SPLIT_ORDER) the items in tile order: sort keys and values (2 x 12 B) + the copy
+        const size_t okb = KMH_SP_SPLIT_ORDER ? ((nsi * 24 + 255) & ~(size_t)255) + sib : 0;
+        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb + okb);
         if (rc) return rc;
         char* base = static_cast<char*>(ctx->sparse[1].ptr);
         SplitItem* d_sitems = reinterpret_cast<SplitItem*>(base);
@@ -2124,6 +2148,26 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         hipLaunchKernelGGL(k_sp_fill, dim3((unsigned)ngb), dim3(64), 0, s, d_nb, d_tbase, g0, L.tbase[g0],
                            target, split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_sitems, d_citems);
         KMH_HIP(ctx, hipGetLastError());
+        if constexpr (KMH_SP_SPLIT_ORDER) {
+            char* ob2 = base + sib + cib + ob + fb;
+            uint64_t* ka = reinterpret_cast<uint64_t*>(ob2);
+            uint64_t* kb = ka + nsi;
+            uint32_t* va = reinterpret_cast<uint32_t*>(kb + nsi);
+            uint32_t* vb = va + nsi;
+            SplitItem* d_sorted_items = reinterpret_cast<SplitItem*>(ob2 + ((nsi * 24 + 255) & ~(size_t)255));
+            const unsigned og = (unsigned)((nsi + 255) / 256);
+            hipLaunchKernelGGL(k_sp_order_keys, dim3(og), dim3(256), 0, s, d_sitems, (uint32_t)nsi, ka, va);
+            KMH_HIP(ctx, hipGetLastError());
+            bool alt = false;
+            int hb = 44 + 1;
+            while (hb < 64 && ((uint64_t)nG >> (hb - 44)) != 0) ++hb;
+            rc = radix_sort_pairs<uint64_t>(ctx, ka, kb, va, vb, nsi, 0, hb, &alt, s);
+            if (rc) return rc;
+            hipLaunchKernelGGL(k_sp_permute, dim3(og), dim3(256), 0, s, d_sitems, alt ? vb : va, (uint32_t)nsi,
+                               d_sorted_items);
+            KMH_HIP(ctx, hipGetLastError());
+            d_sitems = d_sorted_items;
+        }
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         time_begin(ctx, s, "k_sp_split");
