@@ -1120,7 +1120,7 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
 // at its ends hold the neighbouring buckets' segments; with the items of neighbouring buckets of
 // one tile range adjacent, an XCD's workgroups read those lines together (its L2 serves the
 // second read) instead of one item after the other bucket's items have run.
-__global__ __launch_bounds__(256) void k_sp_order_keys(const SplitItem* __restrict__ it, uint32_t n,
+[[maybe_unused]] __global__ __launch_bounds__(256) void k_sp_order_keys(const SplitItem* __restrict__ it, uint32_t n,
                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
@@ -1128,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_sp_order_keys(const SplitItem* __restri
     keys[i] = ((uint64_t)(x.gb / (uint32_t)kSpBuckets) << 44) | ((uint64_t)x.t0 << 10) | (uint64_t)x.b;
     vals[i] = i;
 }
-__global__ __launch_bounds__(256) void k_sp_permute(const SplitItem* __restrict__ in, const uint32_t* __restrict__ idx,
+[[maybe_unused]] __global__ __launch_bounds__(256) void k_sp_permute(const SplitItem* __restrict__ in, const uint32_t* __restrict__ idx,
                                                     uint32_t n, SplitItem* __restrict__ out) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i < n) out[i] = in[idx[i]];
