@@ -124,8 +124,10 @@ __host__ __device__ __forceinline__ uint32_t split_bt(uint32_t per, uint32_t epc
 }
 
 // Passes of one bucket.  With positions (the drop-in) a pass holds 1920-3840 keys, so a bucket of
-// a 2^32-window organism needs ~2200 passes; the split keeps a pass's staging start and region
-// offset as u16 halves of one LDS word (4096 words).
+// a 2^32-window organism needs ~2200 passes; the split keeps each pass's staging start in LDS
+// (pst, kMaxPasses + 1 words) and its reserved region offset in registers (one lane per pass).
+// A bucket that needs more passes fails them, and they are recounted together (one gather + sort
+// per (genome, bucket): fallback_passes).
 constexpr int kMaxPasses = 4096;
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;   // idle queue entry
 
