@@ -121,6 +121,24 @@ using kmh::fail;
 // torch's default stream); the context's own stream serves the host-buffer calls only.
 static hipStream_t pick_stream(kmh_ctx*, void* stream) { return static_cast<hipStream_t>(stream); }
 
+// Stream order of the context's workspace (one context shared by threads on different streams).
+// The _dev entry points return before their kernels finish and every call reuses the context's
+// cached device workspace, so a call on stream s first makes s wait for the work the previous
+// call queued on another stream, then records ctx->ws_done on s once its own work is queued.
+// Calls on one stream are ordered by the stream; calls on different streams run one after the
+// other on the device and never share the workspace in flight (tests/test_gpu_parity.py,
+// test_context_shared_by_two_streams).  Buffer growth and release synchronise the device.
+template <typename F>
+static int on_stream(kmh_ctx* ctx, hipStream_t s, F&& body) {
+    if (ctx->ws_pending && ctx->ws_stream != s) KMH_HIP(ctx, hipStreamWaitEvent(s, ctx->ws_done, 0));
+    const int rc = body(s);
+    if (!ctx->ws_done) KMH_HIP(ctx, hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming));
+    KMH_HIP(ctx, hipEventRecord(ctx->ws_done, s));
+    ctx->ws_stream = s;
+    ctx->ws_pending = true;
+    return rc;
+}
+
 extern "C" {
 
 const char* kmh_version(void) { return "kmerhip 0.2.0 gfx950"; }
@@ -210,6 +228,7 @@ int kmh_ctx_trim(kmh_ctx* ctx, uint64_t keep_bytes) {
         kmh::set_thread_error("kmh_ctx_trim: ctx is NULL");
         return KMH_ERR_INVALID;
     }
+    ctx->err.clear();
     if (workspace_bytes(ctx) <= keep_bytes) return KMH_OK;
     KMH_HIP(ctx, hipSetDevice(ctx->device));
     free_workspace(ctx);
@@ -226,6 +245,7 @@ void kmh_ctx_destroy(kmh_ctx* ctx) {
         if (t.stop) (void)hipEventDestroy(t.stop);
     }
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->ws_done) (void)hipEventDestroy(ctx->ws_done);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -284,7 +304,9 @@ int kmh_count_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offs
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::dense_count(ctx, d_seq, offsets, G, k, d_matrix, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::dense_count(ctx, d_seq, offsets, G, k, d_matrix, s);
+    });
 }
 
 int kmh_first_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
@@ -292,7 +314,9 @@ int kmh_first_dense_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offs
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::dense_first(ctx, d_seq, offsets, G, k, d_first, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::dense_first(ctx, d_seq, offsets, G, k, d_first, s);
+    });
 }
 
 int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, int G,
@@ -300,7 +324,9 @@ int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, i
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::synth(ctx, d_seq, len, stride, G, seed0, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::synth(ctx, d_seq, len, stride, G, seed0, s);
+    });
 }
 
 int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
@@ -309,8 +335,10 @@ int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* off
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::sparse_count_dev(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers,
-                                 pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::sparse_count_dev(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nkmers,
+                                 s);
+    });
 }
 
 uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off) {
@@ -324,7 +352,9 @@ int kmh_rows_encode_u8_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, 
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::rows_encode_u8(ctx, d_rows, rows, cols, d_u8, d_esc, cap, d_esc_n, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::rows_encode_u8(ctx, d_rows, rows, cols, d_u8, d_esc, cap, d_esc_n, s);
+    });
 }
 
 int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uint64_t cols,
@@ -333,8 +363,10 @@ int kmh_rows_decode_u8_dev(kmh_ctx* ctx, const uint8_t* d_u8, uint64_t rows, uin
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::rows_decode_u8(ctx, d_u8, rows, cols, d_esc, cap, d_esc_n, ranks, rows_per_rank,
-                               d_rows, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::rows_decode_u8(ctx, d_u8, rows, cols, d_esc, cap, d_esc_n, ranks, rows_per_rank,
+                               d_rows, s);
+    });
 }
 
 int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, uint64_t cols,
@@ -343,7 +375,9 @@ int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, 
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::rows_encode_u4(ctx, d_rows, rows, cols, d_u4, d_esc, cap, d_esc_n, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::rows_encode_u4(ctx, d_rows, rows, cols, d_u4, d_esc, cap, d_esc_n, s);
+    });
 }
 
 int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
@@ -352,7 +386,9 @@ int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uin
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::rows_decode_u4(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::rows_decode_u4(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, d_rows, s);
+    });
 }
 
 int kmh_count_dense_u4_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
@@ -361,8 +397,10 @@ int kmh_count_dense_u4_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* o
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::dense_count_u4(ctx, d_seq, offsets, G, k, d_matrix, d_u4, d_esc, cap, d_esc_n,
-                               pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::dense_count_u4(ctx, d_seq, offsets, G, k, d_matrix, d_u4, d_esc, cap, d_esc_n,
+                               s);
+    });
 }
 
 int kmh_rows_decode_u4_range_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,
@@ -371,8 +409,10 @@ int kmh_rows_decode_u4_range_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t row
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::rows_decode_u4_range(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, row0, nrows, d_rows,
-                                     pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::rows_decode_u4_range(ctx, d_u4, rows, cols, d_esc, cap, d_esc_n, row0, nrows, d_rows,
+                                     s);
+    });
 }
 
 int kmh_feature_columns_dev(kmh_ctx* ctx, const uint64_t* d_codes, uint64_t n, int k, const int32_t* d_order,
@@ -381,8 +421,10 @@ int kmh_feature_columns_dev(kmh_ctx* ctx, const uint64_t* d_codes, uint64_t n, i
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return kmh::feature_columns(ctx, d_codes, n, k, d_order, d_lg, d_cnt, d_cpg, d_rep, d_gc, d_oe, d_ent,
-                                pick_stream(ctx, stream));
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::feature_columns(ctx, d_codes, n, k, d_order, d_lg, d_cnt, d_cpg, d_rep, d_gc, d_oe, d_ent,
+                                s);
+    });
 }
 
 // Host sequence -> device (padded with one non-base byte so loads past the end are safe).
@@ -409,16 +451,18 @@ int kmh_count_dense_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, ui
     if (n >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "sequence must be shorter than 2^32 - 1 bytes");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     const size_t bins = (size_t)1 << (2 * k);
-    uint8_t* d_seq = nullptr;
-    int rc = stage_sequence(ctx, seq, n, &d_seq);
-    if (rc) return rc;
-    if ((rc = kmh::ensure(ctx, ctx->out, bins * sizeof(uint32_t)))) return rc;
-    const uint64_t off[2] = {0, n};
-    uint32_t* d_counts = static_cast<uint32_t*>(ctx->out.ptr);
-    if ((rc = kmh::dense_count(ctx, d_seq, off, 1, k, d_counts, ctx->stream))) return rc;
-    KMH_HIP(ctx, hipMemcpyAsync(counts, d_counts, bins * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return KMH_OK;
+    return on_stream(ctx, ctx->stream, [&](hipStream_t) {
+        uint8_t* d_seq = nullptr;
+        int rc = stage_sequence(ctx, seq, n, &d_seq);
+        if (rc) return rc;
+        if ((rc = kmh::ensure(ctx, ctx->out, bins * sizeof(uint32_t)))) return rc;
+        const uint64_t off[2] = {0, n};
+        uint32_t* d_counts = static_cast<uint32_t*>(ctx->out.ptr);
+        if ((rc = kmh::dense_count(ctx, d_seq, off, 1, k, d_counts, ctx->stream))) return rc;
+        KMH_HIP(ctx, hipMemcpyAsync(counts, d_counts, bins * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+        KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        return KMH_OK;
+    });
 }
 
 // Checks of every host-buffer count call, before any byte is read or staged.
@@ -443,9 +487,11 @@ int kmh_count_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n, int k, int cano
     int rc = check_count_args(ctx, n, k, canonical);
     if (rc) return rc;
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    uint8_t* d_seq = nullptr;
-    if ((rc = stage_sequence(ctx, seq, n, &d_seq))) return rc;
-    return count_staged_impl(ctx, d_seq, n, k, canonical, out);
+    return on_stream(ctx, ctx->stream, [&](hipStream_t) {
+        uint8_t* d_seq = nullptr;
+        int rc2 = stage_sequence(ctx, seq, n, &d_seq);
+        return rc2 ? rc2 : count_staged_impl(ctx, d_seq, n, k, canonical, out);
+    });
 }
 
 int kmh_stage_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n) {
@@ -456,7 +502,7 @@ int kmh_stage_host(kmh_ctx* ctx, const uint8_t* seq, uint64_t n) {
         return fail(ctx, KMH_ERR_UNSUPPORTED, "sequence must be shorter than 2^32 - 1 bytes (one call)");
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     uint8_t* d_seq = nullptr;
-    int rc = stage_sequence(ctx, seq, n, &d_seq);
+    int rc = on_stream(ctx, ctx->stream, [&](hipStream_t) { return stage_sequence(ctx, seq, n, &d_seq); });
     if (rc) return rc;
     // the host buffer may change after return: the copy from pageable memory completes first
     KMH_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -476,7 +522,9 @@ int kmh_count_staged(kmh_ctx* ctx, int k, int canonical, kmh_kmers** out) {
     int rc = check_count_args(ctx, ctx->staged_n, k, canonical);
     if (rc) return rc;
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return count_staged_impl(ctx, static_cast<uint8_t*>(ctx->seq.ptr), ctx->staged_n, k, canonical, out);
+    return on_stream(ctx, ctx->stream, [&](hipStream_t) {
+        return count_staged_impl(ctx, static_cast<uint8_t*>(ctx->seq.ptr), ctx->staged_n, k, canonical, out);
+    });
 }
 
 static int count_staged_impl(kmh_ctx* ctx, uint8_t* d_seq, uint64_t n, int k, int canonical, kmh_kmers** out) {

@@ -50,6 +50,11 @@ struct Ctx {
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
     hipEvent_t pinned_ready = nullptr;
+    // workspace stream order (kmh_api.cpp, on_stream): the stream of the last call that queued
+    // work on the workspace, and an event recorded on it after that work
+    hipEvent_t ws_done = nullptr;
+    hipStream_t ws_stream = nullptr;
+    bool ws_pending = false;
     // per-kernel timing
     bool timing = false;
     bool timing_skip = false;        // the launch in flight is not timed (KMH_TIMING_ONLY)

@@ -519,12 +519,13 @@ def _code_splitters(rows, k, world, group):
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     cum = np.cumsum(t.cpu().numpy())
     total = int(cum[-1]) if cum.size else 0
-    bounds = [0]
+    # bucket indices stay unshifted (monotone, <= nb) until the end; the last bound is the
+    # code space's end, 1 << 64 at k = 32 (a Python int: never converted to uint64)
+    idx = [0]
     for q in range(1, world):
         b = int(np.searchsorted(cum, total * q / world, side="left")) + 1 if total else (nb * q) // world
-        bounds.append(max(bounds[-1], min(b, nb)) << sh)
-    bounds.append(1 << bits)
-    return bounds
+        idx.append(max(idx[-1], min(b, nb)))
+    return [i << sh for i in idx] + [1 << bits]
 
 
 def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows_fn=None):
@@ -555,7 +556,9 @@ def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     bounds = _code_splitters(rows, k, world, group)
     # per destination: for each of my genomes, the slice of its sorted row in that range
-    cuts = [np.searchsorted(c, np.array(bounds, dtype=np.uint64), side="left") for c, _ in rows]
+    # (the last bound, 1 << 2k, may be 1 << 64: every code lies below it, so its cut is len(c))
+    inner = np.array(bounds[:-1], dtype=np.uint64)
+    cuts = [np.append(np.searchsorted(c, inner, side="left"), c.size) for c, _ in rows]
     send_len = np.array([[int(cut[q + 1] - cut[q]) for cut in cuts] for q in range(world)], np.int64)
     # every rank learns every (source, destination, genome) length: the layout of what it receives
     lens = [None] * world

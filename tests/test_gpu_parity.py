@@ -836,6 +836,62 @@ def test_count_result_views_outlive_other_views(ctx):
     del junk
 
 
+def test_context_shared_by_two_streams(ctx, dev, oracle_lib):
+    """One context (the process-wide _native.context) used by two threads, each counting its
+    own genomes on its own stream, dense k = 12 and sparse k = 21 interleaved: the _dev calls
+    return before their kernels finish and share the context's cached workspace, so the C ABI
+    orders a call behind the previous call's work on another stream (kmh_api.cpp on_stream).
+    Every result matches the oracle."""
+    import threading
+    sets = [[osynth.synth_bases(3_000_000 + 4096 * i + 37 * t, osynth.genome_seed(40 + 4 * t + i))
+             for i in range(3)] for t in range(2)]
+    results, errors = [{}, {}], []
+
+    def work(t):
+        try:
+            st = torch.cuda.Stream(device=dev)
+            buf, offs = _layout(sets[t])
+            with torch.cuda.stream(st):
+                d_seq = torch.from_numpy(buf.copy()).to(dev, non_blocking=False)
+                out_off = _native.sparse_out_offsets(offs, 21)
+                for rep in range(3):
+                    out = torch.full((3, 1 << 24), -7, dtype=torch.int32, device=dev)
+                    ctx.count_dense_dev(d_seq.data_ptr(), offs, 12, out.data_ptr(), st.cuda_stream)
+                    d_codes = torch.empty(int(out_off[-1]), dtype=torch.int64, device=dev)
+                    d_counts = torch.empty(int(out_off[-1]), dtype=torch.int32, device=dev)
+                    d_nk = torch.empty(3, dtype=torch.int64, device=dev)
+                    ctx.count_sparse_dev(d_seq.data_ptr(), offs, 21, 1, d_codes.data_ptr(), d_counts.data_ptr(),
+                                         d_nk.data_ptr(), st.cuda_stream)
+                    results[t][rep] = (out, d_codes, d_counts, d_nk)
+            st.synchronize()
+        except Exception as e:   # noqa: BLE001 -- reported by the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t in range(2):
+        buf, offs = _layout(sets[t])
+        out_off = _native.sparse_out_offsets(offs, 21)
+        for rep in range(3):
+            out, d_codes, d_counts, d_nk = results[t][rep]
+            rows = out.cpu().numpy().view(np.uint32)
+            codes = d_codes.cpu().numpy().view(np.uint64)
+            counts = d_counts.cpu().numpy().view(np.uint32)
+            nk = d_nk.cpu().numpy()
+            for g, seq in enumerate(sets[t]):
+                assert np.array_equal(rows[g], oracle_lib.count_dense(seq, 12)), (t, rep, g)
+                a, n = int(out_off[g]), int(nk[g])
+                o = np.argsort(codes[a:a + n], kind="stable")
+                wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
+                assert np.array_equal(codes[a:a + n][o], wc), (t, rep, g)
+                assert np.array_equal(counts[a:a + n][o], wn), (t, rep, g)
+
+
 def test_bench_pipelined_u8_assembly_rccl():
     """bench.py's pipelined u8 all-gather path (the N > 1 default) through RCCL, one rank."""
     r = _torchrun(["bench.py", "--assemble", "u8", "--genomes", "3", "--genome-len", "3000000",
