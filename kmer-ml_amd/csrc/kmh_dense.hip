@@ -471,10 +471,6 @@ __device__ __forceinline__ void count_chunk(uint32_t* tbl, uint4 q, uint32_t nv,
     }
 }
 
-#ifndef KMH_COUNT_DYN
-#define KMH_COUNT_DYN 1   // 1.90 -> 1.76 ms per config-3 count launch (profiles/r03/ab/r03o_*)
-#endif
-
 // Tiles per wave batch: the expected chunks of a batch must fit the wave's queue of qmax
 // entries (a batch that overflows it is walked lane by lane).
 template <int K>
@@ -517,9 +513,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     __shared__ uint32_t queue[NW][QMAX];     // chunk queues; escape staging of the epilogue
     __shared__ uint32_t wrapped, ecnt, ebase, nent;
     __shared__ unsigned long long hsum;
-#if KMH_COUNT_DYN
     __shared__ unsigned long long nextb;     // the next unclaimed tile batch
-#endif
 
     const uint32_t w = xcd_work_id();
     const int s = (int)(w % (uint32_t)S);
@@ -542,9 +536,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         ecnt = 0u;
         nent = 0u;
         hsum = 0ull;
-#if KMH_COUNT_DYN
         nextb = ta;
-#endif
     }
     __syncthreads();
     KMH_DP(0)
@@ -564,39 +556,20 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         constexpr bool EX = decltype(exact)::value;
         uint32_t ent = 0u;
         uint32_t lo_n = 0, hi_n = 0;
-#if KMH_COUNT_DYN
         // batches claimed from an LDS cursor as the waves get to them, so that the waves of the
-        // workgroup finish together (a static round robin left them waiting at the barrier);
-        // guided: a batch shrinks towards the end of the bucket (at least 4 tiles)
-        auto grab = [&](uint32_t& g) -> uint64_t {
+        // workgroup finish together (a static round robin left them waiting at the barrier: 1.90
+        // -> 1.76 ms per config-3 count launch, profiles/r03/ab/r03o_*)
+        auto grab = [&]() -> uint64_t {
             unsigned long long t = 0;
-            uint32_t gg = (uint32_t)BT;
-            if (lane == 0) {
-                if (KMH_COUNT_DYN == 2) {
-                    const unsigned long long cur = __hip_atomic_load(&nextb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const uint64_t left = cur < tb ? tb - cur : 0;
-                    const uint64_t want = (left + 2 * NW - 1) / (2 * NW);
-                    gg = (uint32_t)(want < 4 ? 4 : (want > (uint64_t)BT ? (uint64_t)BT : want));
-                }
-                t = atomicAdd(&nextb, (unsigned long long)gg);
-            }
-            g = (uint32_t)__builtin_amdgcn_readfirstlane((int)gg);
+            if (lane == 0) t = atomicAdd(&nextb, (unsigned long long)BT);
             return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)t) |
                    ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(t >> 32)) << 32);
         };
-        uint32_t gcur = BT, gnext = BT;
-        uint64_t tw = grab(gcur);
-#else
         const uint32_t gcur = BT, gnext = BT;
-        uint64_t tw = ta + (uint64_t)wave * BT;
-#endif
+        uint64_t tw = grab();
         if (tw < tb) bounds(tw, gcur, lo_n, hi_n);
         for (uint64_t tnext; tw < tb; tw = tnext) {
-#if KMH_COUNT_DYN
-            tnext = grab(gnext);
-#else
-            tnext = tw + (uint64_t)NW * BT;
-#endif
+            tnext = grab();
 #if defined(KMH_EXPERIMENTS) && defined(KMH_EXCH_CUT)
             // A/B only (counts wrong): read only the first (KMH_EXCH_CUT - 1) / KMH_EXCH_CUT of
             // every segment's chunks -- fewer bytes AND fewer LDS adds: an upper bound on what a
@@ -694,9 +667,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             __syncthreads();
             if (threadIdx.x == 0) {
                 ecnt = 0u;   // the first widening's staged escapes are dropped
-#if KMH_COUNT_DYN
                 nextb = ta;
-#endif
             }
             for (int i = threadIdx.x; i < WORDS / 4; i += kCountThreads) tbl4[i] = make_uint4(0u, 0u, 0u, 0u);
             __syncthreads();
@@ -902,10 +873,7 @@ template <int K>
 int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint64_t* d_goff,
                     const uint64_t* d_tbase, int G, uint32_t* d_out, hipStream_t s, const U4Out* enc) {
     constexpr int NBK = num_buckets<K>();
-#ifndef KMH_COUNT_U
-#define KMH_COUNT_U 6
-#endif
-    constexpr int U = KMH_COUNT_U;        // chunk loads in flight per lane (queue = 64 U)
+    constexpr int U = 6;                  // chunk loads in flight per lane (queue = 64 U; 7: no gain, r03ab_u7)
     const size_t row = (size_t)1 << (2 * K);
     // Genomes per batch: the suffix buffer of one batch stays within the budget (8 GiB: 36
     // genomes of 100 Mbp at k = 12).  Measured (profiles/ab2_r02.sh, config 3): 2 / 4 / 8 GiB

@@ -48,32 +48,7 @@ constexpr int kNW = kSpThreads / 64;       // waves per workgroup
 constexpr int kSpBucketBits = 10;
 constexpr int kSpBuckets = 1 << kSpBucketBits;
 constexpr int kQueue = 512;                // per-wave chunk queue of the split kernel
-#ifndef KMH_SP_SPLIT_ORDER
-#define KMH_SP_SPLIT_ORDER 0
-#endif
-#ifndef KMH_SP_SPLIT_NT
-#define KMH_SP_SPLIT_NT 1
-#endif
-#ifndef KMH_SP_SPLIT_VDESC
-#define KMH_SP_SPLIT_VDESC 0
-#endif
-#ifndef KMH_SP_BIN_MUL
-#define KMH_SP_BIN_MUL 0
-#endif
-#ifndef KMH_SP_SPLIT_STB
-#define KMH_SP_SPLIT_STB 0
-#endif
-#ifndef KMH_SP_RESERVE_EARLY
-#define KMH_SP_RESERVE_EARLY 0
-#endif
-#ifndef KMH_SP_QU
-#define KMH_SP_QU 4
-#endif
-constexpr int kQU = KMH_SP_QU;             // chunk loads in flight per lane (split kernel)
-
-#ifndef KMH_SP_SPLIT_V4
-#define KMH_SP_SPLIT_V4 0   // split: 16-byte stores into the count items' regions (A/B)
-#endif
+constexpr int kQU = 4;                     // chunk loads in flight per lane (split kernel)
 
 // Entry width: u32 residues (k <= 21) or u64 (22 <= k <= 32).  A u64 tile holds half the windows,
 // so a tile's entries (128 KiB) and a split item's staging (80 KiB) keep their LDS size.
@@ -750,16 +725,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             }
         }
     };
-    // (KMH_SP_RESERVE_EARLY=1, A/B: the next item's histogram and reservations ahead of this item's
-    // stores, without positions.  Measured slower: split 12.3-12.6 vs 11.7 ms at config 5, the
-    // stores issued a histogram later drain less behind the next item, profiles/r04/r04k/ab)
-    constexpr bool kEarly = kPipe && KMH_SP_RESERVE_EARLY;
     uint32_t aoff[kRR];
-    if constexpr (kEarly) {   // the first item's histogram and reservations
-        histogram(cur, hc);
-        lds_barrier();
-        reserve(cur, aoff);
-    }
 #ifdef KMH_EXPERIMENTS
     unsigned long long st_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stl_ = clock64();
 #endif
@@ -772,9 +738,6 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         const bool has_nn = has_n && nnitem < xb;   // uniform
         uint32_t lo_nn = 0u, hi_nn = 0u;
         SplitItem nnn;
-#if KMH_SP_SPLIT_VDESC
-        uint32_t rawn;   // word lane % 8 of the descriptor of item nnitem + nwx (see B)
-#endif
         {   // on every path (after the last item: a copy of the current one, never used)
             uint64_t tw;
             bool single;
@@ -787,32 +750,22 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             }
             KMH_ST(0)
             bounds(nn, lo_nn, hi_nn);
-            // the descriptor two items ahead.  KMH_SP_SPLIT_VDESC (A/B): one vector load, word
-            // lane % 8 per lane (one VGPR, one cache line), read by readlane below where the wave
-            // waits for its loads anyway, since a scalar load is waited for by the histogram's
-            // barrier (lgkmcnt(0) covers LDS and scalar loads alike)
-            const uint32_t inn = has_nn && nnitem + nwx < xb ? nnitem + nwx : item;
-#if KMH_SP_SPLIT_VDESC
-            static_assert(sizeof(SplitItem) == 32, "descriptor as eight words");
-            rawn = reinterpret_cast<const uint32_t*>(items + inn)[lane & 7];
-#else
-            nnn = items[inn];
-#endif
+            // the descriptor two items ahead (a scalar load: the histogram's barrier waits for it,
+            // lgkmcnt(0) covers LDS and scalar loads alike; one vector load over lanes 0-7, read by
+            // readlane, was no faster: profiles/r04/r04m/ab/vdesc.log)
+            nnn = items[has_nn && nnitem + nwx < xb ? nnitem + nwx : item];
             KMH_ST(1)
         }
 
-        // (C) this item: pass histogram and reservations (with positions; without, they were
-        //     done one item earlier), scan, scatter
+        // (C) this item: pass histogram and reservations, scan, scatter
         const uint32_t np = cur.np;
         const bool rep = np <= (uint32_t)kRepP;   // uniform
         const uint32_t bt = split_bt(cur.per, (uint32_t)EPC);
-        if constexpr (!kEarly) {
-            histogram(cur, hc);
-            KMH_ST(2)
-            lds_barrier();
-            KMH_ST(3)
-            reserve(cur, aoff);
-        }
+        histogram(cur, hc);
+        KMH_ST(2)
+        lds_barrier();
+        KMH_ST(3)
+        reserve(cur, aoff);
         // exclusive scan of the counters (pass-major): thread t owns counters 4t .. 4t + 3 (pass p's
         // 32 replicas are counters 32p .. 32p + 31, i.e. threads 8p .. 8p + 7; without replicas
         // counter p); counters past the item's passes are zero.  (Its barrier also orders the
@@ -868,34 +821,9 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
 
         // A and B have landed by now (waited for here, not behind D's stores)
         if constexpr (kPipe) landed(hn);
-#if KMH_SP_SPLIT_VDESC
-        asm volatile("" ::"v"(lo_nn), "v"(hi_nn), "v"(rawn));
-        nnn.b = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 0);
-        nnn.t0 = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 1);
-        nnn.t1 = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 2);
-        nnn.np = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 3);
-        nnn.gb = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 4);
-        nnn.per = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 5);
-        nnn.cbase = (uint32_t)__builtin_amdgcn_readlane((int)rawn, 6);
-        nnn.pad = 0u;
-#else
         asm volatile("" ::"v"(lo_nn), "v"(hi_nn));
-#endif
         KMH_ST(7)
         hist4[tid] = make_uint4(0u, 0u, 0u, 0u);   // the cursors are dead; the next histogram follows a barrier
-
-        // the next item's histogram and reservations, ahead of this item's stores (see reserve)
-        uint32_t aoff_n[kRR];
-#pragma unroll
-        for (int r = 0; r < kRR; ++r) aoff_n[r] = 0u;
-        if constexpr (kEarly) {
-            if (has_n) {   // uniform
-                lds_barrier();   // zeroed counters visible
-                histogram(nxt, hn);
-                lds_barrier();
-                reserve(nxt, aoff_n);
-            }
-        }
 
         // (D) this item's stores: pass p's run of the staging [pst[p], pst[p + 1]) is appended to
         // count item cbase + p's region at the reserved offset; entries past the region's capacity
@@ -915,86 +843,21 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
                 const uint32_t s0 = pst[p], n = pst[p + 1] - s0;
                 const uint32_t lim = o < (uint32_t)C ? min(n, (uint32_t)C - o) : 0u;
                 const uint64_t d = (uint64_t)(cur.cbase + p) * C + o;
-#if KMH_SP_SPLIT_V4
-                // 16-byte stores on the region's 16-byte boundaries (the run's first and last few
-                // entries one by one); the staging side is read at whatever alignment the run has
-                // there (a uniform choice per pass)
-                {
-                    const uint32_t mis = (uint32_t)(d % (uint64_t)EPC);
-                    const uint32_t head = min(((uint32_t)EPC - mis) % (uint32_t)EPC, lim);
-                    const uint32_t nb = (lim - head) / (uint32_t)EPC, tb = head + nb * (uint32_t)EPC;
-                    if ((uint32_t)lane < head) __builtin_nontemporal_store(sorted[s0 + lane], out + d + lane);
-                    const uint32_t qs = s0 + head;
-                    uint4* dst4 = reinterpret_cast<uint4*>(out + d + head);
-                    if (qs % (uint32_t)EPC == 0u) {
-                        const uint4* src4 = reinterpret_cast<const uint4*>(sorted) + qs / (uint32_t)EPC;
-                        for (uint32_t c = (uint32_t)lane; c < nb; c += 64u) store_nt(dst4 + c, src4[c]);
-                    } else if (sizeof(E) == 4 && (qs & 1u) == 0u) {
-                        const uint2* src2 = reinterpret_cast<const uint2*>(sorted) + qs / 2u;
-                        for (uint32_t c = (uint32_t)lane; c < nb; c += 64u) {
-                            const uint2 a = src2[2u * c], b = src2[2u * c + 1u];
-                            store_nt(dst4 + c, make_uint4(a.x, a.y, b.x, b.y));
-                        }
-                    } else {
-                        const uint32_t* src1 = reinterpret_cast<const uint32_t*>(sorted + qs);
-                        for (uint32_t c = (uint32_t)lane; c < nb; c += 64u)
-                            store_nt(dst4 + c, make_uint4(src1[4u * c], src1[4u * c + 1u], src1[4u * c + 2u],
-                                                          src1[4u * c + 3u]));
-                    }
-                    if ((uint32_t)lane < lim - tb)
-                        __builtin_nontemporal_store(sorted[s0 + tb + lane], out + d + tb + lane);
-                    if constexpr (POS)
-                        for (uint32_t i = (uint32_t)lane; i < lim; i += 64u)
-                            __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
-                }
-#elif KMH_SP_SPLIT_STB
-                // (A/B, not faster: 12.4 vs 12.4 ms) four staging reads in flight per lane (addresses
-                // clamped into the run), then their stores, each at the pass's base + a 32-bit offset
-                E* const ob = out + d;
-                uint32_t* const pb = POS ? opos + d : nullptr;
-                for (uint32_t i0 = 0; i0 < lim; i0 += 256u) {   // (uniform)
-                    E v[4];
-                    uint32_t vp[POS ? 4 : 1];
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const uint32_t i = i0 + 64u * (uint32_t)t + (uint32_t)lane;
-                        const uint32_t ic = i < lim ? i : lim - 1u;
-                        v[t] = sorted[s0 + ic];
-                        if constexpr (POS) vp[t] = spos[s0 + ic];
-                    }
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const uint32_t i = i0 + 64u * (uint32_t)t + (uint32_t)lane;
-                        if (i < lim) {
-                            __builtin_nontemporal_store(v[t], at_byte(ob, (uint32_t)sizeof(E) * i));
-                            if constexpr (POS) __builtin_nontemporal_store(vp[t], at_byte(pb, 4u * i));
-                        }
-                    }
-                }
-#else
+                // non-temporal: the runs are read once, by the count kernel (plain stores wrote
+                // 16.7 instead of 19.2 GB but ran 11.9 vs 11.2 ms, profiles/r04/r04n)
                 for (uint32_t i = (uint32_t)lane; i < lim; i += 64u) {
-                    if constexpr (KMH_SP_SPLIT_NT) {
-                        __builtin_nontemporal_store(sorted[s0 + i], out + d + i);
-                        if constexpr (POS) __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
-                    } else {   // (A/B) plain stores: the L2 completes the runs' partial lines
-                        out[d + i] = sorted[s0 + i];
-                        if constexpr (POS) opos[d + i] = spos[s0 + i];
-                    }
+                    __builtin_nontemporal_store(sorted[s0 + i], out + d + i);
+                    if constexpr (POS) __builtin_nontemporal_store(spos[s0 + i], opos + d + i);
                 }
-#endif
             }
         }
         KMH_ST(8)
         if (!has_n) break;
-        // with positions: the zeroed counters visible before the next histogram (without, the
-        // next scan's barrier orders this item's reads of pst and the staging before its writes)
-        if constexpr (!kEarly) lds_barrier();
+        lds_barrier();   // the zeroed counters visible before the next histogram
         KMH_ST(9)
         item = nitem;
         cur = nxt;
         if constexpr (kPipe) hc = hn;
-#pragma unroll
-        for (int r = 0; r < kRR; ++r) aoff[r] = aoff_n[r];
         nitem = nnitem;
         has_n = has_nn;
         nxt = nn;
@@ -1117,39 +980,12 @@ __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
         citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, (uint32_t)gb, n};
 }
 
-// Split items in tile order (KMH_SP_SPLIT_ORDER): key = (genome in batch, first tile, bucket).  A
-// (tile, bucket) segment is ~128 bytes at an arbitrary offset of its tile's entries, so the lines
-// at its ends hold the neighbouring buckets' segments; with the items of neighbouring buckets of
-// one tile range adjacent, an XCD's workgroups read those lines together (its L2 serves the
-// second read) instead of one item after the other bucket's items have run.
-[[maybe_unused]] __global__ __launch_bounds__(256) void k_sp_order_keys(const SplitItem* __restrict__ it, uint32_t n,
-                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= n) return;
-    const SplitItem x = it[i];
-    keys[i] = ((uint64_t)(x.gb / (uint32_t)kSpBuckets) << 44) | ((uint64_t)x.t0 << 10) | (uint64_t)x.b;
-    vals[i] = i;
-}
-[[maybe_unused]] __global__ __launch_bounds__(256) void k_sp_permute(const SplitItem* __restrict__ in, const uint32_t* __restrict__ idx,
-                                                    uint32_t n, SplitItem* __restrict__ out) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < n) out[i] = in[idx[i]];
-}
-
-// Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel).
-#ifndef KMH_SP_NT_OUT
-// Count output stores: plain since round 4.  Non-temporal stores helped in round 3 (42.9 -> 42.5 ms,
-// profiles/r03/r03c_ab_nt.txt), but with the round-4 stores (a wave's run at a scalar base) they
-// write each run's partial 128-byte lines to HBM unmerged: 55.7 GB for 48 GB of output, count
-// 16.5-16.7 ms vs 14.6 ms with plain stores, which the L2 completes into full lines (48.0 GB;
-// profiles/r04/r04n).  The split keeps non-temporal stores (KMH_SP_SPLIT_NT: plain ones wrote
-// 16.7 instead of 19.2 GB but ran 11.9 vs 11.2 ms).
-#define KMH_SP_NT_OUT 0
-#endif
+// Output stores of the count kernel (48 GB per config-5 step, never read back by the kernel): plain
+// stores, which the L2 completes into full lines (48.0 GB written).  Non-temporal ones sent each wave
+// run's partial 128-byte lines to HBM unmerged: 55.7 GB, count 16.5-16.7 vs 14.6 ms (profiles/r04/r04n).
 template <typename T>
 __device__ __forceinline__ void out_store(T* p, T v) {
-    if constexpr (KMH_SP_NT_OUT) __builtin_nontemporal_store(v, p);
-    else *p = v;
+    *p = v;
 }
 
 // Count work item: deduplication by a counting sort on 13 bits of the key.  The keys of pass p
@@ -1166,16 +1002,13 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // (its consecutive keys or bins, t = its thread) then hits 16 distinct slots of a 256-byte bank
 // row instead of 4 (a 4-way conflict unswizzled).  An aligned run of 16 slots is permuted within
 // itself, so lane-consecutive reads keep one bank per lane.  EPS = elements per slot.
-#ifndef KMH_SWZ
-#define KMH_SWZ 3
-#endif
-__device__ __forceinline__ uint32_t swz_slot(uint32_t c) { return (KMH_SWZ & 2) ? c ^ ((c >> 4) & 3u) : c; }
+__device__ __forceinline__ uint32_t swz_slot(uint32_t c) { return c ^ ((c >> 4) & 3u); }
 template <int EPS>
 __device__ __forceinline__ uint32_t swz(uint32_t a) {
-    return (KMH_SWZ & 2) ? a ^ ((((a / (uint32_t)EPS) >> 4) & 3u) * (uint32_t)EPS) : a;
+    return a ^ ((((a / (uint32_t)EPS) >> 4) & 3u) * (uint32_t)EPS);
 }
-__device__ __forceinline__ uint32_t swzh_slot(uint32_t c) { return (KMH_SWZ & 1) ? c ^ ((c >> 4) & 3u) : c; }
-__device__ __forceinline__ uint32_t swzh(uint32_t a) { return (KMH_SWZ & 1) ? a ^ (((a >> 6) & 3u) << 2) : a; }
+__device__ __forceinline__ uint32_t swzh_slot(uint32_t c) { return c ^ ((c >> 4) & 3u); }
+__device__ __forceinline__ uint32_t swzh(uint32_t a) { return a ^ (((a >> 6) & 3u) << 2); }
 
 constexpr int kBinBits = 13, kBins = 1 << kBinBits;
 constexpr int kBig = 32;        // positions: keys of a bin resolved by comparison (byte counts)
@@ -1252,8 +1085,6 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     // would overflow its field fails the item)
     const int CB = WIDE ? 64 - R : 32;
     const unsigned long long CM = (1ull << CB) - 1ull;
-    const unsigned long long RMK = (1ull << R) - 1ull;   // R <= 54
-    const int SH = R - kBinBits;                         // R >= 16
     const uint32_t cap = limit < (uint32_t)C ? limit : (uint32_t)C;
 
     const uint32_t x = blockIdx.x % 8u, nwg = gridDim.x;
@@ -1285,19 +1116,13 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     // uneven), and the field stays clear of the residue's lowest bits: a canonical code is <= its
     // reverse complement, so its last bases are constrained by its first ones (the bucket), and
     // the low 13 bits put ~7x more keys into bins of 5+ (bins >= 5 per item: 122 vs 18 in a 50 Mbp
-    // simulation; the lowest-bits version ran config 5's count at 145 ms instead of 16).
-    // KMH_SP_BIN_MUL (A/B): the top 13 bits of (r * np) mod 2^R (a 32-bit multiply).
+    // simulation; the lowest-bits version ran config 5's count at 145 ms instead of 16).  The top 13
+    // bits of (r * np) mod 2^R (a 32-bit multiply) were no faster, and bimodal run to run (r04k, r04l).
     auto bin_of = [&](E r, uint32_t np) -> uint32_t {
-        if constexpr (!KMH_SP_BIN_MUL) {
-            const int lg = np > 1u ? 32 - __builtin_clz(np - 1u) : 0;   // (scalar)
-            const int sh = R - lg - 16 > 0 ? R - lg - 16 : 0;
-            if constexpr (sizeof(E) == 4) return __builtin_amdgcn_ubfe((uint32_t)r, (uint32_t)sh, (uint32_t)kBinBits);
-            else return (uint32_t)((uint64_t)r >> sh) & (uint32_t)(kBins - 1);
-        } else if constexpr (sizeof(E) == 4) {
-            return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
-        } else {
-            return (uint32_t)((((uint64_t)r * np) & RMK) >> SH);
-        }
+        const int lg = np > 1u ? 32 - __builtin_clz(np - 1u) : 0;   // (scalar)
+        const int sh = R - lg - 16 > 0 ? R - lg - 16 : 0;
+        if constexpr (sizeof(E) == 4) return __builtin_amdgcn_ubfe((uint32_t)r, (uint32_t)sh, (uint32_t)kBinBits);
+        else return (uint32_t)((uint64_t)r >> sh) & (uint32_t)(kBins - 1);
     };
 
     // An item as loaded: its descriptor, the gb_fail flag of its bucket (a pass of a bucket whose
@@ -2090,10 +1915,8 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         if (tiles == 0) continue;
         GenomeMap m{d_goff, d_tbase, g0, g1, L.tbase[g0], L.goff[G]};
         time_begin(ctx, s, "k_sp_partition");
-        // persistent partition: one workgroup per CU (KMH_SP_PART_GRID = 0: one per tile, the
-        // launch of rounds 1-2, kept for A/B runs)
-        const long pg = env_long("KMH_SP_PART_GRID", std::max(1, ctx->num_cu));
-        const unsigned pgrid = (unsigned)std::min<uint64_t>(tiles, pg > 0 ? (uint64_t)pg : tiles);
+        // persistent partition: one workgroup per CU
+        const unsigned pgrid = (unsigned)std::min<uint64_t>(tiles, (uint64_t)std::max(1, ctx->num_cu));
         launch_partition_k<E, POS>(k, canonical, (unsigned)tiles, pgrid, s, d_seq, m, ent, epos, toff, ldt);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
@@ -2138,9 +1961,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
         const size_t fb = ((nci + 1) * 4 + 255) & ~(size_t)255;
-        // (KMH_SP_SPLIT_ORDER) the items in tile order: sort keys and values (2 x 12 B) + the copy
-        const size_t okb = KMH_SP_SPLIT_ORDER ? ((nsi * 24 + 255) & ~(size_t)255) + sib : 0;
-        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb + okb);
+        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb);
         if (rc) return rc;
         char* base = static_cast<char*>(ctx->sparse[1].ptr);
         SplitItem* d_sitems = reinterpret_cast<SplitItem*>(base);
@@ -2150,32 +1971,11 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         hipLaunchKernelGGL(k_sp_fill, dim3((unsigned)ngb), dim3(64), 0, s, d_nb, d_tbase, g0, L.tbase[g0],
                            target, split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_sitems, d_citems);
         KMH_HIP(ctx, hipGetLastError());
-        if constexpr (KMH_SP_SPLIT_ORDER) {
-            char* ob2 = base + sib + cib + ob + fb;
-            uint64_t* ka = reinterpret_cast<uint64_t*>(ob2);
-            uint64_t* kb = ka + nsi;
-            uint32_t* va = reinterpret_cast<uint32_t*>(kb + nsi);
-            uint32_t* vb = va + nsi;
-            SplitItem* d_sorted_items = reinterpret_cast<SplitItem*>(ob2 + ((nsi * 24 + 255) & ~(size_t)255));
-            const unsigned og = (unsigned)((nsi + 255) / 256);
-            hipLaunchKernelGGL(k_sp_order_keys, dim3(og), dim3(256), 0, s, d_sitems, (uint32_t)nsi, ka, va);
-            KMH_HIP(ctx, hipGetLastError());
-            bool alt = false;
-            int hb = 44 + 1;
-            while (hb < 64 && ((uint64_t)nG >> (hb - 44)) != 0) ++hb;
-            rc = radix_sort_pairs<uint64_t>(ctx, ka, kb, va, vb, nsi, 0, hb, &alt, s);
-            if (rc) return rc;
-            hipLaunchKernelGGL(k_sp_permute, dim3(og), dim3(256), 0, s, d_sitems, alt ? vb : va, (uint32_t)nsi,
-                               d_sorted_items);
-            KMH_HIP(ctx, hipGetLastError());
-            d_sitems = d_sorted_items;
-        }
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         time_begin(ctx, s, "k_sp_split");
-        // persistent split: one workgroup per CU (KMH_SP_SPLIT_GRID = 0: one per item)
-        const long sg = env_long("KMH_SP_SPLIT_GRID", std::max(1, ctx->num_cu));
-        const unsigned sgrid = (unsigned)std::min<uint64_t>(nsi, sg > 0 ? (uint64_t)sg : nsi);
+        // persistent split: one workgroup per CU
+        const unsigned sgrid = (unsigned)std::min<uint64_t>(nsi, (uint64_t)std::max(1, ctx->num_cu));
         hipLaunchKernelGGL((k_sp_split<E, POS>), dim3(sgrid), dim3(kSpThreads), 0, s, ent, epos, toff, ldt,
                            d_sitems, (uint32_t)nsi, R, d_split, d_spos, d_pfill, d_gbfail);
         time_end(ctx, s);
