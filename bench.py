@@ -390,8 +390,8 @@ def main():
         e1 = torch.cuda.Event(enable_timing=True) if record else None
         if record:
             e0.record(stream)
-        if g_local and u4 is not None:
-            ctx.count_dense_u4_dev(d_seq.data_ptr(), offsets, k, buf.data_ptr(), *u4, s)
+        if g_local and u4 is not None:   # buf is scratch here (kmh_count_dense_u4only_dev)
+            ctx.count_dense_u4_dev(d_seq.data_ptr(), offsets, k, buf.data_ptr(), *u4, s, rows=False)
         elif g_local:
             ctx.count_dense_dev(d_seq.data_ptr(), offsets, k, buf.data_ptr(), s)
         if record:
@@ -562,6 +562,9 @@ def main():
         gather_ms = float(t[2]) if gather_ms is not None else None
 
     # sanity: every row sums to the number of valid windows (all-ACGT genomes)
+    if mode == "u4" and g_local and not a.separate_encode:
+        count_into(local, False)   # the fused u4-only count keeps no rows: this rank's own, untimed
+        torch.cuda.synchronize()
     last = locals_[(a.steps - 1) % len(locals_)]
     if mode in ("u4-dense", "u8"):
         full = fulls[(a.steps - 1) % 2]
@@ -686,6 +689,15 @@ def main():
             out["simulated_ranks"] = sim
             out["simulated_copies"] = a.sim_copy
             out["projected_value_at_n"] = G * L / (elapsed / a.steps)
+            # what the projection assumes of the wire: each rank receives the other N - 1 slots
+            # once per step, hidden behind its next count, i.e. at least this rate per GPU
+            # sustained over xGMI (against 7 links x XGMI_LINK_GBS)
+            recv_b = (sim - 1) * P
+            out["projected_xgmi"] = {"received_bytes_per_rank_per_step": recv_b,
+                                     "required_GBs_per_gpu": round(recv_b / (ms * 1e-3) / 1e9, 1),
+                                     "count_phase_ms": round(count_ms, 4),
+                                     "required_GBs_over_count_phase": round(recv_b / (count_ms * 1e-3) / 1e9, 1),
+                                     "frac_of_7_links": round(recv_b / (ms * 1e-3) / 1e9 / (7 * XGMI_LINK_GBS), 4)}
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)

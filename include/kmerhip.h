@@ -230,6 +230,14 @@ int kmh_rows_encode_u4_dev(kmh_ctx* ctx, const uint32_t* d_rows, uint64_t rows, 
 int kmh_count_dense_u4_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                            uint32_t* d_matrix, uint8_t* d_u4, uint32_t* d_esc, uint32_t cap,
                            uint32_t* d_esc_n, void* stream);
+/* The same u4 slot without the u32 rows: d_scratch (G x 4^k u32, device) is working memory
+ * for the rare buckets whose encoding is redone from rows (a count past 65535, or more escapes
+ * than the kernel stages), and its contents are unspecified afterwards.  For k >= 10 this is
+ * the multi-GPU step's count (bench.py, kmerml.kmers.matrix): 4^k x 4 bytes less written per
+ * genome.  Replaces the same reference code as kmh_count_dense_u4_dev. */
+int kmh_count_dense_u4only_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                               uint32_t* d_scratch, uint8_t* d_u4, uint32_t* d_esc, uint32_t cap,
+                               uint32_t* d_esc_n, void* stream);
 /* Widen one block of u4 rows (rows x cols) to u32 at d_rows and apply its escapes (pairs with an
  * index outside the block are ignored: a slot that came off the wire never writes elsewhere). */
 int kmh_rows_decode_u4_dev(kmh_ctx* ctx, const uint8_t* d_u4, uint64_t rows, uint64_t cols,

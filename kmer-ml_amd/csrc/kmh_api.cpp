@@ -398,8 +398,18 @@ int kmh_count_dense_u4_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* o
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
-        return kmh::dense_count_u4(ctx, d_seq, offsets, G, k, d_matrix, d_u4, d_esc, cap, d_esc_n,
-                               s);
+        return kmh::dense_count_u4(ctx, d_seq, offsets, G, k, d_matrix, d_u4, d_esc, cap, d_esc_n, 1, s);
+    });
+}
+
+int kmh_count_dense_u4only_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                               uint32_t* d_scratch, uint8_t* d_u4, uint32_t* d_esc, uint32_t cap,
+                               uint32_t* d_esc_n, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::dense_count_u4(ctx, d_seq, offsets, G, k, d_scratch, d_u4, d_esc, cap, d_esc_n, 0, s);
     });
 }
 

@@ -421,13 +421,16 @@ __device__ __forceinline__ void log_wrap(const FixLog& L, uint64_t row0, uint32_
 // rows_encode_u4 -- nibbles of row g at byte g * 4^k / 2 (element 2i in the low nibble of
 // byte i), every count >= 15 as an exact (g * 4^k + column, value) pair behind *esc_n.  A
 // bucket whose u16 table wrapped is left to k_reencode (listed in redo), which encodes it
-// from the corrected u32 row after k_fixup.
+// from the corrected u32 row after k_fixup.  rows = 0 (kmh_count_dense_u4only_dev, the
+// multi-GPU step): the u32 row slices are written only for the buckets k_reencode reads
+// (a wrapped table, or escapes past the LDS staging), 67 MB less per 100 Mbp genome at k = 12.
 struct U4Out {
     uint32_t* nib;       // u4 block as u32 words (8 counts each)
     uint32_t* esc;       // (index, value) pairs
     uint32_t cap;
     uint32_t* esc_n;
     uint32_t* redo;      // redo[0] = buckets listed; redo[1 + i] = g * NBK + b
+    int rows;            // 1: every row slice written; 0: only those of listed buckets
 };
 
 __device__ __forceinline__ uint32_t sat4(uint32_t x) { return x < 15u ? x : 15u; }
@@ -688,6 +691,9 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         // only): also the slice's u4 nibbles (one u32 of 8 counts per thread and step) and its
         // escapes, staged in the LDS of the queues and appended behind one global atomic.
         enc = ENC && wrapped == 0u;                                // uniform
+        // the u32 slice: always without ENC; with ENC unless rows = 0 (then only a wrapped
+        // table's, which k_reencode encodes after k_fixup has corrected it)
+        const bool wrows = !ENC || E.rows != 0 || exact;           // uniform
         uint32_t* orow = out + row0;
         uint32_t hs = 0u;
         for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
@@ -695,8 +701,10 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
             const uint4 lo4 = make_uint4(x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16);
             const uint4 hi4 = make_uint4(x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16);
             if (S == 1) {
-                store_nt(reinterpret_cast<uint4*>(orow) + 2 * i, lo4);
-                store_nt(reinterpret_cast<uint4*>(orow) + 2 * i + 1, hi4);
+                if (wrows) {
+                    store_nt(reinterpret_cast<uint4*>(orow) + 2 * i, lo4);
+                    store_nt(reinterpret_cast<uint4*>(orow) + 2 * i + 1, hi4);
+                }
                 if (post && !exact) hs += halves(x);
                 if (enc) {
                     const uint32_t e[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
@@ -747,6 +755,14 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         if (!enc && threadIdx.x == 0) {                            // k_reencode redoes this bucket
             const uint32_t at = atomicAdd(E.redo, 1u);
             E.redo[1 + at] = (uint32_t)g * NBK + b;
+        }
+        if (!enc && !E.rows && !exact) {   // escapes past the staging: k_reencode reads the row slice,
+            uint32_t* orow = out + row0;   // which the widening skipped (the table is still exact)
+            for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
+                const uint4 x = tbl4[i];
+                store_nt(reinterpret_cast<uint4*>(orow) + 2 * i, make_uint4(x.x & 0xFFFFu, x.x >> 16, x.y & 0xFFFFu, x.y >> 16));
+                store_nt(reinterpret_cast<uint4*>(orow) + 2 * i + 1, make_uint4(x.z & 0xFFFFu, x.z >> 16, x.w & 0xFFFFu, x.w >> 16));
+            }
         }
         const uint32_t n = min(ecnt, kStage);
         if (enc && threadIdx.x == 0) ebase = n ? atomicAdd(E.esc_n, n) : 0u;
@@ -1036,7 +1052,7 @@ int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, 
 }
 
 int dense_count_u4(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, uint32_t* d_out,
-                   uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, hipStream_t s) {
+                   uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, int rows, hipStream_t s) {
     if (k < 3 || k > KMH_MAX_DENSE_K) return fail(ctx, KMH_ERR_UNSUPPORTED, "the fused u4 count needs 3 <= k <= 12");
     if (!d_seq || !d_out || !d_u4 || !d_esc_n || (cap && !d_esc)) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
     const uint64_t cols = 1ull << (2 * k);
@@ -1048,7 +1064,7 @@ int dense_count_u4(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int 
     const size_t redo_bytes = (1 + (size_t)G * (cols >> kCBits)) * sizeof(uint32_t);
     int rc = ensure(ctx, ctx->redo, redo_bytes);
     if (rc) return rc;
-    U4Out E{reinterpret_cast<uint32_t*>(d_u4), d_esc, cap, d_esc_n, static_cast<uint32_t*>(ctx->redo.ptr)};
+    U4Out E{reinterpret_cast<uint32_t*>(d_u4), d_esc, cap, d_esc_n, static_cast<uint32_t*>(ctx->redo.ptr), rows};
     KMH_HIP(ctx, hipMemsetAsync(d_esc_n, 0, sizeof(uint32_t), s));
     KMH_HIP(ctx, hipMemsetAsync(E.redo, 0, sizeof(uint32_t), s));
     switch (k) {

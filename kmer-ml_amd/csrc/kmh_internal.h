@@ -103,9 +103,10 @@ size_t env_mb(const char* name, size_t dflt);
 // ---- dense path (kmh_dense.hip) ----
 // offsets: host, G+1 entries.  d_out: G x 4^k u32.
 // dense_count plus the u4 encoding of the rows (rows_encode_u4's layout), fused into the
-// count kernel's epilogue for k >= 10.
+// count kernel's epilogue for k >= 10.  rows = 0: d_out is scratch, written only where the
+// encoding needs the u32 rows (k >= 10; k <= 9 counts every row, then encodes them).
 int dense_count_u4(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, uint32_t* d_out,
-                   uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, hipStream_t s);
+                   uint8_t* d_u4, uint32_t* d_esc, uint32_t cap, uint32_t* d_esc_n, int rows, hipStream_t s);
 int dense_count(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                 uint32_t* d_out, hipStream_t s);
 int dense_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,

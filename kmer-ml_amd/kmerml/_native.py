@@ -69,6 +69,8 @@ SIGNATURES = [
     ("kmh_rows_decode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _vp, _vp]),
     ("kmh_count_dense_u4_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp, _vp, _c.c_uint32, _vp,
                                           _vp]),
+    ("kmh_count_dense_u4only_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _vp, _vp, _vp, _c.c_uint32,
+                                              _vp, _vp]),
     ("kmh_rows_decode_u4_range_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _u64, _u64,
                                                 _vp, _vp]),
     ("kmh_rows_decode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _c.c_uint32, _vp, _c.c_int,
@@ -247,12 +249,15 @@ class Context:
                                          ctypes.c_void_p(stream) if stream else None), self._h)
 
     @_locked
-    def count_dense_u4_dev(self, d_seq, offsets, k, d_matrix, d_u4, d_esc, cap, d_esc_n, stream=None):
+    def count_dense_u4_dev(self, d_seq, offsets, k, d_matrix, d_u4, d_esc, cap, d_esc_n, stream=None,
+                           rows=True):
+        """Count + u4 slot in one pass.  rows=False (kmh_count_dense_u4only_dev): d_matrix is
+        scratch, not left holding the u32 rows."""
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
-        _check(lib().kmh_count_dense_u4_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1,
-                                            int(k), ctypes.c_void_p(d_matrix), ctypes.c_void_p(d_u4),
-                                            ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
-                                            ctypes.c_void_p(stream) if stream else None), self._h)
+        fn = lib().kmh_count_dense_u4_dev if rows else lib().kmh_count_dense_u4only_dev
+        _check(fn(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1, int(k), ctypes.c_void_p(d_matrix),
+                  ctypes.c_void_p(d_u4), ctypes.c_void_p(d_esc), int(cap), ctypes.c_void_p(d_esc_n),
+                  ctypes.c_void_p(stream) if stream else None), self._h)
 
     @_locked
     def first_dense_dev(self, d_seq, offsets, k, d_first, stream=None):

@@ -94,20 +94,22 @@ def test_dense_low_complexity(ctx, dev, oracle_lib, k):
         assert np.array_equal(rows[g], oracle_lib.count_dense(seq, k)), (k, g)
 
 
-def _u4_block(ctx, dev, genomes, k, fused):
+def _u4_block(ctx, dev, genomes, k, fused, rows=True):
     """(u32 rows, nibbles, sorted escape pairs, escape count) of count + u4 encode, either fused
-    (kmh_count_dense_u4_dev) or as two passes (kmh_count_dense_dev + kmh_rows_encode_u4_dev)."""
+    (kmh_count_dense_u4_dev; rows=False: kmh_count_dense_u4only_dev, whose rows are scratch) or as
+    two passes (kmh_count_dense_dev + kmh_rows_encode_u4_dev)."""
     buf, offs = _layout(genomes)
     d_seq = torch.from_numpy(buf.copy()).to(dev)
     G, cols = len(genomes), 1 << (2 * k)
-    cap, P = kmatrix.slot_layout_u4(G, cols)
     nib = G * cols // 2
+    cap = G * cols // 4   # room for every escape (the repeated genome's counts are all >= 15)
+    P = nib + 16 + 8 * cap
     out = torch.full((G, cols), -7, dtype=torch.int32, device=dev)
     slot = torch.zeros(P, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     if fused:
         ctx.count_dense_u4_dev(d_seq.data_ptr(), offs, k, out.data_ptr(), slot.data_ptr(),
-                               slot[nib + 16:].data_ptr(), cap, slot[nib:].data_ptr(), s)
+                               slot[nib + 16:].data_ptr(), cap, slot[nib:].data_ptr(), s, rows=rows)
     else:
         ctx.count_dense_dev(d_seq.data_ptr(), offs, k, out.data_ptr(), s)
         ctx.rows_encode_u4(out.data_ptr(), G, cols, slot.data_ptr(), slot[nib + 16:].data_ptr(), cap,
@@ -120,23 +122,33 @@ def _u4_block(ctx, dev, genomes, k, fused):
     return out.cpu().numpy().view(np.uint32), h[:nib], esc, n
 
 
-@pytest.mark.parametrize("k", [8, 10, 12])
-def test_count_dense_u4_fused(ctx, dev, oracle_lib, k):
+@pytest.mark.parametrize("k,rows", [(8, True), (10, True), (12, True), (10, False), (12, False)])
+def test_count_dense_u4_fused(ctx, dev, oracle_lib, k, rows):
     """kmh_count_dense_u4_dev writes the same rows, nibbles and escape set as count + encode,
-    on ragged random genomes, a low-complexity genome (counts > 255) and one whose u16 table
-    wraps (counts > 65535: that bucket is re-encoded from the corrected rows)."""
+    on ragged random genomes, a low-complexity genome (counts > 255), one whose u16 table
+    wraps (counts > 65535: that bucket is re-encoded from the corrected rows) and a 1 Mbp
+    segment repeated 16 times (every count >= 15: more escapes per bucket than the kernel
+    stages, so those buckets are re-encoded from rows too).  rows=False
+    (kmh_count_dense_u4only_dev, the multi-GPU step): the same slot, rows not kept."""
     rng = np.random.default_rng(500 + k)
+    rep = _rand_seq(rng, 1_000_000, alphabet=b"ACGT")
     genomes = [_rand_seq(rng, 3_000_000), np.zeros(0, np.uint8), _rand_seq(rng, 70_001),
                np.frombuffer(b"AT" * 300_000 + b"a" * 5000, np.uint8).copy(),
-               np.frombuffer(b"A" * 200_000 + b"G" + b"T" * 70_000, np.uint8).copy()]
-    r1, n1, e1, c1 = _u4_block(ctx, dev, genomes, k, fused=True)
+               np.frombuffer(b"A" * 200_000 + b"G" + b"T" * 70_000, np.uint8).copy(),
+               np.tile(rep, 16)]
+    r1, n1, e1, c1 = _u4_block(ctx, dev, genomes, k, fused=True, rows=rows)
     r2, n2, e2, c2 = _u4_block(ctx, dev, genomes, k, fused=False)
     for g, seq in enumerate(genomes):
-        assert np.array_equal(r1[g], oracle_lib.count_dense(seq, k)), g
-    assert np.array_equal(r1, r2)
+        assert np.array_equal(r2[g], oracle_lib.count_dense(seq, k)), g
+    if rows:
+        assert np.array_equal(r1, r2)
     assert np.array_equal(n1, n2)
     assert c1 == c2 and c1 > 0 and np.array_equal(e1, e2)
     assert e1[:, 1].max() > 65535
+    assert c1 <= cap
+    if k >= 10:   # the repeated genome's buckets hold more escapes than a count workgroup stages
+        per_bucket = np.bincount((e1[:, 0] >> 16).astype(np.int64))
+        assert per_bucket.max() > 3072
 
 
 @pytest.mark.parametrize("k", [10, 12])
