@@ -17,8 +17,11 @@
  *     torch tensors on the context's device) and a hipStream_t passed as void*
  *     (NULL = the HIP null stream, as everywhere in HIP; torch's default stream);
  *     they only enqueue work.
- *   - One context per (thread, device).  Calls on one context are serialised by the
- *     caller; different contexts may be used concurrently.
+ *   - The caller serialises the calls on one context (the Python mirror holds a lock);
+ *     different contexts may be used concurrently.  Threads may share a context with
+ *     different streams: a call's device work waits for the work the previous call
+ *     queued on another stream (the cached workspace is never used by two calls in
+ *     flight), so such calls run one after the other on the device.
  *   - Base alphabet: A/C/G/T in either case are bases (generate.py:41 upper()s the
  *     record, :55 keeps windows whose characters are all in "ACGT"); every other
  *     byte breaks windows.  k-mer codes are 2 bits per base, A=0 C=1 G=2 T=3, first
@@ -190,6 +193,15 @@ int kmh_synth_dev(kmh_ctx* ctx, uint8_t* d_seq, uint64_t len, uint64_t stride, i
 int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
                          int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
                          uint64_t* d_nkmers, void* stream);
+/* kmh_count_sparse_dev with every genome's rows in ascending code order (the organism rows of
+ * the column-sharded matrix, /root/reference/kmerml/ml/features.py:96-111: its columns are the
+ * sorted union of labels).  Genome g's rows are d_codes / d_counts [out_off[g], out_off[g] +
+ * d_nrows[g]); d_nrows[g] counts its distinct k-mers plus padding rows, which have count 0 and
+ * repeat a neighbouring code (codes stay non-decreasing; the padding is the k-mers that occur
+ * more than once, so a uniform genome has almost none).  Same arguments and limits otherwise. */
+int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
+                                int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
+                                uint64_t* d_nrows, void* stream);
 /* Output offsets of kmh_count_sparse_dev: out_off[g] for g = 0..G (out_off nullable);
  * returns out_off[G], the total capacity in entries. */
 uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off);

@@ -341,6 +341,17 @@ int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* off
     });
 }
 
+int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
+                                int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
+                                uint64_t* d_nrows, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::sparse_count_dev_sorted(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nrows, s);
+    });
+}
+
 uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off) {
     if (!offsets || G < 0) return 0;
     return kmh::sparse_windows(offsets, G, k, out_off);

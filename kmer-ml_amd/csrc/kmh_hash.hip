@@ -344,13 +344,13 @@ __global__ __launch_bounds__(256) void k_sp_sizes(const uint16_t* __restrict__ t
     if (threadIdx.x == 0) nb[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// Pass of residue r (R bits) in a bucket of np passes: floor(r * np / 2^R).  u32 residues
-// (R <= 32): the high half of (r << (32 - R)) * np, one 32-bit multiply; u64 (R <= 54, np <=
-// 1024): the 64-bit product fits.
+// Pass of residue r (R bits) in a bucket of np passes: floor(r * np / 2^R), the high word of
+// (r << (W - R)) * np for W-bit residues (one multiply; exact for every np <= kMaxPasses, so a
+// pass is a contiguous residue range and passes ascend with the residue).
 template <typename E>
 __device__ __forceinline__ uint32_t pass_of(E r, uint32_t np, int R) {
     if constexpr (sizeof(E) == 4) return __umulhi((uint32_t)r << (32 - R), np);
-    else return (uint32_t)(((uint64_t)r * np) >> R);
+    else return (uint32_t)__umul64hi((uint64_t)r << (64 - R), (uint64_t)np);
 }
 
 // Entry i of a 16-byte chunk (4 u32 or 2 u64 entries).
@@ -1048,13 +1048,25 @@ __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks 
 // positions, coalesced) read.  With positions (the drop-in: every k-mer's first position is the
 // minimum over its copies), positions are resolved lane-consecutively by four rounds of reads of
 // the bin's keys 0..3 (clamped) and a loop for larger bins.
-template <typename E, bool POS>
+//
+// ORD (kmh_count_sparse_sorted_dev, the column-sharded matrix): every genome's rows in code order.
+// Item i writes at item_off[i] (the keys of the genome's earlier items, in (bucket, pass) order:
+// passes ascend with the residue), so the items of a genome follow each other in code order with
+// no atomic; the bin is the top 13 bits of the key's offset in its pass (monotone in the key), a
+// bin's keys are sorted in LDS after the scatter (thread t sorts bins 16t .. 16t + 15, ~1 key
+// each), and wave w stores the positions [w C / 8, (w + 1) C / 8) in order.  The item's range
+// holds its keys; the slots past its distinct k-mers are padding (count 0, code = the pass's last
+// code, so the row stays non-decreasing).  An item with a bin of more than kBigN keys fails (the
+// sorted fallback recounts it).
+template <typename E, bool POS, bool ORD>
 __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_count(
     const E* __restrict__ split, const uint32_t* __restrict__ opos, const uint32_t* __restrict__ pfill,
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
     const uint64_t* __restrict__ out_off, uint64_t* __restrict__ codes,
     uint32_t* __restrict__ counts, uint32_t* __restrict__ firsts, unsigned long long* __restrict__ nk,
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
+    static_assert(!(POS && ORD), "code order without positions only");
+    // ORD: out_off holds the output base of every item (item_off), not of every genome
     constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E, POS>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
     constexpr int BQ = BPT / 4;   // uint4 words of a thread's bins
     constexpr bool WIDE = sizeof(E) == 8;
@@ -1118,7 +1130,12 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     // the low 13 bits put ~7x more keys into bins of 5+ (bins >= 5 per item: 122 vs 18 in a 50 Mbp
     // simulation; the lowest-bits version ran config 5's count at 145 ms instead of 16).  The top 13
     // bits of (r * np) mod 2^R (a 32-bit multiply) were no faster, and bimodal run to run (r04k, r04l).
+    // ORD: the top 13 bits of r's offset in its pass, (r * np) mod 2^R (monotone within a pass).
     auto bin_of = [&](E r, uint32_t np) -> uint32_t {
+        if constexpr (ORD) {
+            if constexpr (sizeof(E) == 4) return ((uint32_t)r << (32 - R)) * np >> (32 - kBinBits);
+            else return (uint32_t)((((uint64_t)r << (64 - R)) * (uint64_t)np) >> (64 - kBinBits));
+        }
         const int lg = np > 1u ? 32 - __builtin_clz(np - 1u) : 0;   // (scalar)
         const int sh = R - lg - 16 > 0 ? R - lg - 16 : 0;
         if constexpr (sizeof(E) == 4) return __builtin_amdgcn_ubfe((uint32_t)r, (uint32_t)sh, (uint32_t)kBinBits);
@@ -1209,7 +1226,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t nnitem = nitem + nwx;
     bool has_nn = has_n && nnitem < xb;
     Desc nn = load_desc(has_nn ? nnitem : item);
-    uint64_t obo = out_off[cur.c.g];
+    uint64_t obo = ORD ? out_off[item] : out_off[cur.c.g];
     issue_keys(cur, kr, kp, kn);
     lds_barrier();   // cleared state visible
     count_keys(cur);
@@ -1278,6 +1295,33 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 if constexpr (POS) spos[at] = kp[u];
             }
             lds_barrier();
+            if constexpr (ORD) {
+                // each bin's keys in ascending order (insertion sort in place; bins of more than
+                // BIG keys fail the item below, so a loop here runs at most BIG - 1 times)
+#pragma unroll
+                for (int q = 0; q < BQ; ++q) {
+                    const uint4 rq = h4[swzh_slot(BQ * tid + q)];
+                    const uint32_t rg[4] = {rq.x, rq.y, rq.z, rq.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t bs = rg[i] & 0xFFFFu, be = rg[i] >> 16;
+                        if (be - bs >= 2u && be - bs <= (uint32_t)BIG) {
+                            for (uint32_t x = bs + 1u; x < be; ++x) {
+                                const E key = sorted[swz<EPC>(x)];
+                                uint32_t y = x;
+                                while (y > bs) {
+                                    const E o = sorted[swz<EPC>(y - 1u)];
+                                    if (o <= key) break;
+                                    sorted[swz<EPC>(y)] = o;
+                                    --y;
+                                }
+                                sorted[swz<EPC>(y)] = key;
+                            }
+                        }
+                    }
+                }
+                lds_barrier();
+            }
         }
         KMH_PT(1)
 
@@ -1293,7 +1337,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         //    on a slot holding the key)
         const uint32_t nb = over ? 0u : nbig;
         if (nb) {
-            if (nb > (uint32_t)kMaxBig) {
+            if (ORD || nb > (uint32_t)kMaxBig) {   // (ORD: a big bin's keys would leave code order)
                 if (tid == 0) bad = 1u;
             } else {
                 for (uint32_t xb2 = 0; xb2 < nb; ++xb2) {
@@ -1426,11 +1470,12 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 if constexpr (KPL == 16) reinterpret_cast<uint2*>(nib)[tid] = make_uint2((uint32_t)nv, (uint32_t)(nv >> 32));
                 else nib[tid] = (uint32_t)nv;
                 // the storing wave of these positions: position P0 + u is stored by lane
-                // (P0 + u) % NT, i.e. wave (P0 % NT) / 64 for every u (KPL divides 64)
+                // (P0 + u) % NT, i.e. wave (P0 % NT) / 64 for every u (KPL divides 64); ORD: wave
+                // w stores the positions [w KPL 64, (w + 1) KPL 64) in order, i.e. its own threads'
                 uint32_t e = 0u;
 #pragma unroll
                 for (int u = 0; u < KPL; ++u) e += (uint32_t)(((nv >> (4 * u)) & 0xFull) != 0ull);
-                if (e) atomicAdd(&scnt[(P0 % (uint32_t)NT) / 64u], e);
+                if (e) atomicAdd(&scnt[ORD ? (uint32_t)wave : (P0 % (uint32_t)NT) / 64u], e);
             }
         } else if (!over) {
             // In phases over a group of HB positions, so that every phase's LDS reads are
@@ -1498,7 +1543,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
             for (int jj = 0; jj < KPL; ++jj) wmine += (uint32_t)__popcll(__ballot((fm >> jj) & 1u));
         }
-        if (!over && nb) {   // the hash table's keys are stored by the wave of their slot
+        if (!ORD && !over && nb) {   // the hash table's keys are stored by the wave of their slot
             uint32_t hk = 0u;
 #pragma unroll
             for (int q = 0; q < HPT; ++q) hk += (uint32_t)__popcll(__ballot((htab[q * NT + tid] & CM) != 0ull));
@@ -1521,7 +1566,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         // ahead, the flag and count of the item two ahead, the output offset of the next item
         const RawItem raw_nnn = vload_item(has_nnn ? nnnitem : item);
         const uint32_t v_skip = vload(gb_fail + nn.c.gb), v_n = vload(pfill + nn.idx);
-        const uint64_t v_obo = vload(out_off + nxt.c.g);
+        const uint64_t v_obo = vload(out_off + (ORD ? nitem : nxt.c.g));
         // the output base: one atomic per item, returning during the next item's histogram
         // (its value is first used there: an add here would wait for it)
         unsigned long long ob = 0ull;
@@ -1529,7 +1574,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (fail_item) {
                 const uint32_t at = atomicAdd(&failed[0], 1u);
                 failed[1 + at] = item;
-            } else if (used) {
+            } else if (!ORD && used) {
                 // (the address laundered through a VGPR: with a uniform address the compiler
                 // rewrites the atomic into a wave reduction whose result is waited for at once)
                 uint64_t pa = reinterpret_cast<uint64_t>(nk + cur.c.g);
@@ -1585,9 +1630,15 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 uint32_t nc[SB];   // !POS: the position's nibble (0: not emitted, else its count)
 #pragma unroll
                 for (int x = 0; x < SB; ++x) {
-                    const uint32_t i = (uint32_t)((j0 + x) * NT + tid);
-                    sk[x] = sorted[(uint32_t)((j0 + x) * NT) + stid];   // (= swz(i): NT is a multiple of 64 slots)
-                    if constexpr (!POS) nc[x] = (nib[i >> 3] >> (4u * (i & 7u))) & 0xFu;
+                    if constexpr (ORD) {   // wave w's positions in order: w KPL 64 + 64 j + lane
+                        const uint32_t i = (uint32_t)(wave * KPL * 64 + (j0 + x) * 64 + lane);
+                        sk[x] = sorted[swz<EPC>(i)];
+                        nc[x] = (nib[i >> 3] >> (4u * (i & 7u))) & 0xFu;
+                    } else {
+                        const uint32_t i = (uint32_t)((j0 + x) * NT + tid);
+                        sk[x] = sorted[(uint32_t)((j0 + x) * NT) + stid];   // (= swz(i): NT is a multiple of 64 slots)
+                        if constexpr (!POS) nc[x] = (nib[i >> 3] >> (4u * (i & 7u))) & 0xFu;
+                    }
                 }
 #pragma unroll
                 for (int x = 0; x < SB; ++x) {
@@ -1621,7 +1672,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                     run += (uint32_t)__popcll(m);
                 }
             }
-            if (nb) {
+            if (!ORD && nb) {
 #pragma unroll
                 for (int q = 0; q < HPT; ++q) {
                     const unsigned long long hs = htab[q * NT + tid];
@@ -1634,6 +1685,17 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         if constexpr (POS) firsts[o] = hmin[q * NT + tid];
                     }
                     run += (uint32_t)__popcll(m);
+                }
+            }
+            if constexpr (ORD) {
+                // padding past the item's distinct k-mers: count 0, the item's largest code (its
+                // last sorted key), so the genome's row stays non-decreasing
+                if (used < ntot) {   // (uniform)
+                    const uint64_t pad = hib | (uint64_t)sorted[swz<EPC>(ntot - 1u)];
+                    for (uint32_t i = used + (uint32_t)tid; i < ntot; i += NT) {
+                        codes[obase + i] = pad;
+                        counts[obase + i] = 0u;
+                    }
                 }
             }
         }
@@ -1720,6 +1782,90 @@ __global__ __launch_bounds__(256) void k_sp_append(const E* __restrict__ keys, c
     }
 }
 
+// ORD: output base of every count item of a batch (items in (genome, bucket, pass) order) = the
+// genome's row offset + the keys of its earlier items, and every genome's row length nk[g] (its
+// items' keys: distinct k-mers + padding).  One workgroup; gstart: scratch of a u64 per genome.
+__global__ __launch_bounds__(1024) void k_sp_item_offsets(const uint32_t* __restrict__ pfill,
+                                                          const CountItem* __restrict__ items, uint32_t nci,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          uint64_t* __restrict__ item_off,
+                                                          unsigned long long* __restrict__ gstart, int g0,
+                                                          unsigned long long* __restrict__ nk) {
+    __shared__ unsigned long long ws[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t per = (nci + 1023u) / 1024u, a = min(nci, tid * per), e = min(nci, a + per);
+    unsigned long long s = 0ull;
+    for (uint32_t i = a; i < e; ++i) s += pfill[i];
+    unsigned long long incl = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long x = __shfl_up(incl, d);
+        if ((int)lane >= d) incl += x;
+    }
+    if (lane == 63u) ws[wave] = incl;
+    __syncthreads();
+    unsigned long long pre = incl - s;
+    for (uint32_t w = 0; w < wave; ++w) pre += ws[w];
+    unsigned long long q = pre;
+    for (uint32_t i = a; i < e; ++i) {
+        const uint32_t g = items[i].g;
+        if (i == 0u || items[i - 1u].g != g) gstart[g - (uint32_t)g0] = q;
+        q += pfill[i];
+    }
+    __threadfence();
+    __syncthreads();
+    q = pre;
+    for (uint32_t i = a; i < e; ++i) {
+        const uint32_t g = items[i].g;
+        const unsigned long long gs = gstart[g - (uint32_t)g0];
+        item_off[i] = out_off[g] + (q - gs);
+        q += pfill[i];
+        if (i + 1u == nci || items[i + 1u].g != g) nk[g] = q - gs;
+    }
+}
+
+// ORD fallback, step 3: the runs of the sorted keys of one (genome, bucket)'s failed passes (keys
+// ascend, so their passes ascend too) into those passes' item ranges in order, then each range's
+// padding (count 0, the pass's largest code).  Count item of pass p: cbase + p.
+template <typename E>
+__global__ __launch_bounds__(256) void k_sp_append_ord(const E* __restrict__ keys, uint32_t m,
+                                                       const uint32_t* __restrict__ starts,
+                                                       const uint32_t* __restrict__ nruns, const uint32_t* __restrict__ pmask,
+                                                       uint32_t np, int R, uint64_t hib, uint32_t cbase,
+                                                       const uint64_t* __restrict__ item_off,
+                                                       const uint32_t* __restrict__ pfill, uint64_t* __restrict__ codes,
+                                                       uint32_t* __restrict__ counts) {
+    const uint32_t n = *nruns;
+    auto run_pass = [&](uint32_t r) { return pass_of<E>(keys[starts[r]], np, R); };
+    auto first_run = [&](uint32_t p) {   // the first run whose pass is >= p
+        uint32_t lo = 0u, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2u;
+            if (run_pass(mid) < p) lo = mid + 1u;
+            else hi = mid;
+        }
+        return lo;
+    };
+    for (uint32_t r = threadIdx.x; r < n; r += 256u) {
+        const uint32_t a = starts[r], e = r + 1u < n ? starts[r + 1u] : m;
+        const uint32_t p = run_pass(r);
+        const uint64_t o = item_off[cbase + p] + (r - first_run(p));
+        codes[o] = hib | (uint64_t)keys[a];
+        counts[o] = e - a;
+    }
+    for (uint32_t p = 0; p < np; ++p) {   // (uniform)
+        if (!((pmask[p >> 5] >> (p & 31u)) & 1u)) continue;
+        const uint32_t f = first_run(p), l = first_run(p + 1u), tot = pfill[cbase + p];
+        if (l == f || l - f >= tot) continue;
+        const uint64_t pad = hib | (uint64_t)keys[starts[l - 1u]];
+        const uint64_t base = item_off[cbase + p];
+        for (uint32_t i = l - f + threadIdx.x; i < tot; i += 256u) {
+            codes[base + i] = pad;
+            counts[base + i] = 0u;
+        }
+    }
+}
+
 void* carve(char*& p, size_t bytes) {
     void* r = p;
     p += (bytes + 255) & ~(size_t)255;
@@ -1759,11 +1905,12 @@ void launch_partition_k(int k, int canonical, unsigned tiles, unsigned grid, hip
 // one gather of all of them (passes hold disjoint keys), sort (radix_sort_pairs: with positions,
 // first by position and then stably by key, so a run's first entry holds its first position),
 // runs, append.  Hand-written kernels throughout (kmh_sort.hip).
-template <typename E, bool POS>
+// ORD: item_off / pfill / cbase place the runs in code order (k_sp_append_ord) instead of appending.
+template <typename E, bool POS, bool ORD>
 int fallback_passes(Ctx* ctx, uint32_t g, uint32_t b, const std::vector<uint32_t>& passes, uint32_t np, uint32_t n,
                     const E* ent, const uint32_t* epos, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
                     int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
-                    uint32_t* firsts, hipStream_t s) {
+                    uint32_t* firsts, const uint64_t* item_off, const uint32_t* pfill, uint32_t cbase, hipStream_t s) {
     const size_t ne = ((size_t)n * sizeof(E) + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
     const size_t mb = ((size_t)(np + 31) / 32 * 4 + 255) & ~(size_t)255;
     int rc = ensure(ctx, ctx->sparse[5], 2 * ne + 7 * n4 + mb + 1024);
@@ -1821,8 +1968,12 @@ int fallback_passes(Ctx* ctx, uint32_t g, uint32_t b, const std::vector<uint32_t
     }
     rc = run_starts<E>(ctx, keys, m, flags, ex, starts, small + 1, s);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_sp_append<E, POS>), dim3(1), dim3(256), 0, s, keys, pos, m, starts, small + 1,
-                       (uint64_t)b << R, out_off, nk + g, codes, counts, firsts);
+    if constexpr (ORD)
+        hipLaunchKernelGGL(k_sp_append_ord<E>, dim3(1), dim3(256), 0, s, keys, m, starts, small + 1, d_mask, np, R,
+                           (uint64_t)b << R, cbase, item_off, pfill, codes, counts);
+    else
+        hipLaunchKernelGGL((k_sp_append<E, POS>), dim3(1), dim3(256), 0, s, keys, pos, m, starts, small + 1,
+                           (uint64_t)b << R, out_off, nk + g, codes, counts, firsts);
     KMH_HIP(ctx, hipGetLastError());
     KMH_HIP(ctx, hipStreamSynchronize(s));
     return KMH_OK;
@@ -1843,7 +1994,7 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 
 namespace {
 
-template <typename E, bool POS>
+template <typename E, bool POS, bool ORD = false>
 int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                           int canonical, uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts,
                           uint64_t* d_nkmers, hipStream_t s) {
@@ -1961,13 +2112,19 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const size_t cib = (nci * sizeof(CountItem) + 255) & ~(size_t)255;
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
         const size_t fb = ((nci + 1) * 4 + 255) & ~(size_t)255;
-        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb);
+        // ORD: the items' output bases and a genome-start scratch
+        const size_t iob = ORD ? ((nci * 8 + 255) & ~(size_t)255) + (((size_t)nG * 8 + 255) & ~(size_t)255) : 0;
+        rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb + iob);
         if (rc) return rc;
         char* base = static_cast<char*>(ctx->sparse[1].ptr);
         SplitItem* d_sitems = reinterpret_cast<SplitItem*>(base);
         CountItem* d_citems = reinterpret_cast<CountItem*>(base + sib);
         uint64_t* d_out_off = reinterpret_cast<uint64_t*>(base + sib + cib);
         uint32_t* d_failed = reinterpret_cast<uint32_t*>(base + sib + cib + ob);
+        uint64_t* d_item_off = ORD ? reinterpret_cast<uint64_t*>(base + sib + cib + ob + fb) : nullptr;
+        unsigned long long* d_gstart =
+            ORD ? reinterpret_cast<unsigned long long*>(base + sib + cib + ob + fb + ((nci * 8 + 255) & ~(size_t)255))
+                : nullptr;
         hipLaunchKernelGGL(k_sp_fill, dim3((unsigned)ngb), dim3(64), 0, s, d_nb, d_tbase, g0, L.tbase[g0],
                            target, split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_sitems, d_citems);
         KMH_HIP(ctx, hipGetLastError());
@@ -1994,10 +2151,15 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             KMH_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_split_prof), z, sizeof(z)));
         }
 #endif
+        if constexpr (ORD) {   // every item's output base (its genome's earlier items' keys) and row lengths
+            hipLaunchKernelGGL(k_sp_item_offsets, dim3(1), dim3(1024), 0, s, d_pfill, d_citems, (uint32_t)nci,
+                               d_out_off, d_item_off, d_gstart, g0, reinterpret_cast<unsigned long long*>(d_nkmers));
+            KMH_HIP(ctx, hipGetLastError());
+        }
         time_begin(ctx, s, "k_sp_count");
         const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
-        hipLaunchKernelGGL((k_sp_count<E, POS>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_pfill,
-                           d_citems, (uint32_t)nci, R, limit, d_out_off, d_codes, d_counts, d_firsts,
+        hipLaunchKernelGGL((k_sp_count<E, POS, ORD>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_pfill,
+                           d_citems, (uint32_t)nci, R, limit, ORD ? d_item_off : d_out_off, d_codes, d_counts, d_firsts,
                            reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
@@ -2060,9 +2222,10 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             for (; j < ids.size() && citems[ids[j]].gb == it.gb; ++j) passes.push_back(citems[ids[j]].p);
             ctx->fb_passes += passes.size();
             ctx->fb_groups += 1;
-            rc = fallback_passes<E, POS>(ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt,
-                                         L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
-                                         reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts, s);
+            rc = fallback_passes<E, POS, ORD>(ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt,
+                                              L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
+                                              reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts,
+                                              d_item_off, d_pfill, ids[i] - it.p, s);
             if (rc) return rc;
             i = j;
         }
@@ -2087,6 +2250,18 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
                                                       d_nkmers, s);
     return sparse_count_dev_impl<uint64_t, false>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, nullptr,
                                                   d_nkmers, s);
+}
+
+int sparse_count_dev_sorted(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                            int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
+                            hipStream_t s) {
+    if (k < 13 || k > 32) return fail(ctx, KMH_ERR_UNSUPPORTED, "device sparse counting needs 13 <= k <= 32");
+    if (!d_seq || !d_codes || !d_counts || !d_nkmers) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    if (k <= 21)
+        return sparse_count_dev_impl<uint32_t, false, true>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts,
+                                                            nullptr, d_nkmers, s);
+    return sparse_count_dev_impl<uint64_t, false, true>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts,
+                                                        nullptr, d_nkmers, s);
 }
 
 int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, int canonical,

@@ -157,6 +157,12 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                      int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
                      hipStream_t s);
+// The same counts with every genome's rows in ascending code order: genome g's rows are
+// [out_off[g], out_off[g] + d_nkmers[g]), and the rows whose count is 0 are padding (their code
+// repeats a neighbouring code, so the codes stay non-decreasing).
+int sparse_count_dev_sorted(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
+                            int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
+                            hipStream_t s);
 // The same pipeline with every entry's window position carried along: d_firsts[i] (u32, relative
 // to the genome) = the first window start of k-mer i (the drop-in's first-occurrence order).
 int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, int canonical,

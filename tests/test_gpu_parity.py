@@ -145,7 +145,7 @@ def test_count_dense_u4_fused(ctx, dev, oracle_lib, k, rows):
     assert np.array_equal(n1, n2)
     assert c1 == c2 and c1 > 0 and np.array_equal(e1, e2)
     assert e1[:, 1].max() > 65535
-    assert c1 <= cap
+    assert e1.shape[0] == c1   # every escape fit the slot
     if k >= 10:   # the repeated genome's buckets hold more escapes than a count workgroup stages
         per_bucket = np.bincount((e1[:, 0] >> 16).astype(np.int64))
         assert per_bucket.max() > 3072
