@@ -198,10 +198,22 @@ int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* off
  * sorted union of labels).  Genome g's rows are d_codes / d_counts [out_off[g], out_off[g] +
  * d_nrows[g]); d_nrows[g] counts its distinct k-mers plus padding rows, which have count 0 and
  * repeat a neighbouring code (codes stay non-decreasing; the padding is the k-mers that occur
- * more than once, so a uniform genome has almost none).  Same arguments and limits otherwise. */
+ * more than once, so a uniform genome has almost none); d_ndistinct[g] (device) receives the
+ * distinct k-mers alone.  Same arguments and limits otherwise. */
 int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
                                 int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
-                                uint64_t* d_nrows, void* stream);
+                                uint64_t* d_nrows, uint64_t* d_ndistinct, void* stream);
+/* One rank's column shard of the organisms x k-mers matrix for sparse k (features.py:96-111:
+ * columns = the sorted union of the organisms' labels).  d_codes holds R organism rows back to
+ * back, row r = d_codes[row_off[r], row_off[r + 1]) (row_off: host, R + 1 entries), each sorted
+ * by code, every code in [lo_code, hi_code_incl] (the rows of kmh_count_sparse_sorted_dev without
+ * their padding, cut to the rank's code range).  Writes the sorted union of the codes to
+ * d_columns (room for row_off[R] - row_off[0] entries), the column index of every row entry to
+ * d_indices[row_off[0] ..] (so row_off, these indices and the rows' counts form the shard's CSR),
+ * and the union's size to *ncols (host).  1 <= R <= 4096.  Synchronises `stream`. */
+int kmh_shard_union_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R,
+                        uint64_t lo_code, uint64_t hi_code_incl, uint64_t* d_columns, int64_t* d_indices,
+                        uint64_t* ncols, void* stream);
 /* Output offsets of kmh_count_sparse_dev: out_off[g] for g = 0..G (out_off nullable);
  * returns out_off[G], the total capacity in entries. */
 uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off);

@@ -62,6 +62,7 @@ int drop(Ctx* ctx, DevBuf& b) {
     KMH_HIP(ctx, hipDeviceSynchronize());
     KMH_HIP(ctx, hipFree(b.ptr));
     if (&b == &ctx->seq) ctx->staged_ok = false;
+    if (&b == &ctx->meta) ctx->meta_cache.clear();
     b.ptr = nullptr;
     b.bytes = 0;
     return KMH_OK;
@@ -193,6 +194,7 @@ static void free_workspace(kmh_ctx* ctx) {
     ctx->pinned = nullptr;
     ctx->pinned_bytes = 0;
     ctx->staged_ok = false;
+    ctx->meta_cache.clear();
 }
 
 static uint64_t workspace_bytes(const kmh_ctx* ctx) {
@@ -343,12 +345,24 @@ int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* off
 
 int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
                                 int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
-                                uint64_t* d_nrows, void* stream) {
+                                uint64_t* d_nrows, uint64_t* d_ndistinct, void* stream) {
     if (!ctx) return KMH_ERR_INVALID;
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
-        return kmh::sparse_count_dev_sorted(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nrows, s);
+        return kmh::sparse_count_dev_sorted(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts, d_nrows,
+                                            d_ndistinct, s);
+    });
+}
+
+int kmh_shard_union_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R,
+                        uint64_t lo_code, uint64_t hi_code_incl, uint64_t* d_columns, int64_t* d_indices,
+                        uint64_t* ncols, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::shard_union(ctx, d_codes, row_off, R, lo_code, hi_code_incl, d_columns, d_indices, ncols, s);
     });
 }
 

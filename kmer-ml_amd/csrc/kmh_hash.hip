@@ -1066,7 +1066,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t* __restrict__ counts, uint32_t* __restrict__ firsts, unsigned long long* __restrict__ nk,
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
     static_assert(!(POS && ORD), "code order without positions only");
-    // ORD: out_off holds the output base of every item (item_off), not of every genome
+    // ORD: out_off holds the output base of every item (item_off), not of every genome, and nk
+    // receives every genome's distinct k-mers (its row length is written by k_sp_item_offsets)
     constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E, POS>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
     constexpr int BQ = BPT / 4;   // uint4 words of a thread's bins
     constexpr bool WIDE = sizeof(E) == 8;
@@ -1574,7 +1575,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (fail_item) {
                 const uint32_t at = atomicAdd(&failed[0], 1u);
                 failed[1 + at] = item;
-            } else if (!ORD && used) {
+            } else if (used) {   // (ORD: nk counts the distinct k-mers; the base is item_off)
                 // (the address laundered through a VGPR: with a uniform address the compiler
                 // rewrites the atomic into a wave reduction whose result is waited for at once)
                 uint64_t pa = reinterpret_cast<uint64_t>(nk + cur.c.g);
@@ -1598,7 +1599,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
         // register copy or at the scatter).
         landed_keys();
         if (tid == 0) {
-            obase = ob + obo;
+            obase = ORD ? obo : ob + obo;
             nbig = bad = 0u;
         }
         Desc nnn;
@@ -1834,8 +1835,9 @@ __global__ __launch_bounds__(256) void k_sp_append_ord(const E* __restrict__ key
                                                        uint32_t np, int R, uint64_t hib, uint32_t cbase,
                                                        const uint64_t* __restrict__ item_off,
                                                        const uint32_t* __restrict__ pfill, uint64_t* __restrict__ codes,
-                                                       uint32_t* __restrict__ counts) {
+                                                       uint32_t* __restrict__ counts, unsigned long long* __restrict__ ndist) {
     const uint32_t n = *nruns;
+    if (threadIdx.x == 0) atomicAdd(ndist, (unsigned long long)n);
     auto run_pass = [&](uint32_t r) { return pass_of<E>(keys[starts[r]], np, R); };
     auto first_run = [&](uint32_t p) {   // the first run whose pass is >= p
         uint32_t lo = 0u, hi = n;
@@ -1970,7 +1972,7 @@ int fallback_passes(Ctx* ctx, uint32_t g, uint32_t b, const std::vector<uint32_t
     if (rc) return rc;
     if constexpr (ORD)
         hipLaunchKernelGGL(k_sp_append_ord<E>, dim3(1), dim3(256), 0, s, keys, m, starts, small + 1, d_mask, np, R,
-                           (uint64_t)b << R, cbase, item_off, pfill, codes, counts);
+                           (uint64_t)b << R, cbase, item_off, pfill, codes, counts, nk + g);
     else
         hipLaunchKernelGGL((k_sp_append<E, POS>), dim3(1), dim3(256), 0, s, keys, pos, m, starts, small + 1,
                            (uint64_t)b << R, out_off, nk + g, codes, counts, firsts);
@@ -1994,10 +1996,11 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 
 namespace {
 
+// ORD: d_nkmers receives the row lengths (distinct + padding) and d_ndist the distinct k-mers.
 template <typename E, bool POS, bool ORD = false>
 int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                           int canonical, uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts,
-                          uint64_t* d_nkmers, hipStream_t s) {
+                          uint64_t* d_nkmers, hipStream_t s, uint64_t* d_ndist = nullptr) {
     constexpr int kSpTile = Sp<E, POS>::TILE, kCaps = Sp<E, POS>::CAPS;
     Layout L;
     int rc = make_layout(ctx, offsets, G, k, (uint64_t)kSpTile, L);
@@ -2010,7 +2013,9 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
     rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
     if (rc) return rc;
     KMH_HIP(ctx, hipMemsetAsync(d_nkmers, 0, (size_t)G * sizeof(uint64_t), s));
+    if (ORD) KMH_HIP(ctx, hipMemsetAsync(d_ndist, 0, (size_t)G * sizeof(uint64_t), s));
     if (L.ntiles == 0) return KMH_OK;
+    unsigned long long* const d_nk = reinterpret_cast<unsigned long long*>(ORD ? d_ndist : d_nkmers);
 
     const size_t tile_bytes = (size_t)kSpTile * sizeof(E);
     const size_t budget = env_mb("KMH_SP_BUDGET_MB", 16384) << 20;
@@ -2160,7 +2165,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
         hipLaunchKernelGGL((k_sp_count<E, POS, ORD>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_pfill,
                            d_citems, (uint32_t)nci, R, limit, ORD ? d_item_off : d_out_off, d_codes, d_counts, d_firsts,
-                           reinterpret_cast<unsigned long long*>(d_nkmers), d_gbfail, d_failed);
+                           d_nk, d_gbfail, d_failed);
         time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
 #ifdef KMH_EXPERIMENTS
@@ -2224,8 +2229,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             ctx->fb_groups += 1;
             rc = fallback_passes<E, POS, ORD>(ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt,
                                               L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
-                                              reinterpret_cast<unsigned long long*>(d_nkmers), d_codes, d_counts, d_firsts,
-                                              d_item_off, d_pfill, ids[i] - it.p, s);
+                                              d_nk, d_codes, d_counts, d_firsts, d_item_off, d_pfill, ids[i] - it.p, s);
             if (rc) return rc;
             i = j;
         }
@@ -2253,15 +2257,16 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
 }
 
 int sparse_count_dev_sorted(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
-                            int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
-                            hipStream_t s) {
+                            int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nrows,
+                            uint64_t* d_ndist, hipStream_t s) {
     if (k < 13 || k > 32) return fail(ctx, KMH_ERR_UNSUPPORTED, "device sparse counting needs 13 <= k <= 32");
-    if (!d_seq || !d_codes || !d_counts || !d_nkmers) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    if (!d_seq || !d_codes || !d_counts || !d_nrows || !d_ndist)
+        return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
     if (k <= 21)
         return sparse_count_dev_impl<uint32_t, false, true>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts,
-                                                            nullptr, d_nkmers, s);
+                                                            nullptr, d_nrows, s, d_ndist);
     return sparse_count_dev_impl<uint64_t, false, true>(ctx, d_seq, offsets, G, k, canonical, d_codes, d_counts,
-                                                        nullptr, d_nkmers, s);
+                                                        nullptr, d_nrows, s, d_ndist);
 }
 
 int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, int canonical,

@@ -40,6 +40,8 @@ struct Ctx {
     std::string err;
     // device workspace
     DevBuf seq, suf, toff, meta, out, out2, fix, redo, sparse[8], order, sort_tmp, scan_tmp, first;
+    // the (goff, tbase) layout last copied to `meta` (upload_layout skips an identical copy)
+    std::vector<uint64_t> meta_cache;
     // kmh_stage_host: bytes of the host sequence staged in `seq` (valid while staged_ok)
     uint64_t staged_n = 0;
     bool staged_ok = false;
@@ -158,16 +160,23 @@ int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, in
                      int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
                      hipStream_t s);
 // The same counts with every genome's rows in ascending code order: genome g's rows are
-// [out_off[g], out_off[g] + d_nkmers[g]), and the rows whose count is 0 are padding (their code
-// repeats a neighbouring code, so the codes stay non-decreasing).
+// [out_off[g], out_off[g] + d_nrows[g]), and the rows whose count is 0 are padding (their code
+// repeats a neighbouring code, so the codes stay non-decreasing); d_ndist[g] = distinct k-mers.
 int sparse_count_dev_sorted(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
-                            int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
-                            hipStream_t s);
+                            int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nrows,
+                            uint64_t* d_ndist, hipStream_t s);
 // The same pipeline with every entry's window position carried along: d_firsts[i] (u32, relative
 // to the genome) = the first window start of k-mer i (the drop-in's first-occurrence order).
 int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k, int canonical,
                            uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts, uint64_t* d_nkmers,
                            hipStream_t s);
+
+// ---- column shard of the sparse matrix (kmh_shard.hip) ----
+// R sorted organism rows of codes in [lo, hi_incl], rows back to back: row r is d_codes[row_off[r],
+// row_off[r + 1]) (host offsets).  d_columns (>= the entries) receives the sorted union of the
+// codes, d_indices[e] (for every entry e of the rows) its column; *ncols the union's size.
+int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
+                uint64_t hi_incl, uint64_t* d_columns, int64_t* d_indices, uint64_t* ncols, hipStream_t s);
 
 // ---- feature columns of the feature CSV (kmh_features.hip) ----
 int feature_columns(Ctx* ctx, const uint64_t* d_codes, uint64_t n, int k, const int32_t* d_order, const double* d_lg,

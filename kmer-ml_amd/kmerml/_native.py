@@ -63,6 +63,9 @@ SIGNATURES = [
     ("kmh_format_lines_seq", _c.c_int64, [_c.c_int, _vp, _u64, _vp, _vp, _u64, _vp, _u64]),
     ("kmh_write_file", _c.c_int, [_c.c_char_p, _vp, _u64, _c.c_int, _c.c_int]),
     ("kmh_count_sparse_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp]),
+    ("kmh_count_sparse_sorted_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp,
+                                               _vp]),
+    ("kmh_shard_union_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _u64, _u64, _vp, _vp, _u64p, _vp]),
     ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
     ("kmh_rows_encode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
@@ -282,6 +285,31 @@ class Context:
                                           int(bool(canonical)), ctypes.c_void_p(d_codes),
                                           ctypes.c_void_p(d_counts), ctypes.c_void_p(d_nkmers),
                                           ctypes.c_void_p(stream) if stream else None), self._h)
+
+    @_locked
+    def count_sparse_sorted_dev(self, d_seq, offsets, k, canonical, d_codes, d_counts, d_nrows, d_ndistinct,
+                                stream=None):
+        """count_sparse_dev with every genome's rows in ascending code order (kmh_count_sparse_sorted_dev):
+        genome g's rows are [sparse_out_offsets(offsets, k)[g], + d_nrows[g]); rows of count 0 are
+        padding; d_ndistinct[g] = its distinct k-mers.  Synchronises the stream."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        _check(lib().kmh_count_sparse_sorted_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1, int(k),
+                                                 int(bool(canonical)), ctypes.c_void_p(d_codes),
+                                                 ctypes.c_void_p(d_counts), ctypes.c_void_p(d_nrows),
+                                                 ctypes.c_void_p(d_ndistinct),
+                                                 ctypes.c_void_p(stream) if stream else None), self._h)
+
+    @_locked
+    def shard_union_dev(self, d_codes, row_off, lo_code, hi_code_incl, d_columns, d_indices, stream=None):
+        """kmh_shard_union_dev: the sorted union of R sorted rows (row r = d_codes[row_off[r],
+        row_off[r + 1]), host offsets) into d_columns and every entry's column into d_indices;
+        returns the union's size."""
+        ro = np.ascontiguousarray(row_off, dtype=np.uint64)
+        n = ctypes.c_uint64(0)
+        _check(lib().kmh_shard_union_dev(self._h, ctypes.c_void_p(d_codes), _ptr(ro), ro.size - 1, int(lo_code),
+                                         int(hi_code_incl), ctypes.c_void_p(d_columns), ctypes.c_void_p(d_indices),
+                                         ctypes.byref(n), ctypes.c_void_p(stream) if stream else None), self._h)
+        return int(n.value)
 
     # -- matrix assembly encoding (device pointers) --
     @_locked

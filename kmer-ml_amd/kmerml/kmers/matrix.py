@@ -464,14 +464,33 @@ class ShardedSparseMatrix:
         self.rank, self.world = rank, world
 
     @property
+    def on_device(self):
+        """True when the arrays are device tensors (the GPU path: columns int64 storage of u64,
+        values int32 storage of u32); indptr is always a host int64 array."""
+        return not isinstance(self.values, np.ndarray)
+
+    @property
     def nnz(self):
-        return int(self.values.size)
+        return int(self.values.numel() if self.on_device else self.values.size)
+
+    def host(self):
+        """The same shard with numpy arrays (columns uint64, indices int64, values uint32)."""
+        if not self.on_device:
+            return self
+        return ShardedSparseMatrix(self.k, self.G, self.lo_code, self.hi_code,
+                                   self.columns.cpu().numpy().view(np.uint64), np.asarray(self.indptr, np.int64),
+                                   self.indices.cpu().numpy(), self.values.cpu().numpy().view(np.uint32),
+                                   self.rank, self.world)
+
+    def __getstate__(self):   # all_gather_object and pickling carry the host form
+        return self.host().__dict__
 
     def dense(self):
         """The shard as a dense [G, ncols] int64 array (small shards only)."""
-        out = np.zeros((self.G, self.columns.size), np.int64)
-        rows = np.repeat(np.arange(self.G), np.diff(self.indptr))
-        out[rows, self.indices] = self.values
+        h = self.host()
+        out = np.zeros((h.G, h.columns.size), np.int64)
+        rows = np.repeat(np.arange(h.G), np.diff(h.indptr))
+        out[rows, h.indices] = h.values
         return out
 
     @staticmethod
@@ -493,6 +512,7 @@ class ShardedSparseMatrix:
         import pandas as pd
 
         k = shards[0].k
+        shards = [s.host() for s in shards]
         cols = np.concatenate([s.columns for s in shards]) if shards else np.zeros(0, np.uint64)
         vals = np.concatenate([s.dense() for s in shards], axis=1) if shards else np.zeros((0, 0), np.int64)
         labels = ShardedSparseMatrix.labels(cols, k)
@@ -517,15 +537,7 @@ def _code_splitters(rows, k, world, group):
     if dist.get_backend(group) != "gloo":
         t = t.cuda()
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    cum = np.cumsum(t.cpu().numpy())
-    total = int(cum[-1]) if cum.size else 0
-    # bucket indices stay unshifted (monotone, <= nb) until the end; the last bound is the
-    # code space's end, 1 << 64 at k = 32 (a Python int: never converted to uint64)
-    idx = [0]
-    for q in range(1, world):
-        b = int(np.searchsorted(cum, total * q / world, side="left")) + 1 if total else (nb * q) // world
-        idx.append(max(idx[-1], min(b, nb)))
-    return [i << sh for i in idx] + [1 << bits]
+    return _splitters_from_hist(t.cpu().numpy(), k, world)
 
 
 def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows_fn=None):
@@ -543,6 +555,8 @@ def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows
 
     files = list(genome_files)
     G = len(files)
+    if rows_fn is None and 13 <= k <= 32:   # device-resident: sorted rows, all-to-all, kmh_shard_union_dev
+        return _sparse_matrix_dev(files, k, canonical, device, group)
     if rows_fn is None:
         lo, rows = sparse_rows(files, k, canonical=canonical, device=device, group=group)
     else:
@@ -589,6 +603,210 @@ def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows
             parts.append((glo + j, rc[pos:pos + n], rn[pos:pos + n]))
             pos += n
     return _assemble_shard(k, G, bounds[rank], bounds[rank + 1], parts, rank, world)
+
+
+def sorted_rows_dev(genome_files, k, canonical=True, device=None, group=None):
+    """This rank's block of genomes counted on the GPU with every row in code order
+    (kmh_count_sparse_sorted_dev, 13 <= k <= 32), its padding dropped: returns (lo, codes, counts,
+    roff) with codes / counts device tensors (int64 / int32 storage of u64 / u32) holding the rows
+    back to back, row i = genome lo + i = [roff[i], roff[i + 1]) (roff: host uint64)."""
+    import torch
+    import torch.distributed as dist
+
+    if not 13 <= k <= 32:
+        raise NotImplementedError("sorted device rows need 13 <= k <= 32")
+    files = list(genome_files)
+    world, rank = 1, 0
+    if dist.is_available() and dist.is_initialized():
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_bounds(len(files), world, rank)
+    if device is None:
+        device = torch.cuda.current_device()
+    dev = torch.device("cuda", device)
+    n = hi - lo
+    if n == 0:
+        return lo, torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.int32, device=dev), \
+            np.zeros(1, np.uint64)
+    buf, offsets = pack_genomes(files[lo:hi], k)
+    d_seq = torch.from_numpy(buf).to(dev) if buf.size else torch.zeros(16, dtype=torch.uint8, device=dev)
+    out_off = _native.sparse_out_offsets(offsets, k)
+    cap = max(int(out_off[-1]), 1)
+    codes = torch.empty(cap, dtype=torch.int64, device=dev)
+    counts = torch.empty(cap, dtype=torch.int32, device=dev)
+    nrows = torch.empty(n, dtype=torch.int64, device=dev)
+    ndist = torch.empty(n, dtype=torch.int64, device=dev)
+    ctx = _native.context(device)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    ctx.count_sparse_sorted_dev(d_seq.data_ptr(), offsets, k, canonical, codes.data_ptr(), counts.data_ptr(),
+                                nrows.data_ptr(), ndist.data_ptr(), s)
+    del d_seq
+    nr, nd = nrows.cpu().numpy(), ndist.cpu().numpy()
+    roff = np.zeros(n + 1, np.uint64)
+    roff[1:] = np.cumsum(nd)
+    if all(int(out_off[g]) == int(roff[g]) and nr[g] == nd[g] for g in range(n)):
+        return lo, codes, counts, roff   # back to back already, no padding: no copy
+    c2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
+    n2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int32, device=dev)
+    for g in range(n):
+        a, m, b = int(out_off[g]), int(nr[g]), int(roff[g])
+        if nr[g] == nd[g]:
+            c2[b:b + m].copy_(codes[a:a + m])
+            n2[b:b + m].copy_(counts[a:a + m])
+        else:   # padding rows (count 0) dropped
+            keep = counts[a:a + m] != 0
+            c2[b:b + int(nd[g])].copy_(codes[a:a + m][keep])
+            n2[b:b + int(nd[g])].copy_(counts[a:a + m][keep])
+    return lo, c2, n2, roff
+
+
+def _row_histogram(codes, roff, k, nbits=16):
+    """Counts of the rows' codes per top-`nbits`-bit prefix (a device searchsorted over the sorted
+    rows: no pass over the entries)."""
+    import torch
+
+    bits = 2 * k
+    sh = max(bits - nbits, 0)
+    nb = 1 << min(bits, nbits)
+    dev = codes.device
+    hist = np.zeros(nb, np.int64)
+    if codes.numel() == 0:
+        return hist
+    # signed view of u64 codes: order-preserving after flipping the top bit when k = 32
+    flip = k == 32
+    edges = torch.arange(1, nb, dtype=torch.int64, device=dev) << sh
+    if flip:
+        edges = edges ^ torch.iinfo(torch.int64).min
+    for r in range(roff.size - 1):
+        a, b = int(roff[r]), int(roff[r + 1])
+        if b == a:
+            continue
+        row = codes[a:b]
+        if flip:
+            row = row ^ torch.iinfo(torch.int64).min
+        cuts = torch.searchsorted(row, edges).cpu().numpy()
+        hist += np.diff(np.concatenate(([0], cuts, [b - a])))
+    return hist
+
+
+def _cuts(codes, a, b, bounds, k):
+    """Positions in the sorted row codes[a:b] of the code bounds (each the first entry >= bound)."""
+    import torch
+
+    row = codes[a:b]
+    e = torch.tensor([min(x, (1 << 64) - 1) for x in bounds], dtype=torch.uint64).view(torch.int64).to(codes.device)
+    if k == 32:
+        row = row ^ torch.iinfo(torch.int64).min
+        e = e ^ torch.iinfo(torch.int64).min
+    c = torch.searchsorted(row, e).cpu().numpy().astype(np.int64)
+    return c
+
+
+def _sparse_matrix_dev(files, k, canonical, device, group):
+    """sparse_matrix on the GPU: sorted device rows, an all-to-all of their code-range slices
+    (one all_to_all_single per genome index of the ranks' blocks), the shard's union and CSR
+    by kmh_shard_union_dev.  Every array stays in device memory."""
+    import torch
+    import torch.distributed as dist
+
+    G = len(files)
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    lo, codes, counts, roff = sorted_rows_dev(files, k, canonical=canonical, device=device, group=group)
+    dev = codes.device
+    n = roff.size - 1
+    if world == 1:   # one shard: every genome's row, the whole code space
+        rc, rn, indptr, lo_code, hi_code = codes, counts, roff.astype(np.int64), 0, 1 << (2 * k)
+    else:
+        hist = torch.from_numpy(_row_histogram(codes, roff, k))
+        gloo = dist.get_backend(group) == "gloo"
+        t = hist if gloo else hist.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        tot = t.cpu().numpy()
+        bounds = _splitters_from_hist(tot, k, world)
+        B = block_rows(G, world)
+        # send_len[j, q]: entries of my genome j in rank q's range
+        send_len = np.zeros((B, world), np.int64)
+        cuts = []
+        for j in range(n):
+            a, b = int(roff[j]), int(roff[j + 1])
+            c = _cuts(codes, a, b, bounds[1:-1], k) if b > a else np.zeros(world - 1, np.int64)
+            c = np.concatenate(([0], c, [b - a]))
+            cuts.append(c)
+            send_len[j] = np.diff(c)
+        lt = torch.from_numpy(send_len)
+        allt = torch.zeros((world, B, world), dtype=torch.int64)
+        if gloo:
+            dist.all_gather_into_tensor(allt, lt, group=group)
+        else:
+            g2 = torch.zeros((world, B, world), dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(g2, lt.to(dev), group=group)
+            allt = g2.cpu()
+        lens = allt.numpy()   # lens[src, j, dst]
+        # receive layout: genome-major; genome g = block of source src, index j
+        gl = np.zeros(G, np.int64)
+        for src in range(world):
+            glo, ghi = shard_bounds(G, world, src)
+            for j in range(ghi - glo):
+                gl[glo + j] = lens[src, j, rank]
+        indptr = np.zeros(G + 1, np.int64)
+        np.cumsum(gl, out=indptr[1:])
+        total = int(indptr[-1])
+        rc = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+        rn = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        for j in range(B):
+            in_splits = [int(x) for x in (send_len[j] if j < n else np.zeros(world, np.int64))]
+            out_splits = [int(lens[src, j, rank]) for src in range(world)]
+            for src_t, dst_t in ((codes, rc), (counts, rn)):
+                if j < n:
+                    a = int(roff[j])
+                    inp = src_t[a:a + sum(in_splits)]
+                else:
+                    inp = src_t[:0]
+                out = torch.empty(sum(out_splits), dtype=src_t.dtype, device=dev)
+                if gloo:
+                    ho = torch.empty(sum(out_splits), dtype=src_t.dtype)
+                    dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=group)
+                    out.copy_(ho)
+                else:
+                    dist.all_to_all_single(out, inp.contiguous(), out_splits, in_splits, group=group)
+                pos = 0
+                for src in range(world):
+                    glo, ghi = shard_bounds(G, world, src)
+                    m = out_splits[src]
+                    if j < ghi - glo and m:
+                        g = glo + j
+                        dst_t[int(indptr[g]):int(indptr[g]) + m].copy_(out[pos:pos + m])
+                    pos += m
+        del codes, counts
+        lo_code, hi_code = bounds[rank], bounds[rank + 1]
+    total = int(indptr[-1])
+    columns = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    indices = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    ncols = 0
+    if total and hi_code > lo_code:
+        ctx = _native.context(dev.index)
+        ncols = ctx.shard_union_dev(rc.data_ptr(), indptr.astype(np.uint64), lo_code, hi_code - 1,
+                                    columns.data_ptr(), indices.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    return ShardedSparseMatrix(k, G, lo_code, hi_code, columns[:ncols], indptr, indices[:total], rn[:total],
+                               rank, world)
+
+
+def _splitters_from_hist(hist, k, world):
+    """world - 1 code boundaries cutting a histogram of the codes' top bits (all ranks' rows)
+    into ~equal shares (as _code_splitters)."""
+    bits = 2 * k
+    sh = max(bits - 16, 0)
+    nb = 1 << min(bits, 16)
+    cum = np.cumsum(hist)
+    total = int(cum[-1]) if cum.size else 0
+    # bucket indices stay unshifted (monotone, <= nb) until the end; the last bound is the
+    # code space's end, 1 << 64 at k = 32 (a Python int: never converted to uint64)
+    idx = [0]
+    for q in range(1, world):
+        b = int(np.searchsorted(cum, total * q / world, side="left")) + 1 if total else (nb * q) // world
+        idx.append(max(idx[-1], min(b, nb)))
+    return [i << sh for i in idx] + [1 << bits]
 
 
 def _assemble_shard(k, G, lo_code, hi_code, parts, rank, world):

@@ -1275,3 +1275,150 @@ def test_sparse_skewed_bucket_fallback_grouped(ctx, oracle_lib, monkeypatch):
     o = np.argsort(codes, kind="stable")
     assert np.array_equal(codes[o], wc) and np.array_equal(counts[o], wn) and np.array_equal(first[o], wf)
     assert np.all(np.diff(first.astype(np.int64)) > 0)
+
+
+# ---------------------------------------------------------------- sorted rows and the column shard (config 5's matrix)
+def _sparse_sorted(ctx, dev, genomes, k, canonical):
+    """kmh_count_sparse_sorted_dev on host genomes -> per genome (codes, counts) with the padding
+    dropped, after checking the row contract: codes non-decreasing over the whole row (padding
+    included), padding = count 0, d_ndistinct = the rows of nonzero count."""
+    buf, offs = _layout(genomes)
+    d_seq = torch.from_numpy(buf.copy()).to(dev)
+    out_off = _native.sparse_out_offsets(offs, k)
+    cap = max(int(out_off[-1]), 1)
+    d_codes = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+    d_counts = torch.full((cap,), -7, dtype=torch.int32, device=dev)
+    d_nr = torch.full((len(genomes),), -1, dtype=torch.int64, device=dev)
+    d_nd = torch.full((len(genomes),), -1, dtype=torch.int64, device=dev)
+    ctx.count_sparse_sorted_dev(d_seq.data_ptr(), offs, k, canonical, d_codes.data_ptr(), d_counts.data_ptr(),
+                                d_nr.data_ptr(), d_nd.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    nr, nd = d_nr.cpu().numpy(), d_nd.cpu().numpy()
+    codes = d_codes.cpu().numpy().view(np.uint64)
+    counts = d_counts.cpu().numpy().view(np.uint32)
+    res = []
+    for g in range(len(genomes)):
+        a, n = int(out_off[g]), int(nr[g])
+        assert 0 <= nd[g] <= n <= int(out_off[g + 1]) - a, g
+        c, m = codes[a:a + n], counts[a:a + n]
+        assert np.all(c[1:] >= c[:-1]), g                  # the row in code order, padding included
+        keep = m != 0
+        assert int(keep.sum()) == int(nd[g]), g
+        assert np.all(c[keep][1:] > c[keep][:-1]), g       # distinct k-mers strictly ascending
+        res.append((c[keep], m[keep]))
+    return res
+
+
+@pytest.mark.parametrize("k,canonical", [(13, 0), (17, 1), (21, 0), (21, 1), (22, 1), (27, 0), (32, 1)])
+def test_sparse_sorted_dev_vs_oracle(ctx, dev, oracle_lib, k, canonical):
+    """kmh_count_sparse_sorted_dev (the rows of the config-5 matrix): every genome's distinct
+    k-mers and counts in code order, equal to the C oracle's sorted output, on ragged genomes
+    (lowercase, N, '-', newlines, an empty genome, genomes shorter than k)."""
+    rng = np.random.default_rng(900 + k * 2 + canonical)
+    genomes = _ragged_genomes(rng, [400_000, 32768 + 21, 1_000_003, 17])
+    got = _sparse_sorted(ctx, dev, genomes, k, canonical)
+    for g, seq in enumerate(genomes):
+        wc, wn, _ = oracle_lib.count_sparse(seq, k, canonical=bool(canonical))
+        assert np.array_equal(got[g][0], wc), g
+        assert np.array_equal(got[g][1], wn), g
+
+
+@pytest.mark.parametrize("k", [21, 27])
+def test_sparse_sorted_dev_fallback_and_repeats(ctx, dev, oracle_lib, monkeypatch, k):
+    """The sorted rows when passes fail: tables capped so that most passes go to the sort
+    fallback (whose runs land in their passes' ranges in order, padding behind them), repeats
+    whose big bins fail an item in sorted mode, one genome per batch, and low-complexity genomes."""
+    rng = np.random.default_rng(77 + k)
+    seg = osynth.synth_bases(2000, osynth.genome_seed(71))
+    parts = []
+    for i in range(30):
+        parts.append(osynth.synth_bases(int(rng.integers(500, 20_000)), osynth.genome_seed(2000 + i)))
+        parts.append(seg)
+    genomes = _ragged_genomes(rng, [600_000, 70_001]) + [
+        np.concatenate(parts), np.full(100_000, ord("A"), np.uint8),
+        np.frombuffer(b"ACGTTTGACCA" * 20_000, np.uint8).copy()]
+    want = [oracle_lib.count_sparse(s, k, canonical=True)[:2] for s in genomes]
+    for env in ({}, {"KMH_SP_TARGET": "37", "KMH_SP_LIMIT": "12288"}, {"KMH_SP_TARGET": "100000", "KMH_SP_LIMIT": "40"},
+                {"KMH_SP_BUDGET_MB": "1", "KMH_SP_LIMIT": "50"}):
+        for key in ("KMH_SP_TARGET", "KMH_SP_LIMIT", "KMH_SP_BUDGET_MB"):
+            monkeypatch.delenv(key, raising=False)
+        for key, v in env.items():
+            monkeypatch.setenv(key, v)
+        got = _sparse_sorted(ctx, dev, genomes, k, 1)
+        for g in range(len(genomes)):
+            assert np.array_equal(got[g][0], want[g][0]), (env, g)
+            assert np.array_equal(got[g][1], want[g][1]), (env, g)
+
+
+def _shard_union(ctx, dev, rows, lo, hi_incl):
+    """kmh_shard_union_dev over host rows (sorted uint64 arrays) -> (columns, indices per row)."""
+    roff = np.zeros(len(rows) + 1, np.uint64)
+    roff[1:] = np.cumsum([r.size for r in rows])
+    allc = np.concatenate(rows) if rows else np.zeros(0, np.uint64)
+    d = torch.from_numpy(np.ascontiguousarray(allc).view(np.int64).copy()).to(dev)
+    cols = torch.full((max(allc.size, 1),), -1, dtype=torch.int64, device=dev)
+    idx = torch.full((max(allc.size, 1),), -1, dtype=torch.int64, device=dev)
+    n = ctx.shard_union_dev(d.data_ptr(), roff, lo, hi_incl, cols.data_ptr(), idx.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+    c = cols[:n].cpu().numpy().view(np.uint64)
+    ix = idx.cpu().numpy()
+    return c, [ix[int(roff[r]):int(roff[r + 1])] for r in range(len(rows))]
+
+
+@pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow"])
+def test_shard_union_vs_numpy(ctx, dev, case):
+    """kmh_shard_union_dev (the column union and CSR indices of a shard) against numpy's
+    union1d / searchsorted: rows of distinct codes (the LDS path), rows sharing half their codes,
+    100 identical rows (every bin over its limit: the radix-sort fallback for every sub-range),
+    a mixture with empty rows, and a narrow code range (sub-ranges of one code)."""
+    rng = np.random.default_rng({"distinct": 1, "shared": 2, "identical": 3, "mixed": 4, "narrow": 5}[case])
+    lo, hi = 1 << 40, (1 << 41) - 1
+    if case == "distinct":
+        rows = [np.unique(rng.integers(lo, hi, 200_000, dtype=np.uint64)) for _ in range(7)]
+    elif case == "shared":
+        base = rng.integers(lo, hi, 300_000, dtype=np.uint64)
+        rows = [np.unique(np.concatenate([base[:150_000], rng.integers(lo, hi, 150_000, dtype=np.uint64)]))
+                for _ in range(5)]
+    elif case == "identical":
+        one = np.unique(rng.integers(lo, hi, 50_000, dtype=np.uint64))
+        rows = [one.copy() for _ in range(100)]
+    elif case == "mixed":
+        one = np.unique(rng.integers(lo, hi, 30_000, dtype=np.uint64))
+        rows = [np.zeros(0, np.uint64), one, np.unique(rng.integers(lo, hi, 90_000, dtype=np.uint64))] + \
+               [one.copy() for _ in range(40)] + [np.zeros(0, np.uint64)]
+    else:
+        lo, hi = 5_000_000, 5_003_999
+        rows = [np.unique(rng.integers(lo, hi + 1, 3_000, dtype=np.uint64)) for _ in range(9)]
+    cols, idx = _shard_union(ctx, dev, rows, lo, hi)
+    want = np.unique(np.concatenate(rows))
+    assert np.array_equal(cols, want)
+    for r, row in enumerate(rows):
+        assert np.array_equal(idx[r], np.searchsorted(want, row)), r
+
+
+def test_sparse_matrix_two_config5_genomes(tmp_path, ctx, dev, oracle_lib):
+    """the device-resident matrix of two full config-5 genomes (250 Mbp
+    synthetic genomes 0 and 1, k = 21 canonical): sparse_matrix's shard (sorted rows on the GPU,
+    kmh_shard_union_dev) against the C oracle's counts -- columns strictly ascending and every one
+    used, and for each genome columns[indices] = its k-mers and values = their counts."""
+    seqs = [oracle_lib.synth(250_000_000, osynth.genome_seed(g)) for g in range(2)]
+    files = []
+    for g, seq in enumerate(seqs):
+        p = tmp_path / f"SYN_{g:04d}.fa"
+        osynth.write_fasta(p, [(f"SYN_{g:04d}", seq.tobytes())], width=1 << 30)
+        files.append(str(p))
+    m = kmatrix.sparse_matrix(files, 21, canonical=True, device=0)
+    assert m.on_device and m.G == 2 and m.lo_code == 0 and m.hi_code == 1 << 42
+    cols = m.columns
+    assert bool(torch.all(cols[1:] > cols[:-1]).item())
+    used = torch.zeros(cols.numel(), dtype=torch.int32, device=cols.device)
+    used[m.indices] = 1
+    assert bool(torch.all(used == 1).item())
+    for g, seq in enumerate(seqs):
+        wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
+        a, b = int(m.indptr[g]), int(m.indptr[g + 1])
+        assert b - a == wc.size
+        got_c = cols[m.indices[a:b]].cpu().numpy().view(np.uint64)
+        assert np.array_equal(got_c, wc)
+        assert np.array_equal(m.values[a:b].cpu().numpy().view(np.uint32), wn)
+        del wc, wn
