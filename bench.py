@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--separate-encode", action="store_true",
                    help="compact u4 assembly: count, then encode in a second pass (A/B of the fused "
                         "kmh_count_dense_u4_dev)")
+    p.add_argument("--no-matrix", action="store_true",
+                   help="--workload sparse (and the config-5 object): skip the column-sharded matrix leg")
     p.add_argument("--no-config5", action="store_true",
                    help="dense N = 1: skip the config-5 measurement (16 x 250 Mbp, k = 21 canonical, "
                         "3 timed steps) that the default run appends to its JSON line as \"config5\"")
@@ -671,7 +673,7 @@ def main():
             torch.cuda.empty_cache()
             sa = argparse.Namespace(k=21, genomes=16, genome_len=250_000_000, steps=3, warmup=1,
                                     cpu_sample=0, forward=False, backend=a.backend, pmc_summary=a.pmc_summary,
-                                    cpu=cpu5)
+                                    cpu=cpu5, no_matrix=a.no_matrix)
             try:
                 out["config5"] = run_sparse(sa, 1, 0, dev, dev_index, emit=False)
             except Exception as e:   # never lose the config-3 line over the extra measurement
@@ -898,6 +900,16 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
+    if not getattr(a, "no_matrix", False) and g_local:
+        # the column-sharded matrix of these genomes, device-resident: sorted
+        # rows (kmh_count_sparse_sorted_dev), padding dropped, at N > 1 the all-to-all of code
+        # ranges, the shard's union and CSR indices (kmh_shard_union_dev); timed apart
+        del d_codes, d_counts
+        torch.cuda.empty_cache()
+        mx = matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev)
+        if rank == 0:
+            out["matrix"] = mx
+    if rank == 0:
         if not emit:
             return out
         print(json.dumps(out), flush=True)
@@ -906,6 +918,54 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
         dist.destroy_process_group()
     if not ok:
         raise SystemExit("sparse count check failed")
+
+
+def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
+    """Time the device-resident column-sharded matrix of this rank's genomes (count in code order +
+    shard) over `steps` runs after one warm-up; check the shard (columns ascending, every column
+    used, counts summing to the windows)."""
+    from kmerml.kmers.matrix import shard_from_rows, sorted_rows_from_device
+    t_rows, t_all = [], []
+    m = None
+    for i in range(steps + 1):
+        m = None
+        torch.cuda.empty_cache()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        codes, counts, roff = sorted_rows_from_device(d_seq, offsets, k, canonical)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        m = shard_from_rows(codes, counts, roff, G, k)
+        del codes, counts
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t2 = time.perf_counter()
+        if i:
+            t_rows.append((t1 - t0) * 1e3)
+            t_all.append((t2 - t0) * 1e3)
+    cols = m.columns
+    ok = bool(torch.all(cols[1:] > cols[:-1]).item()) if cols.numel() > 1 else True
+    used = torch.zeros(cols.numel(), dtype=torch.int32, device=dev)
+    used[m.indices] = 1
+    ok = ok and bool(torch.all(used == 1).item())
+    tot = int(m.values.to(torch.int64).sum().item())
+    g_local = len(offsets) - 1
+    want = g_local * (a.genome_len - k + 1) if world == 1 else None
+    ok = ok and (want is None or tot == want)
+    ms = float(np.mean(t_all))
+    if world > 1:
+        t = torch.tensor([ms, 0.0 if ok else 1.0], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms, ok = float(t[0]), float(t[1]) == 0.0
+    return {"matrix_ms": round(ms, 2), "sorted_rows_ms": round(float(np.mean(t_rows)), 2),
+            "shard_ms": round(ms - float(np.mean(t_rows)), 2), "steps": steps,
+            "what": f"this rank's {g_local} genomes -> its column shard of the organisms x k-mers matrix "
+                    "(features.py:96-111): kmh_count_sparse_sorted_dev, padding dropped, "
+                    + ("all-to-all of code ranges, " if world > 1 else "") + "kmh_shard_union_dev (columns + CSR)",
+            "ncols": int(cols.numel()), "nnz": m.nnz, "shard_checked": ok}
 
 
 if __name__ == "__main__":

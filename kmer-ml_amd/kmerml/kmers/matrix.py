@@ -623,28 +623,37 @@ def sorted_rows_dev(genome_files, k, canonical=True, device=None, group=None):
     if device is None:
         device = torch.cuda.current_device()
     dev = torch.device("cuda", device)
-    n = hi - lo
-    if n == 0:
+    if hi == lo:
         return lo, torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(0, dtype=torch.int32, device=dev), \
             np.zeros(1, np.uint64)
     buf, offsets = pack_genomes(files[lo:hi], k)
     d_seq = torch.from_numpy(buf).to(dev) if buf.size else torch.zeros(16, dtype=torch.uint8, device=dev)
+    codes, counts, roff = sorted_rows_from_device(d_seq, offsets, k, canonical)
+    return lo, codes, counts, roff
+
+
+def sorted_rows_from_device(d_seq, offsets, k, canonical=True):
+    """The sorted rows (as sorted_rows_dev) of genomes already in device memory: d_seq (uint8
+    tensor) holds them at offsets (host uint64[n + 1], 16-byte aligned starts)."""
+    import torch
+
+    dev = d_seq.device
+    n = len(offsets) - 1
     out_off = _native.sparse_out_offsets(offsets, k)
     cap = max(int(out_off[-1]), 1)
     codes = torch.empty(cap, dtype=torch.int64, device=dev)
     counts = torch.empty(cap, dtype=torch.int32, device=dev)
     nrows = torch.empty(n, dtype=torch.int64, device=dev)
     ndist = torch.empty(n, dtype=torch.int64, device=dev)
-    ctx = _native.context(device)
+    ctx = _native.context(dev.index)
     s = torch.cuda.current_stream(dev).cuda_stream
     ctx.count_sparse_sorted_dev(d_seq.data_ptr(), offsets, k, canonical, codes.data_ptr(), counts.data_ptr(),
                                 nrows.data_ptr(), ndist.data_ptr(), s)
-    del d_seq
     nr, nd = nrows.cpu().numpy(), ndist.cpu().numpy()
     roff = np.zeros(n + 1, np.uint64)
     roff[1:] = np.cumsum(nd)
     if all(int(out_off[g]) == int(roff[g]) and nr[g] == nd[g] for g in range(n)):
-        return lo, codes, counts, roff   # back to back already, no padding: no copy
+        return codes, counts, roff   # back to back already, no padding: no copy
     c2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
     n2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int32, device=dev)
     for g in range(n):
@@ -656,7 +665,7 @@ def sorted_rows_dev(genome_files, k, canonical=True, device=None, group=None):
             keep = counts[a:a + m] != 0
             c2[b:b + int(nd[g])].copy_(codes[a:a + m][keep])
             n2[b:b + int(nd[g])].copy_(counts[a:a + m][keep])
-    return lo, c2, n2, roff
+    return c2, n2, roff
 
 
 def _row_histogram(codes, roff, k, nbits=16):
@@ -702,17 +711,25 @@ def _cuts(codes, a, b, bounds, k):
 
 
 def _sparse_matrix_dev(files, k, canonical, device, group):
-    """sparse_matrix on the GPU: sorted device rows, an all-to-all of their code-range slices
-    (one all_to_all_single per genome index of the ranks' blocks), the shard's union and CSR
-    by kmh_shard_union_dev.  Every array stays in device memory."""
+    """sparse_matrix on the GPU: sorted device rows (sorted_rows_dev), then shard_from_rows."""
+    lo, codes, counts, roff = sorted_rows_dev(files, k, canonical=canonical, device=device, group=group)
+    return shard_from_rows(codes, counts, roff, len(files), k, group=group)
+
+
+def shard_from_rows(codes, counts, roff, G, k, group=None):
+    """This rank's ShardedSparseMatrix from its sorted device rows (genomes shard_bounds(G, W,
+    rank), row i = codes / counts [roff[i], roff[i + 1])): with W > 1 ranks the code space is cut
+    into W ranges of ~equal entries (an all-reduced histogram of the codes' top 16 bits, from a
+    device searchsorted of the sorted rows) and one all_to_all_single per genome index of the
+    ranks' blocks sends every row's slice of each range to its rank (RCCL over xGMI, or gloo);
+    then kmh_shard_union_dev builds the columns (sorted union) and the CSR indices on the device.
+    Every array stays in device memory; `codes` / `counts` may be consumed."""
     import torch
     import torch.distributed as dist
 
-    G = len(files)
     dist_on = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size(group) if dist_on else 1
     rank = dist.get_rank(group) if dist_on else 0
-    lo, codes, counts, roff = sorted_rows_dev(files, k, canonical=canonical, device=device, group=group)
     dev = codes.device
     n = roff.size - 1
     if world == 1:   # one shard: every genome's row, the whole code space
@@ -727,22 +744,14 @@ def _sparse_matrix_dev(files, k, canonical, device, group):
         B = block_rows(G, world)
         # send_len[j, q]: entries of my genome j in rank q's range
         send_len = np.zeros((B, world), np.int64)
-        cuts = []
         for j in range(n):
             a, b = int(roff[j]), int(roff[j + 1])
             c = _cuts(codes, a, b, bounds[1:-1], k) if b > a else np.zeros(world - 1, np.int64)
-            c = np.concatenate(([0], c, [b - a]))
-            cuts.append(c)
-            send_len[j] = np.diff(c)
-        lt = torch.from_numpy(send_len)
-        allt = torch.zeros((world, B, world), dtype=torch.int64)
-        if gloo:
-            dist.all_gather_into_tensor(allt, lt, group=group)
-        else:
-            g2 = torch.zeros((world, B, world), dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(g2, lt.to(dev), group=group)
-            allt = g2.cpu()
-        lens = allt.numpy()   # lens[src, j, dst]
+            send_len[j] = np.diff(np.concatenate(([0], c, [b - a])))
+        lt = torch.from_numpy(send_len) if gloo else torch.from_numpy(send_len).to(dev)
+        parts = [torch.zeros_like(lt) for _ in range(world)]
+        dist.all_gather(parts, lt, group=group)
+        lens = np.stack([t.cpu().numpy() for t in parts])   # lens[src, j, dst]
         # receive layout: genome-major; genome g = block of source src, index j
         gl = np.zeros(G, np.int64)
         for src in range(world):

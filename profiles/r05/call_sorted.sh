@@ -9,7 +9,10 @@ timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --t
 rc=$?
 tail -2 $out/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 -u bench.py --simulate-ranks 8 --cpu-sample 0 --steps 20 > $out/sim8_torch.log 2>&1
-rc=$?
+timeout -k 10 300 python3 -u bench.py --simulate-ranks 8 --cpu-sample 0 --steps 20 > $out/sim8_torch.log 2>&1 || exit $?
 tail -c 300 $out/sim8_torch.log
+# config 5 with the device-resident matrix leg (16 x 250 Mbp, one rank)
+timeout -k 10 300 python3 -u bench.py --workload sparse --cpu-sample 0 --steps 3 --warmup 1 > $out/sparse.log 2>&1
+rc=$?
+tail -c 600 $out/sparse.log
 exit $rc
