@@ -247,7 +247,7 @@ __device__ __forceinline__ void visit_raw(uint4 a, uint4 b, uint4 n, uint32_t tm
 // Counters the first launch of a count clears on its way (instead of one memset launch each:
 // the wrap log's cursor, the escape count, the re-encode list), nullable.
 struct Zero3 {
-    uint32_t* p[3];
+    uint32_t* p[4];
 };
 
 template <int K>
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kPThreads, 6) void k_partition(const uint8_t* __res
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t r4 = ((uint32_t)lane & 31u) << 2;   // byte offset of this lane's replica
     const uint64_t lt = xcd_work_id();
-    if (blockIdx.x == 0 && threadIdx.x < 3 && z.p[threadIdx.x]) *z.p[threadIdx.x] = 0u;
+    if (blockIdx.x == 0 && threadIdx.x < 4 && z.p[threadIdx.x]) *z.p[threadIdx.x] = 0u;
     const uint64_t gt = m.tile_lo + lt;
     const int g = find_genome(m, gt);
     const uint64_t tstart = m.goff[g] + (gt - m.tbase[g]) * (uint64_t)kPTile;
@@ -435,9 +435,10 @@ __device__ __forceinline__ void log_wrap(const FixLog& L, uint64_t row0, uint32_
 // Fused u4 encoding of the count rows (kmh_count_dense_u4_dev): the same block layout as
 // rows_encode_u4 -- nibbles of row g at byte g * 4^k / 2 (element 2i in the low nibble of
 // byte i), every count >= 15 as an exact (g * 4^k + column, value) pair behind *esc_n.  A
-// bucket whose u16 table wrapped is left to k_reencode (listed in redo), which encodes it
-// from the corrected u32 row after k_fixup.  rows = 0 (kmh_count_dense_u4only_dev, the
-// multi-GPU step): the u32 row slices are written only for the buckets k_reencode reads
+// bucket whose u16 table wrapped is listed in redo and re-encoded from the corrected u32 row by
+// the last workgroup of the last launch (after it applied the wrap log).  rows = 0
+// (kmh_count_dense_u4only_dev, the multi-GPU step): the u32 row slices are written only for the
+// buckets re-encoded from rows
 // (a wrapped table, or escapes past the LDS staging), 67 MB less per 100 Mbp genome at k = 12.
 struct U4Out {
     uint32_t* nib;       // u4 block as u32 words (8 counts each)
@@ -446,6 +447,9 @@ struct U4Out {
     uint32_t* esc_n;
     uint32_t* redo;      // redo[0] = buckets listed; redo[1 + i] = g * NBK + b
     int rows;            // 1: every row slice written; 0: only those of listed buckets
+    uint32_t* done;      // workgroups of the last launch that finished (cleared by the partition)
+    int tail;            // 1 on the last batch's launch: its last workgroup applies the wrap log
+                         // and re-encodes the listed buckets (no k_fixup / k_reencode launches)
 };
 
 __device__ __forceinline__ uint32_t sat4(uint32_t x) { return x < 15u ? x : 15u; }
@@ -662,9 +666,9 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     };
     // With one workgroup per bucket (S = 1) the row slice and its nibbles can be rewritten, so
     // the check rides on the widening's own read of the table: the first widening keeps its
-    // escapes in LDS (a bucket past the staging is left to k_reencode, which encodes it from
+    // escapes in LDS (a bucket past the staging is left to the re-encode, which encodes it from
     // the rows), and a failed check drops them, counts the bucket again exactly (the wraps
-    // make it a k_reencode bucket) and widens again.  With split rows (S > 1, added with
+    // make it a re-encoded bucket) and widens again.  With split rows (S > 1, added with
     // atomics) the table is checked before it is widened.  One call site of each walk (a
     // third inlined copy made the compiler spill to scratch).
 #if defined(KMH_EXPERIMENTS) && (defined(KMH_EXCH_CUT) || defined(KMH_EXCH_COMPACT))
@@ -707,7 +711,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
         // escapes, staged in the LDS of the queues and appended behind one global atomic.
         enc = ENC && wrapped == 0u;                                // uniform
         // the u32 slice: always without ENC; with ENC unless rows = 0 (then only a wrapped
-        // table's, which k_reencode encodes after k_fixup has corrected it)
+        // table's, which the re-encode reads after the wrap log has corrected it)
         const bool wrows = !ENC || E.rows != 0 || exact;           // uniform
         uint32_t* orow = out + row0;
         uint32_t hs = 0u;
@@ -739,7 +743,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
                                 if (at < kStage) {
                                     stage[2 * at] = idx;
                                     stage[2 * at + 1] = e[j];
-                                }   // past the staging: k_reencode encodes this bucket
+                                }   // past the staging: this bucket is re-encoded from its row
                                 ++at;
                             }
                         }
@@ -767,11 +771,11 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
     if (ENC) {
         __syncthreads();
         if (ecnt > kStage) enc = false;                            // uniform
-        if (!enc && threadIdx.x == 0) {                            // k_reencode redoes this bucket
+        if (!enc && threadIdx.x == 0) {                            // re-encoded from its row (tail)
             const uint32_t at = atomicAdd(E.redo, 1u);
             E.redo[1 + at] = (uint32_t)g * NBK + b;
         }
-        if (!enc && !E.rows && !exact) {   // escapes past the staging: k_reencode reads the row slice,
+        if (!enc && !E.rows && !exact) {   // escapes past the staging: the re-encode reads the row slice,
             uint32_t* orow = out + row0;   // which the widening skipped (the table is still exact)
             for (int i = threadIdx.x; i < (int)kCBins / 8; i += kCountThreads) {
                 const uint4 x = tbl4[i];
@@ -788,34 +792,44 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count(
                     E.esc[2 * (uint64_t)(ebase + i)] = stage[2 * i];
                     E.esc[2 * (uint64_t)(ebase + i) + 1] = stage[2 * i + 1];
                 }
-    }
-}
-
-// u4 encoding of the buckets whose u16 table wrapped (listed by k_bucket_count<ENC>), from the
-// u32 rows after k_fixup: one workgroup per listed bucket, escapes one global atomic each
-// (such buckets hold counts >= 65536: rare, and exact either way).
-template <int K>
-__global__ __launch_bounds__(256) void k_reencode(const uint32_t* __restrict__ rows, U4Out E) {
-    constexpr int NBK = num_buckets<K>();
-    const uint32_t n = E.redo[0];
-    for (uint32_t it = blockIdx.x; it < n; it += gridDim.x) {
-        const uint32_t gb = E.redo[1 + it];
-        const uint64_t row0 = (uint64_t)(gb / NBK) * (1ull << (2 * K)) + (uint64_t)(gb % NBK) * kCBins;
-        for (uint32_t i = threadIdx.x; i < kCBins / 8; i += 256) {
-            uint32_t w = 0u;
+        if (E.tail) {   // (uniform) the last workgroup to finish applies the wrap log and re-encodes
+            // a listed bucket's row slice and wrap-log entries are released before it counts in
+            // (the other workgroups wrote nothing the last one reads)
+            if (!enc) __threadfence();
+            __syncthreads();
+            if (threadIdx.x == 0) wrapped = atomicAdd(E.done, 1u) == gridDim.x - 1u ? 2u : 0u;
+            __syncthreads();
+            if (wrapped == 2u) {   // (uniform)
+                __threadfence();
+                const uint32_t nf = min(__hip_atomic_load(L.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), L.cap);
+                for (uint32_t i = threadIdx.x; i < nf; i += kCountThreads) {
+                    const unsigned long long e = L.entries[i];
+                    atomicAdd(&out[e >> 1], (e & 1ull) ? 0xFFFFFFFFu : 65536u);
+                }
+                __threadfence();
+                __syncthreads();
+                const uint32_t nr = __hip_atomic_load(E.redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (uint32_t it = 0; it < nr; ++it) {
+                    const uint32_t gb = E.redo[1 + it];
+                    const uint64_t r0 = (uint64_t)(gb / NBK) * (1ull << (2 * K)) + (uint64_t)(gb % NBK) * kCBins;
+                    for (uint32_t i = threadIdx.x; i < kCBins / 8; i += kCountThreads) {
+                        uint32_t w = 0u;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t v = rows[row0 + 8 * i + j];
-                w |= sat4(v) << (4 * j);
-                if (v >= 15u) {
-                    const uint32_t at = atomicAdd(E.esc_n, 1u);
-                    if (at < E.cap) {
-                        E.esc[2 * (uint64_t)at] = (uint32_t)(row0 + 8 * i + j);
-                        E.esc[2 * (uint64_t)at + 1] = v;
+                        for (int j = 0; j < 8; ++j) {
+                            const uint32_t v = out[r0 + 8 * i + j];
+                            w |= sat4(v) << (4 * j);
+                            if (v >= 15u) {
+                                const uint32_t at = atomicAdd(E.esc_n, 1u);
+                                if (at < E.cap) {
+                                    E.esc[2 * (uint64_t)at] = (uint32_t)(r0 + 8 * i + j);
+                                    E.esc[2 * (uint64_t)at + 1] = v;
+                                }
+                            }
+                        }
+                        E.nib[r0 / 8 + i] = w;
                     }
                 }
             }
-            E.nib[row0 / 8 + i] = w;
         }
     }
 }
@@ -946,14 +960,16 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
     fl.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
     // the counters every later kernel adds to: cleared by the first partition launch (a batch
     // without tiles comes first only if every genome of it is too short for one window)
-    Zero3 z{{fl.cursor, enc ? enc->esc_n : nullptr, enc ? enc->redo : nullptr}};
+    // (ENC: the last launch's done counter, in the wrap log's header: fl.cursor + 1)
+    uint32_t* done = fl.cursor + 1;
+    Zero3 z{{fl.cursor, enc ? enc->esc_n : nullptr, enc ? enc->redo : nullptr, done}};
     if (L.tbase[G] == L.tbase[0] || L.tbase[batch_end(0).first] == L.tbase[0]) {
-        KMH_HIP(ctx, hipMemsetAsync(fl.cursor, 0, 4, s));
+        KMH_HIP(ctx, hipMemsetAsync(fl.cursor, 0, 8, s));
         if (enc) {
             KMH_HIP(ctx, hipMemsetAsync(enc->esc_n, 0, 4, s));
             KMH_HIP(ctx, hipMemsetAsync(enc->redo, 0, 4, s));
         }
-        z = Zero3{{nullptr, nullptr, nullptr}};
+        z = Zero3{{nullptr, nullptr, nullptr, nullptr}};
     }
 
     for (int g = 0; g < G;) {
@@ -979,14 +995,19 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
             time_begin(ctx, s, "k_partition");
             hipLaunchKernelGGL(k_partition<K>, dim3((unsigned)tiles), dim3(kPThreads), 0, s, d_seq, m, suf,
                                toff, ldt, z);
-            z = Zero3{{nullptr, nullptr, nullptr}};
+            z = Zero3{{nullptr, nullptr, nullptr, nullptr}};
             time_end(ctx, s);
             KMH_HIP(ctx, hipGetLastError());
         }
         time_begin(ctx, s, "k_bucket_count");
-        if (enc)
+        if (enc) {
+            U4Out e = *enc;
+            e.done = done;
+            e.tail = h == G;   // the last batch's launch does the wrap fixes and re-encodes (only it
+                               // counts into `done`, which the first partition launch cleared)
             hipLaunchKernelGGL((k_bucket_count<K, U, true>), dim3((unsigned)(nG * NBK * S)), dim3(kCountThreads), 0,
-                               s, suf, toff, ldt, m, S, d_out, fl, *enc);
+                               s, suf, toff, ldt, m, S, d_out, fl, e);
+        }
         else
             hipLaunchKernelGGL((k_bucket_count<K, U, false>), dim3((unsigned)(nG * NBK * S)), dim3(kCountThreads), 0,
                                s, suf, toff, ldt, m, S, d_out, fl, U4Out{});
@@ -1007,12 +1028,10 @@ int run_partitioned(Ctx* ctx, const uint8_t* d_seq, const Layout& L, const uint6
 #endif
         g = h;
     }
-    time_begin(ctx, s, "k_fixup");
-    hipLaunchKernelGGL(k_fixup, dim3(64), dim3(256), 0, s, fl, d_out);
-    time_end(ctx, s);
-    KMH_HIP(ctx, hipGetLastError());
-    if (enc) {
-        hipLaunchKernelGGL(k_reencode<K>, dim3(64), dim3(256), 0, s, d_out, *enc);
+    if (!enc) {   // (the fused encode's last count workgroup applies the log and re-encodes)
+        time_begin(ctx, s, "k_fixup");
+        hipLaunchKernelGGL(k_fixup, dim3(64), dim3(256), 0, s, fl, d_out);
+        time_end(ctx, s);
         KMH_HIP(ctx, hipGetLastError());
     }
     return KMH_OK;
