@@ -750,10 +750,6 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
             }
             KMH_ST(0)
             bounds(nn, lo_nn, hi_nn);
-            // the descriptor two items ahead (a scalar load: the histogram's barrier waits for it,
-            // lgkmcnt(0) covers LDS and scalar loads alike; one vector load over lanes 0-7, read by
-            // readlane, was no faster: profiles/r04/r04m/ab/vdesc.log)
-            nnn = items[has_nn && nnitem + nwx < xb ? nnitem + nwx : item];
             KMH_ST(1)
         }
 
@@ -819,6 +815,12 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_split(
         lds_barrier();
         KMH_ST(6)
 
+        // the descriptor two items ahead, first used by the next item's bounds: a scalar load counts
+        // in lgkmcnt like the LDS operations, so every LDS barrier waits for it -- issued here, after
+        // the scatter's barrier, only the end-of-item barrier (behind the wait for A and B and the
+        // queued stores) waits for it, instead of the histogram's barrier right after it was issued
+        // (round 4: 4.7 Mcyc per wave at that barrier, profiles/r04/r04p/ab/exp0.log)
+        nnn = items[has_nn && nnitem + nwx < xb ? nnitem + nwx : item];
         // A and B have landed by now (waited for here, not behind D's stores)
         if constexpr (kPipe) landed(hn);
         asm volatile("" ::"v"(lo_nn), "v"(hi_nn));
