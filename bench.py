@@ -749,19 +749,22 @@ def run_e2e(dev, dev_index, cpu):
     import tempfile
     from kmerml.kmers import generate as kgen
     ctx = _native.context(dev_index)
-    cases = [("yeast_standin_12.16Mbp", YEAST_LENGTHS, [8, 9, 10, 11, 12]),
-             ("synthetic_100Mbp", [100_000_000], [8, 9, 10, 11, 12]),
-             ("yeast_standin_12.16Mbp", YEAST_LENGTHS, [21])]
+    # (the last case: the class default compress=True, generate.py:10,79-91 -- gzip files)
+    cases = [("yeast_standin_12.16Mbp", YEAST_LENGTHS, [8, 9, 10, 11, 12], False),
+             ("yeast_standin_12.16Mbp", YEAST_LENGTHS, [21], False),
+             ("yeast_standin_12.16Mbp", YEAST_LENGTHS, [8, 9, 10, 11, 12], True),
+             ("synthetic_100Mbp", [100_000_000], [8, 9, 10, 11, 12], False)]
     out = {"call": "KmerExtractor(output_dir, compress=False).extract_kmers_from_fasta(fasta, k_values) "
-                   "(scripts/extract_kmers.py:55-61 defaults: -k 8,9,10,11,12, no --compress)",
+                   "(scripts/extract_kmers.py:55-61 defaults: -k 8,9,10,11,12, no --compress); the case with "
+                   "compress=True is the class default (generate.py:10), gzip-compressed k{k}.txt.gz files",
            "cases": []}
     with tempfile.TemporaryDirectory() as tmp:
-        for name, lengths, ks in cases:
+        for name, lengths, ks, gz in cases:
             fa = os.path.join(tmp, f"{name}.fa")
             if not os.path.exists(fa):
                 _write_synth_fasta(ctx, dev, fa, lengths, "SYN_chr" if len(lengths) > 1 else "SYN_")
             L = sum(lengths)
-            ex = kgen.KmerExtractor(output_dir=os.path.join(tmp, "out"), compress=False)
+            ex = kgen.KmerExtractor(output_dir=os.path.join(tmp, "out"), compress=gz)
             for timed in (False, True):
                 kgen.PROFILE = {}
                 t0 = time.perf_counter()
@@ -771,13 +774,19 @@ def run_e2e(dev, dev_index, cpu):
             stages = {k: round(v, 4) for k, v in kgen.PROFILE.items()}
             kgen.PROFILE = None
             odir = os.path.join(tmp, "out", name)
-            lines = sum(sum(1 for _ in open(os.path.join(odir, f"k{k}.txt"), "rb")) for k in ks)
-            nbytes = sum(os.path.getsize(os.path.join(odir, f"k{k}.txt")) for k in ks)
+            ext = ".txt.gz" if gz else ".txt"
+            if gz:
+                import gzip
+                lines = sum(sum(1 for _ in gzip.open(os.path.join(odir, f"k{k}{ext}"), "rb")) for k in ks)
+            else:
+                lines = sum(sum(1 for _ in open(os.path.join(odir, f"k{k}{ext}"), "rb")) for k in ks)
+            nbytes = sum(os.path.getsize(os.path.join(odir, f"k{k}{ext}")) for k in ks)
             case = {"input": f"{name}: {len(lengths)} record(s), {L} bases, 80-column FASTA", "k_values": ks,
+                    "compress": gz,
                     "seconds": round(dt, 4), "bases_per_s": L / dt, "bases_x_k_per_s": L * len(ks) / dt,
                     "stages_s": stages, "lines_written": lines, "bytes_written": nbytes}
             ref = (cpu or {}).get(21 if ks == [21] else 12)
-            if ref:   # the reference's loop + writer at the rates measured on its sample
+            if ref and not gz:   # the reference's loop + writer at the rates measured on its sample
                 est = len(ks) * L / ref["value"] + lines * ref["save_seconds"] / ref["save_lines"]
                 case["reference_projection"] = {
                     "seconds": round(est, 1), "bases_per_s": L / est,
@@ -786,7 +795,7 @@ def run_e2e(dev, dev_index, cpu):
                     "speedup": round(est / dt, 1)}
             out["cases"].append(case)
             for k in ks:
-                os.remove(os.path.join(odir, f"k{k}.txt"))
+                os.remove(os.path.join(odir, f"k{k}{ext}"))
             if name.startswith("synthetic"):
                 os.remove(fa)
     return out
