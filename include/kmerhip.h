@@ -203,6 +203,13 @@ int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* off
 int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
                                 int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
                                 uint64_t* d_nrows, uint64_t* d_ndistinct, void* stream);
+/* The rows of kmh_count_sparse_sorted_dev without their padding: row r = d_codes / d_counts
+ * [src_off[r], src_off[r] + src_len[r]) is written to d_out_codes / d_out_counts from dst_off[r]
+ * on, its entries of count 0 dropped and the others kept in order (host offset arrays of R
+ * entries; dst_off[r + 1] - dst_off[r] must hold row r's nonzero entries, d_ndistinct[r]). */
+int kmh_rows_compact_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* src_off,
+                         const uint64_t* src_len, int R, uint64_t* d_out_codes, uint32_t* d_out_counts,
+                         const uint64_t* dst_off, void* stream);
 /* One rank's column shard of the organisms x k-mers matrix for sparse k (features.py:96-111:
  * columns = the sorted union of the organisms' labels).  d_codes holds R organism rows back to
  * back, row r = d_codes[row_off[r], row_off[r + 1]) (row_off: host, R + 1 entries), each sorted

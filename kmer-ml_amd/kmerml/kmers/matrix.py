@@ -656,15 +656,9 @@ def sorted_rows_from_device(d_seq, offsets, k, canonical=True):
         return codes, counts, roff   # back to back already, no padding: no copy
     c2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
     n2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int32, device=dev)
-    for g in range(n):
-        a, m, b = int(out_off[g]), int(nr[g]), int(roff[g])
-        if nr[g] == nd[g]:
-            c2[b:b + m].copy_(codes[a:a + m])
-            n2[b:b + m].copy_(counts[a:a + m])
-        else:   # padding rows (count 0) dropped
-            keep = counts[a:a + m] != 0
-            c2[b:b + int(nd[g])].copy_(codes[a:a + m][keep])
-            n2[b:b + int(nd[g])].copy_(counts[a:a + m][keep])
+    # the padding (count-0 rows) dropped on the device, rows back to back (kmh_rows_compact_dev)
+    ctx.rows_compact_dev(codes.data_ptr(), counts.data_ptr(), out_off[:n], nr.astype(np.uint64), c2.data_ptr(),
+                         n2.data_ptr(), roff[:n], s)
     return c2, n2, roff
 
 
