@@ -74,7 +74,7 @@ def parse():
                         "synthetic FASTA files, per-stage clocks) that the default run appends as \"e2e\"")
     p.add_argument("--simulate-ranks", type=int, default=0,
                    help="one process on one GPU doing what ONE rank of N does per step at config 4 "
-                        "(count G/N genomes, encode u4, and the all-gather's writes modelled as N "
+                        "(count G/N genomes, encode u4, and the all-gather's writes modelled as N - 1 "
                         "device copies of the slot; no xGMI): a projection, labelled as such")
     p.add_argument("--sim-copy", choices=("torch", "none"), default="torch",
                    help="--simulate-ranks: model the all-gather's writes by device copies (torch), or "
@@ -411,8 +411,10 @@ def main():
         payload = B * bins // 2
         local = torch.zeros((B, bins), dtype=torch.int32, device=dev)
         locals_ = [local]
-        send = [torch.zeros(P, dtype=torch.uint8, device=dev) for _ in range(2)]
         recv = [torch.zeros(span * P, dtype=torch.uint8, device=dev) for _ in range(2)]
+        # in-place all-gather (RCCL's in-place form, sendbuff = recvbuff + rank * count): the
+        # rank's own slot of recv IS its send buffer, written once by the count, never copied
+        send = [r[rank * P:(rank + 1) * P] for r in recv]
         inflight = [None, None]
         side = torch.cuda.Stream(dev) if sim else None
 
@@ -430,10 +432,10 @@ def main():
             else:   # count + u4 encode in one pass (kmh_count_dense_u4_dev)
                 count_into(local, record, u4=(sb.data_ptr(), sb[payload + 16:].data_ptr(), cap,
                                               sb[payload:].data_ptr()))
-            if sim:   # the gather's HBM side: every slot of recv written from this rank's slot
+            if sim:   # the gather's HBM side: every other slot of recv written (from this rank's)
                 side.wait_stream(stream)
                 with torch.cuda.stream(side):
-                    for q in range(span if a.sim_copy == "torch" else 0):
+                    for q in range(1, span if a.sim_copy == "torch" else 1):
                         recv[b][q * P:(q + 1) * P].copy_(sb)
                     ev = torch.cuda.Event()
                     ev.record(side)
@@ -687,7 +689,8 @@ def main():
         if sim:
             out["config"]["workload"] = (f"projection: ONE rank of config 4 at N = {sim} on one GPU (its {g_local} of "
                                          f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k}, u4 encode, the all-gather "
-                                         f"modelled as {sim} device copies of its slot; no xGMI traffic, no other ranks)")
+                                         f"modelled as {sim - 1} device copies of its slot into the others (the all-gather is in place: "
+                                         f"the count writes the rank's own slot); no xGMI traffic, no other ranks)")
             out["simulated_ranks"] = sim
             out["simulated_copies"] = a.sim_copy
             out["projected_value_at_n"] = G * L / (elapsed / a.steps)
@@ -934,16 +937,21 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
     shard) over `steps` runs after one warm-up; check the shard (columns ascending, every column
     used, counts summing to the windows)."""
     from kmerml.kmers.matrix import shard_from_rows, sorted_rows_from_device
-    t_rows, t_all = [], []
+    t_rows, t_all, phases = [], [], []
     m = None
+    # the first run is a warm-up: its torch.empty calls reach hipMalloc (~23 GB/s for these
+    # 32-48 GB buffers: 4.2 s of the first run); later runs reuse the caching allocator's blocks
     for i in range(steps + 1):
         m = None
-        torch.cuda.empty_cache()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        codes, counts, roff = sorted_rows_from_device(d_seq, offsets, k, canonical)
+        ph = {}
+        st0 = _native.context(dev.index).stats()
+        codes, counts, roff = sorted_rows_from_device(d_seq, offsets, k, canonical, timings=ph)
+        st1 = _native.context(dev.index).stats()
+        ph["fallback_passes"] = st1["fallback_passes"] - st0["fallback_passes"]
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         m = shard_from_rows(codes, counts, roff, G, k)
@@ -953,6 +961,7 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
             dist.barrier()
         t2 = time.perf_counter()
         if i:
+            phases.append(ph)
             t_rows.append((t1 - t0) * 1e3)
             t_all.append((t2 - t0) * 1e3)
     cols = m.columns
@@ -971,6 +980,8 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
         ms, ok = float(t[0]), float(t[1]) == 0.0
     return {"matrix_ms": round(ms, 2), "sorted_rows_ms": round(float(np.mean(t_rows)), 2),
             "shard_ms": round(ms - float(np.mean(t_rows)), 2), "steps": steps,
+            "sorted_rows_phases": {key: round(float(np.mean([p.get(key, 0.0) for p in phases])), 2)
+                                   for key in phases[-1]} if phases else {},
             "what": f"this rank's {g_local} genomes -> its column shard of the organisms x k-mers matrix "
                     "(features.py:96-111): kmh_count_sparse_sorted_dev, padding dropped, "
                     + ("all-to-all of code ranges, " if world > 1 else "") + "kmh_shard_union_dev (columns + CSR)",

@@ -193,15 +193,9 @@ __device__ __forceinline__ void each_window(const Bases& b, F&& f) {
         if (((b.inv << j) >> (64 - K)) == 0ull) f(code(j), j);
 }
 
-// Persistent, one workgroup per CU (144 KiB of LDS).  XCD x (= blockIdx % 8) takes a contiguous
+// Persistent, one workgroup per CU (132 KiB of LDS).  XCD x (= blockIdx % 8) takes a contiguous
 // run of the tiles, so the u16 offsets its workgroups write side by side share L2 lines, and its
-// workgroups stride through that run.  Bucket counters are replicated across LDS banks (round 5;
-// one counter per bucket put 49 % of the LDS cycles into bank conflicts): the histogram counts
-// bucket b in 16 u16 replicas, replica r = lane & 15 in half r & 1 of word 8 b + r / 2, kept in the
-// staging (free until the scatter, 32 KiB); the scan turns them into 8 replicas of scatter
-// cursors (lane & 7, word 4 b + r / 2, 16 KiB of their own: replica r's range holds the windows
-// counted by replicas r and r + 8).  The 32 lanes of a group then hit at most 2 / 4 words of one
-// bank row per bucket-bank instead of 32 random banks.  Each tile's 64 bytes per thread are loaded behind the
+// workgroups stride through that run.  Each tile's 64 bytes per thread are loaded behind the
 // previous tile's LDS work, and each tile's entries drain behind the next tile's: the barriers
 // wait for LDS operations only (lds_barrier), and the one wait for memory -- the next tile's
 // bytes, encoded before this tile's stores are issued -- comes after a tile of LDS work.
@@ -219,16 +213,10 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     static_assert(R <= 8 * (int)sizeof(E), "residues fit the entry");
     __shared__ __attribute__((aligned(16))) E sorted[kSpTile];
     __shared__ __attribute__((aligned(16))) uint32_t spos[POS ? kSpTile : 4];
-    __shared__ __attribute__((aligned(16))) uint32_t cur8[kSpBuckets * 4];   // scatter cursors
+    __shared__ uint32_t cnt[kSpBuckets];
     __shared__ uint32_t wsum[kNW];
-    static_assert(kSpTile * sizeof(E) >= kSpBuckets * 8 * 4, "the histogram's replicas fit the staging");
-    static_assert(kSpTile <= 65535, "cursors fit u16 halves");
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t* const h16 = reinterpret_cast<uint32_t*>(sorted);   // the histogram's replicas
-    uint4* const h16q = reinterpret_cast<uint4*>(h16);
-    const uint32_t hsh = 16u * ((uint32_t)lane & 1u);               // this lane's half
-    const uint32_t j16 = ((uint32_t)lane & 15u) >> 1, j8 = ((uint32_t)lane & 7u) >> 1;
     const uint32_t x = blockIdx.x % 8u, nwg = gridDim.x;
     const uint32_t nwx = (nwg - x + 7u) / 8u;                      // workgroups on XCD x
     const uint32_t tq = ntiles / 8u, trem = ntiles % 8u;
@@ -268,8 +256,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
     uint4 v[4];
     load_raw(seq, cur.base, cur.gend, cur.fast, v);
     Bases bs = encode_bases(v, cur.base, cur.gend);
-    h16q[tid] = make_uint4(0u, 0u, 0u, 0u);
-    h16q[tid + kSpThreads] = make_uint4(0u, 0u, 0u, 0u);
+    cnt[tid] = 0u;
     __syncthreads();
 
     for (;;) {
@@ -281,23 +268,11 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
             if (nxt.fast) load_raw(seq, nxt.base, nxt.gend, true, v);   // lands during this tile
         }
 
-        each_window<K, CANON, WPT>(bs, [&](uint64_t c, int) {
-            atomicAdd(&h16[((uint32_t)(c >> R) << 3) | j16], 1u << hsh);
-        });
+        each_window<K, CANON, WPT>(bs, [&](uint64_t c, int) { atomicAdd(&cnt[(uint32_t)(c >> R)], 1u); });
         lds_barrier();
 
-        // Exclusive scan of the bucket counts (thread = bucket); the 8 scatter cursors of the
-        // thread's bucket start at its segment start, replica r after replicas < r (r and r + 8)
-        const uint4 ha = h16q[2 * tid], hb = h16q[2 * tid + 1];
-        uint32_t rc8[8];
-        {
-            const uint32_t wa[4] = {ha.x, ha.y, ha.z, ha.w}, wb[4] = {hb.x, hb.y, hb.z, hb.w};
-#pragma unroll
-            for (int r = 0; r < 8; ++r) rc8[r] = ((wa[r >> 1] >> (16 * (r & 1))) & 0xFFFFu) + ((wb[r >> 1] >> (16 * (r & 1))) & 0xFFFFu);
-        }
-        uint32_t n0 = 0u;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) n0 += rc8[r];
+        // Exclusive scan of the bucket counts; cnt becomes the scatter cursor.
+        const uint32_t n0 = cnt[tid];
         const uint32_t incl = scan64(n0);   // DPP: no LDS-pipe shuffles
         if (lane == 63) wsum[wave] = incl;
         lds_barrier();
@@ -308,23 +283,14 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
             total += wsum[w];
         }
         const uint32_t s0 = pre + incl - n0;
-        {
-            uint32_t run = s0, cw[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                cw[q] = run | ((run + rc8[2 * q]) << 16);
-                run += rc8[2 * q] + rc8[2 * q + 1];
-            }
-            reinterpret_cast<uint4*>(cur8)[tid] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-        }
+        cnt[tid] = s0;
         toff[(uint64_t)tid * ldt + lt] = (uint16_t)s0;
         if (tid == 0) toff[(uint64_t)kSpBuckets * ldt + lt] = (uint16_t)total;
         lds_barrier();
 
         const uint32_t p0 = cur.p0;
         each_window<K, CANON, WPT>(bs, [&](uint64_t c, int j) {
-            const uint32_t slot =
-                __builtin_amdgcn_ubfe(atomicAdd(&cur8[((uint32_t)(c >> R) << 2) | j8], 1u << hsh), hsh, 16);
+            const uint32_t slot = atomicAdd(&cnt[(uint32_t)(c >> R)], 1u);
             sorted[slot] = (E)(c & RM);
             if constexpr (POS) spos[slot] = p0 + (uint32_t)j;
         });
@@ -336,6 +302,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
             if (!nxt.fast) load_raw(seq, nxt.base, nxt.gend, false, v);
             bs = encode_bases(v, nxt.base, nxt.gend);
         }
+        cnt[tid] = 0u;   // (the cursors are dead; the next histogram starts after a barrier)
 
         E* dst = ent + (uint64_t)lt * kSpTile;
 #if defined(KMH_EXPERIMENTS) && KMH_SP_PART_EXP == 1
@@ -345,18 +312,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
 #endif
         for (uint32_t i = tid; i < n4; i += kSpThreads)
             store_nt(reinterpret_cast<uint4*>(dst) + i, reinterpret_cast<const uint4*>(sorted)[i]);
-        if (tid == 0)   // the partial last chunk, by one thread (it also clears that chunk below)
-            for (uint32_t i = EPC * n4; i < total; ++i) __builtin_nontemporal_store(sorted[i], dst + i);
-        // the next histogram's replicas cleared behind the copy-out: chunk c of the first 2048 is
-        // read only by thread c % 1024 (c = tid, tid + 1024; the partial chunk n4 by thread 0),
-        // which clears it after its own read (an LDS write after a read of the same wave stays in
-        // order); the loop's closing barrier makes the zeros visible
-        {
-            const uint32_t c0 = (uint32_t)tid, c1 = (uint32_t)tid + kSpThreads;
-            if (c0 != n4 || tid == 0) h16q[c0] = make_uint4(0u, 0u, 0u, 0u);
-            if (c1 != n4) h16q[c1] = make_uint4(0u, 0u, 0u, 0u);
-            if (tid == 0 && n4 < 2u * kSpThreads) h16q[n4] = make_uint4(0u, 0u, 0u, 0u);
-        }
+        if (tid < (int)(total % EPC)) __builtin_nontemporal_store(sorted[EPC * n4 + tid], dst + EPC * n4 + tid);
         if constexpr (POS) {
             uint32_t* pdst = epos + (uint64_t)lt * kSpTile;
             for (uint32_t i = tid; i < total / 4; i += kSpThreads)
@@ -364,7 +320,7 @@ __global__ __launch_bounds__(kSpThreads) void k_sp_partition(const uint8_t* __re
             if (tid < (int)(total % 4)) pdst[4 * (total / 4) + tid] = spos[4 * (total / 4) + tid];
         }
         if (!more) break;
-        lds_barrier();   // zeroed replicas visible; this tile's LDS reads done before the next scatter
+        lds_barrier();   // zeroed counters visible; this tile's LDS reads done before the next scatter
         lt = nlt;
         cur = nxt;
     }

@@ -632,12 +632,23 @@ def sorted_rows_dev(genome_files, k, canonical=True, device=None, group=None):
     return lo, codes, counts, roff
 
 
-def sorted_rows_from_device(d_seq, offsets, k, canonical=True):
+def sorted_rows_from_device(d_seq, offsets, k, canonical=True, timings=None):
     """The sorted rows (as sorted_rows_dev) of genomes already in device memory: d_seq (uint8
-    tensor) holds them at offsets (host uint64[n + 1], 16-byte aligned starts)."""
+    tensor) holds them at offsets (host uint64[n + 1], 16-byte aligned starts).  `timings`: a dict
+    that receives the phases' wall times in ms (each phase synchronised; for the bench)."""
+    import time
     import torch
 
     dev = d_seq.device
+    tick = [time.perf_counter()]
+
+    def phase(name):
+        if timings is not None:
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            timings[name] = timings.get(name, 0.0) + (t - tick[0]) * 1e3
+            tick[0] = t
+
     n = len(offsets) - 1
     out_off = _native.sparse_out_offsets(offsets, k)
     cap = max(int(out_off[-1]), 1)
@@ -647,18 +658,22 @@ def sorted_rows_from_device(d_seq, offsets, k, canonical=True):
     ndist = torch.empty(n, dtype=torch.int64, device=dev)
     ctx = _native.context(dev.index)
     s = torch.cuda.current_stream(dev).cuda_stream
+    phase("alloc_ms")
     ctx.count_sparse_sorted_dev(d_seq.data_ptr(), offsets, k, canonical, codes.data_ptr(), counts.data_ptr(),
                                 nrows.data_ptr(), ndist.data_ptr(), s)
     nr, nd = nrows.cpu().numpy(), ndist.cpu().numpy()
+    phase("count_ms")
     roff = np.zeros(n + 1, np.uint64)
     roff[1:] = np.cumsum(nd)
     if all(int(out_off[g]) == int(roff[g]) and nr[g] == nd[g] for g in range(n)):
         return codes, counts, roff   # back to back already, no padding: no copy
     c2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
     n2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int32, device=dev)
+    phase("alloc_ms")
     # the padding (count-0 rows) dropped on the device, rows back to back (kmh_rows_compact_dev)
     ctx.rows_compact_dev(codes.data_ptr(), counts.data_ptr(), out_off[:n], nr.astype(np.uint64), c2.data_ptr(),
                          n2.data_ptr(), roff[:n], s)
+    phase("compact_ms")
     return c2, n2, roff
 
 
