@@ -958,25 +958,92 @@ __global__ __launch_bounds__(1024) void k_sp_plan(const uint32_t* __restrict__ n
     }
 }
 
-// Writes the items planned by k_sp_plan: one 64-thread workgroup per (genome, bucket).
+// Split items in tile order.  Listed bucket by bucket, the items of one (genome, bucket) would run
+// side by side on one XCD (its workgroups take a run of consecutive items) and read one bucket's
+// segments from every tile of the genome; the 128-byte line a segment shares with the next
+// bucket's segment of the same tile would be read again much later, from HBM (the split read
+// 1.6x its entries).  So k_sp_fill writes every genome's split items ordered by (first tile,
+// tiles per item ts, bucket): items over the same tiles run together and that line is still in
+// the XCD's L2.  The items are the same; only their indices change.  k_sp_order (one workgroup
+// per genome, thread = bucket) lists the genome's distinct ts values ascending with the number of
+// non-empty buckets using each (tab: ts | count << 16; ts <= 16 * 64, a count <= 1024) and each
+// bucket's rank among the buckets of its ts (grank).  Item i of a bucket starts at tile x = i ts;
+// the items before it are, for every value v of count c (ns = ceil(tiles / v) items each), c
+// min(ns, ceil(x / v)) starting before x, plus c more when v < ts and one of them starts at x,
+// plus the bucket's rank.
+__global__ __launch_bounds__(kSpBuckets) void k_sp_order(const uint32_t* __restrict__ nb,
+                                                         const uint64_t* __restrict__ tbase, int g0,
+                                                         uint32_t target, uint32_t split_target, uint32_t epc,
+                                                         uint32_t* __restrict__ grank, uint32_t* __restrict__ tab,
+                                                         uint32_t* __restrict__ nv) {
+    static_assert(kSpBuckets == 1024 && kNW * 64 <= kSpBuckets, "one thread per bucket and per ts value");
+    __shared__ uint32_t tss[kSpBuckets], cnt[kSpBuckets], ws[16];
+    const uint32_t gl = blockIdx.x, b = threadIdx.x, lane = b & 63u, wave = b >> 6;
+    const uint32_t gb = gl * (uint32_t)kSpBuckets + b;
+    const GbRule r(nb[gb], gb_tiles(tbase, g0, (int)gb), target, split_target, epc);
+    const uint32_t v = r.nsplit ? r.ts : 0u;   // 0: no items
+    tss[b] = v;
+    cnt[b] = 0u;
+    __syncthreads();
+    if (v) atomicAdd(&cnt[v - 1u], 1u);
+    uint32_t rk = 0u;
+    for (uint32_t j = 0; j < b; ++j) rk += tss[j] == v ? 1u : 0u;
+    grank[gb] = rk;
+    __syncthreads();
+    // thread t: value t + 1; the values in use compacted in ascending order
+    const uint32_t c = cnt[b], f = c ? 1u : 0u;
+    uint32_t incl = f;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(incl, d);
+        if ((int)lane >= d) incl += x;
+    }
+    if (lane == 63u) ws[wave] = incl;
+    __syncthreads();
+    uint32_t pre = 0u, tot = 0u;
+    for (uint32_t w = 0; w < (uint32_t)kNW; ++w) {
+        if (w < wave) pre += ws[w];
+        tot += ws[w];
+    }
+    if (c) tab[gb - b + pre + incl - 1u] = (b + 1u) | (c << 16);
+    if (b == 0u) nv[gl] = tot;
+}
+
+// Writes the items planned by k_sp_plan: one 64-thread workgroup per (genome, bucket); the
+// genome's split items in tile order (k_sp_order), its count items in pair order.
 __global__ __launch_bounds__(64) void k_sp_fill(const uint32_t* __restrict__ nb,
                                                 const uint64_t* __restrict__ tbase, int g0,
                                                 uint64_t tile_lo, uint32_t target, uint32_t split_target,
                                                 uint32_t epc,
                                                 const uint32_t* __restrict__ sofs,
                                                 const uint32_t* __restrict__ cofs,
+                                                const uint32_t* __restrict__ grank, const uint32_t* __restrict__ tab,
+                                                const uint32_t* __restrict__ nv,
                                                 SplitItem* __restrict__ sitems, CountItem* __restrict__ citems) {
+    __shared__ uint32_t tv[kSpBuckets];
     const int gb = blockIdx.x;
     const uint32_t n = nb[gb];
-    if (!n) return;
-    const int g = g0 + gb / kSpBuckets;
+    if (!n) return;   // (the whole workgroup)
+    const int gl = gb / kSpBuckets;
+    const int g = g0 + gl;
+    const uint32_t V = nv[gl];
+    for (uint32_t u = threadIdx.x; u < V; u += 64u) tv[u] = tab[(uint32_t)gl * kSpBuckets + u];
+    __syncthreads();
     const uint32_t b = (uint32_t)(gb % kSpBuckets);
-    const uint32_t ta = (uint32_t)(tbase[g] - tile_lo), tb = (uint32_t)(tbase[g + 1] - tile_lo);
-    const GbRule r(n, tb - ta, target, split_target, epc);
-    const uint32_t s0 = sofs[gb];
+    const uint32_t ta = (uint32_t)(tbase[g] - tile_lo), tb = (uint32_t)(tbase[g + 1] - tile_lo), nt = tb - ta;
+    const GbRule r(n, nt, target, split_target, epc);
+    const uint32_t s0 = sofs[(uint32_t)gl * kSpBuckets] + grank[gb];
     for (uint32_t i = threadIdx.x; i < r.nsplit; i += 64u) {
-        const uint32_t t = ta + i * r.ts;
-        sitems[s0 + i] = SplitItem{b, t, min(t + r.ts, tb), r.np, (uint32_t)gb, r.per, cofs[gb], 0u};
+        const uint32_t x = i * r.ts;
+        uint32_t at = s0;
+        for (uint32_t u = 0; u < V; ++u) {
+            const uint32_t vu = tv[u] & 0xFFFFu, cu = tv[u] >> 16;
+            const uint32_t nsu = (nt + vu - 1u) / vu, q = x / vu, rm = x - q * vu;
+            at += cu * min(nsu, q + (rm ? 1u : 0u));
+            if (vu < r.ts && rm == 0u && q < nsu) at += cu;
+        }
+        const uint32_t t = ta + x;
+        sitems[at] = SplitItem{b, t, min(t + r.ts, tb), r.np, (uint32_t)gb, r.per, cofs[gb], 0u};
     }
     for (uint32_t p = threadIdx.x; p < r.np; p += 64u)
         citems[cofs[gb] + p] = CountItem{(uint32_t)g, b, p, r.np, (uint32_t)gb, n};
@@ -2082,19 +2149,25 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         // bucket sizes -> split and count work items, planned and written on the device;
         // the host reads back only the two item totals to size the buffers
         const size_t ngb = (size_t)nG * kSpBuckets;
-        rc = ensure(ctx, ctx->sparse[4], ngb * 16 + 4096);
+        rc = ensure(ctx, ctx->sparse[4], ngb * 24 + (size_t)nG * 4 + 4096);
         if (rc) return rc;
         uint32_t* d_nb = static_cast<uint32_t*>(ctx->sparse[4].ptr);
         uint32_t* d_gbfail = d_nb + ngb;
         uint32_t* d_sofs = d_gbfail + ngb;
         uint32_t* d_cofs = d_sofs + ngb;
-        uint32_t* d_totals = d_cofs + ngb;
+        uint32_t* d_grank = d_cofs + ngb;     // k_sp_order: rank among the genome's buckets of equal ts
+        uint32_t* d_tab = d_grank + ngb;      // k_sp_order: distinct ts values per genome
+        uint32_t* d_nv = d_tab + ngb;
+        uint32_t* d_totals = d_nv + nG;
         KMH_HIP(ctx, hipMemsetAsync(d_gbfail, 0, ngb * 4, s));
         hipLaunchKernelGGL(k_sp_sizes, dim3((unsigned)ngb), dim3(256), 0, s, toff, ldt, d_tbase, g0,
                            L.tbase[g0], d_nb);
         KMH_HIP(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_sp_plan, dim3(1), dim3(1024), 0, s, d_nb, (int)ngb, d_tbase, g0, target,
                            split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_totals);
+        KMH_HIP(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_sp_order, dim3((unsigned)nG), dim3(kSpBuckets), 0, s, d_nb, d_tbase, g0, target,
+                           split_target, (uint32_t)epc<E>(), d_grank, d_tab, d_nv);
         KMH_HIP(ctx, hipGetLastError());
         uint32_t totals[2] = {0u, 0u};
         KMH_HIP(ctx, hipMemcpyAsync(totals, d_totals, 8, hipMemcpyDeviceToHost, s));
@@ -2133,7 +2206,8 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             ORD ? reinterpret_cast<unsigned long long*>(base + sib + cib + ob + fb + ((nci * 8 + 255) & ~(size_t)255))
                 : nullptr;
         hipLaunchKernelGGL(k_sp_fill, dim3((unsigned)ngb), dim3(64), 0, s, d_nb, d_tbase, g0, L.tbase[g0],
-                           target, split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_sitems, d_citems);
+                           target, split_target, (uint32_t)epc<E>(), d_sofs, d_cofs, d_grank, d_tab, d_nv, d_sitems,
+                           d_citems);
         KMH_HIP(ctx, hipGetLastError());
         KMH_HIP(ctx, hipMemcpyAsync(d_out_off, out_off.data(), (size_t)(G + 1) * 8, hipMemcpyHostToDevice, s));
         KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
