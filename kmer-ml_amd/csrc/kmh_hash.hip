@@ -1366,16 +1366,54 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
             lds_barrier();
             if constexpr (ORD) {
-                // each bin's keys in ascending order (insertion sort in place; bins of more than
-                // BIG keys fail the item below, so a loop here runs at most BIG - 1 times)
+                // each bin's keys in ascending order.  Bins of 2..4 keys (almost every bin that
+                // needs it: ~1 key per bin) by a sorting network in registers -- four reads per bin
+                // at addresses clamped into the bin, all of a thread's 16 bins issued together,
+                // missing keys as the largest value -- and bins of 5..BIG keys (rare; more fail the
+                // item below) by insertion in place.  (An insertion sort of every bin was a chain of
+                // dependent LDS round trips per bin slot, taken by the whole wave whenever one of
+                // its lanes had a bin to sort: the sorted count ran 2.3x the unsorted one.)
+                constexpr E kTop = ~(E)0;
+                auto cswap = [](E& a, E& b) {
+                    const E lo = a < b ? a : b, hi = a < b ? b : a;
+                    a = lo;
+                    b = hi;
+                };
 #pragma unroll
                 for (int q = 0; q < BQ; ++q) {
                     const uint4 rq = h4[swzh_slot(BQ * tid + q)];
                     const uint32_t rg[4] = {rq.x, rq.y, rq.z, rq.w};
+                    E kv[4][4];
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const uint32_t bs = rg[i] & 0xFFFFu, be = rg[i] >> 16;
-                        if (be - bs >= 2u && be - bs <= (uint32_t)BIG) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const uint32_t y = bs + (uint32_t)t;
+                            kv[i][t] = sorted[swz<EPC>(y < be ? y : bs)];
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t bs = rg[i] & 0xFFFFu, n = (rg[i] >> 16) - bs;
+                        E a = kv[i][0], b = n > 1u ? kv[i][1] : kTop, c = n > 2u ? kv[i][2] : kTop,
+                          d = n > 3u ? kv[i][3] : kTop;
+                        cswap(a, b);
+                        cswap(c, d);
+                        cswap(a, c);
+                        cswap(b, d);
+                        cswap(b, c);
+                        if (n >= 2u && n <= 4u) {
+                            sorted[swz<EPC>(bs)] = a;
+                            sorted[swz<EPC>(bs + 1u)] = b;
+                            if (n > 2u) sorted[swz<EPC>(bs + 2u)] = c;
+                            if (n > 3u) sorted[swz<EPC>(bs + 3u)] = d;
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t bs = rg[i] & 0xFFFFu, be = rg[i] >> 16;
+                        if (be - bs > 4u && be - bs <= (uint32_t)BIG) {
                             for (uint32_t x = bs + 1u; x < be; ++x) {
                                 const E key = sorted[swz<EPC>(x)];
                                 uint32_t y = x;
@@ -1854,18 +1892,59 @@ __global__ __launch_bounds__(256) void k_sp_append(const E* __restrict__ keys, c
 
 // ORD: output base of every count item of a batch (items in (genome, bucket, pass) order) = the
 // genome's row offset + the keys of its earlier items, and every genome's row length nk[g] (its
-// items' keys: distinct k-mers + padding).  One workgroup; gstart: scratch of a u64 per genome.
-__global__ __launch_bounds__(1024) void k_sp_item_offsets(const uint32_t* __restrict__ pfill,
-                                                          const CountItem* __restrict__ items, uint32_t nci,
-                                                          const uint64_t* __restrict__ out_off,
-                                                          uint64_t* __restrict__ item_off,
-                                                          unsigned long long* __restrict__ gstart, int g0,
-                                                          unsigned long long* __restrict__ nk) {
-    __shared__ unsigned long long ws[16];
+// items' keys: distinct k-mers + padding).  Three launches over chunks of kIoChunk items (one
+// workgroup each; the single-workgroup version walked 512 items per thread with uncoalesced loads:
+// 5 ms per config-5 batch): (1) chunk sums and the genomes' totals (nk, one atomic per wave when its
+// items share a genome), (2) one workgroup scans the chunk sums (cpre) and the batch's genome totals
+// (gst), (3) every item's base.
+constexpr int kIoPer = 16, kIoChunk = 256 * kIoPer;
+
+__global__ __launch_bounds__(256) void k_sp_io_sums(const uint32_t* __restrict__ pfill,
+                                                    const CountItem* __restrict__ items, uint32_t nci,
+                                                    unsigned long long* __restrict__ csum,
+                                                    unsigned long long* __restrict__ nk) {
+    __shared__ unsigned long long ws[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t a = blockIdx.x * (uint32_t)kIoChunk + threadIdx.x * (uint32_t)kIoPer;
+    unsigned long long tot = 0ull, run = 0ull;
+    uint32_t g = a < nci ? items[a].g : 0u;
+    bool split = false;   // this thread's items span two genomes or more
+    for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) {
+        const uint32_t i = a + j, gi = items[i].g;
+        const unsigned long long v = pfill[i];
+        if (gi != g) {
+            atomicAdd(&nk[g], run);
+            run = 0ull;
+            g = gi;
+            split = true;
+        }
+        run += v;
+        tot += v;
+    }
+    // the last genome's run: one atomic per wave when every lane holds the same genome
+    const uint32_t g0 = (uint32_t)__shfl(g, 0);
+    const bool same = !__any(split || (a < nci && g != g0) || a >= nci);
+    if (same) {
+        unsigned long long r = run;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) r += __shfl_xor(r, d);
+        if (lane == 0u) atomicAdd(&nk[g0], r);
+    } else if (a < nci) {
+        atomicAdd(&nk[g], run);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) tot += __shfl_xor(tot, d);
+    if (lane == 0u) ws[wave] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) csum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// One workgroup: exclusive scans of n u64 values in place (sequential runs per thread + a block scan).
+__device__ void block_scan_u64_inplace(unsigned long long* v, uint32_t n, unsigned long long* ws) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t per = (nci + 1023u) / 1024u, a = min(nci, tid * per), e = min(nci, a + per);
+    const uint32_t per = (n + 1023u) / 1024u, a = min(n, tid * per), e = min(n, a + per);
     unsigned long long s = 0ull;
-    for (uint32_t i = a; i < e; ++i) s += pfill[i];
+    for (uint32_t i = a; i < e; ++i) s += v[i];
     unsigned long long incl = s;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1874,23 +1953,52 @@ __global__ __launch_bounds__(1024) void k_sp_item_offsets(const uint32_t* __rest
     }
     if (lane == 63u) ws[wave] = incl;
     __syncthreads();
-    unsigned long long pre = incl - s;
-    for (uint32_t w = 0; w < wave; ++w) pre += ws[w];
-    unsigned long long q = pre;
+    unsigned long long p = incl - s;
+    for (uint32_t w = 0; w < wave; ++w) p += ws[w];
     for (uint32_t i = a; i < e; ++i) {
-        const uint32_t g = items[i].g;
-        if (i == 0u || items[i - 1u].g != g) gstart[g - (uint32_t)g0] = q;
-        q += pfill[i];
+        const unsigned long long x = v[i];
+        v[i] = p;
+        p += x;
     }
-    __threadfence();
     __syncthreads();
-    q = pre;
-    for (uint32_t i = a; i < e; ++i) {
-        const uint32_t g = items[i].g;
-        const unsigned long long gs = gstart[g - (uint32_t)g0];
-        item_off[i] = out_off[g] + (q - gs);
-        q += pfill[i];
-        if (i + 1u == nci || items[i + 1u].g != g) nk[g] = q - gs;
+}
+
+// cpre[c] = the keys of the chunks before c; gst[j] = the keys of the batch's genomes before g0 + j.
+__global__ __launch_bounds__(1024) void k_sp_io_scan(unsigned long long* __restrict__ csum, uint32_t nch,
+                                                     const unsigned long long* __restrict__ nk, int g0, int nG,
+                                                     unsigned long long* __restrict__ gst) {
+    __shared__ unsigned long long ws[16];
+    for (uint32_t j = threadIdx.x; j < (uint32_t)nG; j += 1024u) gst[j] = nk[g0 + (int)j];
+    __syncthreads();
+    block_scan_u64_inplace(csum, nch, ws);
+    block_scan_u64_inplace(gst, (uint32_t)nG, ws);
+}
+
+__global__ __launch_bounds__(256) void k_sp_io_write(const uint32_t* __restrict__ pfill,
+                                                     const CountItem* __restrict__ items, uint32_t nci,
+                                                     const unsigned long long* __restrict__ cpre,
+                                                     const unsigned long long* __restrict__ gst, int g0,
+                                                     const uint64_t* __restrict__ out_off,
+                                                     uint64_t* __restrict__ item_off) {
+    __shared__ unsigned long long ws[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t a = blockIdx.x * (uint32_t)kIoChunk + threadIdx.x * (uint32_t)kIoPer;
+    unsigned long long s = 0ull;
+    for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) s += pfill[a + j];
+    unsigned long long incl = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long x = __shfl_up(incl, d);
+        if ((int)lane >= d) incl += x;
+    }
+    if (lane == 63u) ws[wave] = incl;
+    __syncthreads();
+    unsigned long long p = cpre[blockIdx.x] + incl - s;
+    for (uint32_t w = 0; w < wave; ++w) p += ws[w];
+    for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) {
+        const uint32_t i = a + j, g = items[i].g;
+        item_off[i] = out_off[g] + (p - gst[g - (uint32_t)g0]);
+        p += pfill[i];
     }
 }
 
@@ -2193,7 +2301,10 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         const size_t ob = ((size_t)(G + 1) * 8 + 255) & ~(size_t)255;
         const size_t fb = ((nci + 1) * 4 + 255) & ~(size_t)255;
         // ORD: the items' output bases and a genome-start scratch
-        const size_t iob = ORD ? ((nci * 8 + 255) & ~(size_t)255) + (((size_t)nG * 8 + 255) & ~(size_t)255) : 0;
+        const size_t nch = (nci + kIoChunk - 1) / kIoChunk;
+        const size_t iob = ORD ? ((nci * 8 + 255) & ~(size_t)255) + (((size_t)nG * 8 + 255) & ~(size_t)255) +
+                                     ((nch * 8 + 255) & ~(size_t)255)
+                               : 0;
         rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb + iob);
         if (rc) return rc;
         char* base = static_cast<char*>(ctx->sparse[1].ptr);
@@ -2233,8 +2344,15 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         }
 #endif
         if constexpr (ORD) {   // every item's output base (its genome's earlier items' keys) and row lengths
-            hipLaunchKernelGGL(k_sp_item_offsets, dim3(1), dim3(1024), 0, s, d_pfill, d_citems, (uint32_t)nci,
-                               d_out_off, d_item_off, d_gstart, g0, reinterpret_cast<unsigned long long*>(d_nkmers));
+            unsigned long long* const d_csum = d_gstart + (((size_t)nG * 8 + 255) & ~(size_t)255) / 8;
+            unsigned long long* const d_rows = reinterpret_cast<unsigned long long*>(d_nkmers);
+            hipLaunchKernelGGL(k_sp_io_sums, dim3((unsigned)nch), dim3(256), 0, s, d_pfill, d_citems, (uint32_t)nci, d_csum,
+                               d_rows);
+            KMH_HIP(ctx, hipGetLastError());
+            hipLaunchKernelGGL(k_sp_io_scan, dim3(1), dim3(1024), 0, s, d_csum, (uint32_t)nch, d_rows, g0, nG, d_gstart);
+            KMH_HIP(ctx, hipGetLastError());
+            hipLaunchKernelGGL(k_sp_io_write, dim3((unsigned)nch), dim3(256), 0, s, d_pfill, d_citems, (uint32_t)nci,
+                               d_csum, d_gstart, g0, d_out_off, d_item_off);
             KMH_HIP(ctx, hipGetLastError());
         }
         time_begin(ctx, s, "k_sp_count");

@@ -6,16 +6,21 @@
 // the sorted union of their codes (`columns`) and, for every row entry, its column index
 // (`indices`): with the rows' offsets as indptr and their counts as values, the shard's CSR.
 //
-// The code range is cut into S sub-ranges of 2^SH codes (~2048 entries each, all rows
-// together).  k_shard_starts finds where every row enters every sub-range (one pass over the
-// codes, no search); then one workgroup per sub-range gathers the rows' pieces into LDS and
-// sorts them by a counting sort on 13 bits of the code (~0.5 entries per bin) followed by an
-// insertion sort of each bin, after which equal codes are adjacent: run heads are the union.
-// k_shard_union runs twice -- the union's size per sub-range, then (after a scan) the columns
-// and the indices -- so no entry moves through memory other than its code being read.  A
-// sub-range that overflows the LDS (more than kShCap entries, or a bin of more than kShBin:
-// codes shared by many organisms, low-complexity data) is left to an exact fallback: its
-// entries are gathered, radix-sorted (kmh_sort.hip) and written the same way.
+// The code range is cut into units of ~kShTarget entries (all rows together), sized by the
+// entries' density: a coarse grid of 2^16 power-of-two cells (k_shard_coarse: every row's start
+// in every cell, by binary search), each cell cut into ceil(entries / kShTarget) equal code spans
+// (k_shard_cells, k_shard_units: the units' first and end codes), and every row's start in every
+// unit by a binary search inside its cell (k_shard_ustarts).  Then one workgroup per unit gathers
+// the rows' pieces into LDS and sorts them by a counting sort on 13 bits of the code (~0.75
+// entries per bin) followed by an insertion sort of each bin, after which equal codes are
+// adjacent: run heads are the union.  k_shard_union runs twice -- the union's size per unit, then
+// (after a scan) the columns and the indices -- so no entry moves through memory other than its
+// code being read.  A unit that overflows the LDS (more than kShCap entries, or a bin of more
+// than kShBin: codes shared by many organisms, low-complexity data) is left to an exact
+// fallback: its entries are gathered, radix-sorted (kmh_sort.hip) and written the same way.
+// (Round 5: until then the units were uniform code spans of ~2048 entries on average and their
+// starts came from a pass over every code; the workgroups were latency-bound per unit, and a
+// uniform span must stay small enough for the densest part of the range.)
 #include <algorithm>
 #include <vector>
 
@@ -28,37 +33,99 @@ constexpr int kShThreads = 1024;
 constexpr int kShCap = 8192;        // entries of one sub-range in LDS
 constexpr int kShBinBits = 13;
 constexpr int kShBins = 1 << kShBinBits;
-constexpr int kShBin = 32;          // entries of one bin sorted in place (more: fallback)
+constexpr int kShBin = 64;          // entries of one bin sorted in place (more: fallback)
 constexpr int kShMaxRows = 4096;    // organisms of one shard (LDS piece table)
-constexpr int kShTarget = 2048;     // expected entries per sub-range
+constexpr int kShRoffCache = 1024;  // row offsets kept in LDS
+constexpr int kShTarget = 6144;     // entries per unit (units of one coarse cell share its entries)
+constexpr int kShCoarseBits = 16;   // coarse cells: at most 2^16
 
-// Sub-range of code c: (c - lo) >> SH.
-__device__ __forceinline__ uint64_t sub_of(uint64_t c, uint64_t lo, int SH) { return (c - lo) >> SH; }
+// First entry of row[a, b) that is >= c (row ascending).
+__device__ __forceinline__ uint32_t lower_in(const uint64_t* __restrict__ row, uint32_t a, uint32_t b, uint64_t c) {
+    while (a < b) {
+        const uint32_t m = a + (b - a) / 2u;
+        if (row[m] < c) a = m + 1u;
+        else b = m;
+    }
+    return a;
+}
 
-// st[r * (S + 1) + s] = the first entry of row r (relative to the row) whose sub-range is >= s,
-// for s = 0 .. S (st[.. S] = the row's length).  Entry i writes the sub-ranges (sub(i - 1),
-// sub(i)]; the last entry also (sub(n - 1), S].  One grid row per organism row.
-__global__ __launch_bounds__(256) void k_shard_starts(const uint64_t* __restrict__ codes,
-                                                      const uint64_t* __restrict__ roff, uint64_t lo, int SH,
-                                                      uint32_t S, uint32_t* __restrict__ st) {
-    const uint32_t r = blockIdx.y;
-    const uint64_t a = roff[r], n = roff[r + 1] - a;
-    uint32_t* row = st + (uint64_t)r * (S + 1u);
-    if (n == 0) {
-        for (uint64_t s = (uint64_t)blockIdx.x * 256u + threadIdx.x; s <= S; s += (uint64_t)gridDim.x * 256u)
-            row[s] = 0u;
+// cs[r * (Q + 1) + q] = the first entry of row r (relative to the row) whose code is >= the
+// start of coarse cell q, lo + q 2^CSH (q = Q: the row's length).  One thread per (q, r).
+__global__ __launch_bounds__(256) void k_shard_coarse(const uint64_t* __restrict__ codes,
+                                                      const uint64_t* __restrict__ roff, int R, uint64_t lo,
+                                                      int CSH, uint32_t Q, uint32_t* __restrict__ cs) {
+    const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (x >= (uint64_t)(Q + 1u) * (uint64_t)R) return;
+    const uint32_t r = (uint32_t)(x / (Q + 1u)), q = (uint32_t)(x % (Q + 1u));
+    const uint64_t a = roff[r];
+    const uint32_t n = (uint32_t)(roff[r + 1] - a);
+    cs[x] = q == Q ? n : lower_in(codes + a, 0u, n, lo + ((uint64_t)q << CSH));
+}
+
+// Units of coarse cell q: nu[q] = ceil(its entries (all rows) / kShTarget).
+__global__ __launch_bounds__(256) void k_shard_cells(const uint32_t* __restrict__ cs, int R, uint32_t Q,
+                                                     uint32_t* __restrict__ nu) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= Q) return;
+    uint64_t e = 0;
+    for (int r = 0; r < R; ++r) e += cs[(uint64_t)r * (Q + 1u) + q + 1u] - cs[(uint64_t)r * (Q + 1u) + q];
+    nu[q] = (uint32_t)((e + kShTarget - 1) / kShTarget);
+}
+
+// The units of cell q (ubase[q] .. + nu[q]): equal code spans [ub, ue] of the cell [lo + q 2^CSH,
+// + 2^CSH) (the last cell ends at hi): of its W codes, part j starts at j (W / n) + min(j, W % n).
+// One thread per cell.
+__global__ __launch_bounds__(256) void k_shard_units(const uint32_t* __restrict__ nu,
+                                                     const unsigned long long* __restrict__ ubase, uint32_t Q,
+                                                     uint64_t lo, uint64_t hi_incl, int CSH,
+                                                     uint64_t* __restrict__ ub, uint64_t* __restrict__ ue,
+                                                     uint32_t* __restrict__ ucell) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= Q) return;
+    const uint32_t n = nu[q];
+    if (!n) return;
+    const uint64_t c0 = lo + ((uint64_t)q << CSH);
+    const uint64_t last = q + 1u == Q ? hi_incl : c0 + ((1ull << CSH) - 1u);   // the cell's last code
+    const uint64_t W = last - c0 + 1u;   // <= 2^63 (CSH <= 63); n <= W (a cell of W codes holds <= R W entries, R <= kShTarget)
+    const uint64_t qw = W / n, rw = W % n;
+    const uint64_t u0 = ubase[q];
+    for (uint32_t j = 0; j < n; ++j) {
+        ub[u0 + j] = c0 + (uint64_t)j * qw + (j < rw ? j : rw);
+        ue[u0 + j] = j + 1u == n ? last : c0 + (uint64_t)(j + 1u) * qw + (j + 1u < rw ? j + 1u : rw) - 1u;   // (inclusive)
+        ucell[u0 + j] = q;
+    }
+}
+
+// st[r * (U + 1) + u] = the first entry of row r whose code is >= unit u's first code, found
+// inside the unit's coarse cell; st[.. U] = the row's length.  One thread per (u, r).
+__global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restrict__ codes,
+                                                       const uint64_t* __restrict__ roff, int R,
+                                                       const uint32_t* __restrict__ cs, uint32_t Q,
+                                                       const uint64_t* __restrict__ ub,
+                                                       const uint32_t* __restrict__ ucell, uint32_t U,
+                                                       uint32_t* __restrict__ st) {
+    const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (x >= (uint64_t)(U + 1u) * (uint64_t)R) return;
+    const uint32_t r = (uint32_t)(x / (U + 1u)), u = (uint32_t)(x % (U + 1u));
+    const uint64_t a = roff[r];
+    if (u == U) {
+        st[x] = (uint32_t)(roff[r + 1] - a);
         return;
     }
-    // (codes outside [lo, hi] -- not a valid input -- are clamped into the last sub-range: wrong
-    // columns, never a write outside the table)
-    const uint64_t smax = (uint64_t)S - 1u;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
-        const uint64_t si = min(sub_of(codes[a + i], lo, SH), smax);
-        const uint64_t sp = i ? min(sub_of(codes[a + i - 1], lo, SH), smax) + 1u : 0u;
-        for (uint64_t s = sp; s <= si; ++s) row[s] = (uint32_t)i;
-        if (i + 1 == n)
-            for (uint64_t s = si + 1u; s <= S; ++s) row[s] = (uint32_t)n;
+    const uint32_t q = ucell[u];
+    const uint32_t* c = cs + (uint64_t)r * (Q + 1u);
+    st[x] = lower_in(codes + a, c[q], c[q + 1u], ub[u]);
+}
+
+// Unit of code c (fallback only): the last unit whose first code is <= c.
+__device__ __forceinline__ uint32_t unit_of(const uint64_t* __restrict__ ub, uint32_t U, uint64_t c) {
+    uint32_t a = 0u, b = U - 1u;
+    while (a < b) {
+        const uint32_t m = (a + b + 1u) / 2u;
+        if (ub[m] <= c) a = m;
+        else b = m - 1u;
     }
+    return a;
 }
 
 // Block-wide exclusive scan of one u32 per thread (kShThreads); returns the thread's prefix,
@@ -80,15 +147,16 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
     return pre + incl - v;
 }
 
-// One workgroup per sub-range (persistent: s = blockIdx.x, += gridDim.x).  WRITE = false: the
-// number of distinct codes of every sub-range into ucount (0 for a sub-range left to the
-// fallback, which is listed in big).  WRITE = true: the columns [colbase[s], colbase[s + 1]) and
-// the column index of every entry.
+// One workgroup per unit (persistent: s = blockIdx.x, += gridDim.x; unit s = codes [ub[s], ue[s]],
+// row r's piece = entries st[r][s] .. st[r][s + 1]).  WRITE = false: the number of distinct codes of
+// every unit into ucount (0 for a unit left to the fallback, which is listed in big).  WRITE =
+// true: the columns [colbase[s], colbase[s + 1]) and the column index of every entry.
 template <bool WRITE>
 __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
-                                                            const uint32_t* __restrict__ st, uint32_t S, uint64_t lo,
-                                                            int SH, uint32_t* __restrict__ ucount,
+                                                            const uint32_t* __restrict__ st, uint32_t S,
+                                                            const uint64_t* __restrict__ ub,
+                                                            const uint64_t* __restrict__ ue, uint32_t* __restrict__ ucount,
                                                             uint32_t* __restrict__ big,
                                                             const unsigned long long* __restrict__ colbase,
                                                             uint64_t* __restrict__ columns,
@@ -98,12 +166,15 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
     __shared__ uint32_t hist[kShBins];
     __shared__ uint32_t pfx[kShMaxRows + 1];   // the rows' pieces: exclusive prefix of their sizes
     __shared__ uint32_t pa[kShMaxRows];        // the pieces' first entries (relative to their rows)
+    __shared__ uint64_t sroff[kShRoffCache];  // the first rows' offsets (the rest read from memory)
     __shared__ uint32_t ws[kShThreads / 64];
     __shared__ uint32_t flag;
     constexpr int PER = kShCap / kShThreads;   // entries per thread
     constexpr int BPT = kShBins / kShThreads;  // bins per thread
     const int tid = threadIdx.x;
-    const int bsh = SH > kShBinBits ? SH - kShBinBits : 0;
+    for (int r = tid; r < R && r < kShRoffCache; r += kShThreads) sroff[r] = roff[r];
+    // (made visible by the first unit's barriers)
+    auto row_base = [&](int r) { return r < kShRoffCache ? sroff[r] : roff[r]; };
 
     // row of gathered entry i: the last row whose prefix is <= i
     auto row_of = [&](uint32_t i) {
@@ -117,7 +188,9 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
     };
 
     for (uint32_t s = blockIdx.x; s < S; s += gridDim.x) {
-        // 1. the pieces of the rows in sub-range s
+        // WRITE: the unit's first column, loaded now and first used after the sort
+        const unsigned long long cb = WRITE ? colbase[s] : 0ull;
+        // 1. the pieces of the rows in unit s
         // this thread's rows: a contiguous run of at most 4 (R <= kShMaxRows), so that the
         // block scan of the threads' sums is the rows' prefix in row order
         const int rq = (R + kShThreads - 1) / kShThreads, r0 = min(R, tid * rq), r1 = min(R, r0 + rq);
@@ -147,22 +220,37 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
             __syncthreads();
             continue;
         }
+        if (T == 0u) {   // (uniform) an empty unit (a part of a coarse cell with no entries)
+            if (!WRITE && tid == 0) ucount[s] = 0u;
+            __syncthreads();
+            continue;
+        }
         __syncthreads();
-        // 2. the codes into registers, their bins counted
-        const uint64_t base = lo + ((uint64_t)s << SH);
+        // 2. the codes into registers, their bins counted: 13 bits over the unit's span
+        const uint64_t base = ub[s], span1 = ue[s] - base;   // span - 1
+        const int sbits = span1 ? 64 - __builtin_clzll(span1) : 0;
+        const int bsh = sbits > kShBinBits ? sbits - kShBinBits : 0;
+        // every load in flight at once: addresses first (LDS), then the loads (a load whose
+        // result feeds an LDS atomic before the next load is issued made the 8 loads of a thread
+        // 8 serial round trips), then the bins
         uint64_t cv[PER];
         uint32_t bv[PER];
+        {
+            uint64_t at[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t i = (uint32_t)(u * kShThreads + tid), ic = i < T ? i : T - 1u;   // (T >= 1)
+                const int r = row_of(ic);
+                at[u] = row_base(r) + pa[r] + (ic - pfx[r]);
+            }
+#pragma unroll
+            for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
+        }
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const uint32_t i = (uint32_t)(u * kShThreads + tid);
-            cv[u] = 0ull;
-            bv[u] = 0u;
-            if (i < T) {
-                const int r = row_of(i);
-                cv[u] = codes[roff[r] + pa[r] + (i - pfx[r])];
-                bv[u] = (uint32_t)min((cv[u] - base) >> bsh, (uint64_t)(kShBins - 1));
-                atomicAdd(&hist[bv[u]], 1u);
-            }
+            bv[u] = (uint32_t)min((cv[u] - base) >> bsh, (uint64_t)(kShBins - 1));
+            if (i < T) atomicAdd(&hist[bv[u]], 1u);
         }
         __syncthreads();
         // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
@@ -234,7 +322,6 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
         if constexpr (!WRITE) {
             if (tid == 0) ucount[s] = U;
         } else {
-            const unsigned long long cb = colbase[s];
             uint32_t run = hp;   // heads before this thread's positions
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
@@ -246,7 +333,7 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
                     }
                     const uint32_t i = sidx[p];
                     const int r = row_of(i);
-                    indices[roff[r] + pa[r] + (i - pfx[r])] = (int64_t)(cb + run - 1u);
+                    indices[row_base(r) + pa[r] + (i - pfx[r])] = (int64_t)(cb + run - 1u);
                 }
             }
         }
@@ -317,11 +404,12 @@ __global__ __launch_bounds__(256) void k_shard_big_gather(const uint64_t* __rest
 // Fallback, runs: every run of the sorted gathered codes adds one to its sub-range's count.
 __global__ __launch_bounds__(256) void k_shard_big_count(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ starts,
-                                                         const uint32_t* __restrict__ nruns, uint64_t lo, int SH,
+                                                         const uint32_t* __restrict__ nruns,
+                                                         const uint64_t* __restrict__ ub, uint32_t U,
                                                          uint32_t* __restrict__ ucount) {
     const uint32_t n = *nruns;
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < n; r += gridDim.x * 256u)
-        atomicAdd(&ucount[sub_of(keys[starts[r]], lo, SH)], 1u);
+        atomicAdd(&ucount[unit_of(ub, U, keys[starts[r]])], 1u);
 }
 
 // Fallback, write: run r's column = colbase[its sub-range] + (r - the sub-range's first run);
@@ -329,18 +417,19 @@ __global__ __launch_bounds__(256) void k_shard_big_count(const uint64_t* __restr
 __global__ __launch_bounds__(256) void k_shard_big_write(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, uint64_t m,
                                                          const uint32_t* __restrict__ starts,
-                                                         const uint32_t* __restrict__ nruns, uint64_t lo, int SH,
+                                                         const uint32_t* __restrict__ nruns,
+                                                         const uint64_t* __restrict__ ub, uint32_t U,
                                                          const unsigned long long* __restrict__ colbase,
                                                          const uint64_t* __restrict__ gpos,
                                                          uint64_t* __restrict__ columns, int64_t* __restrict__ indices) {
     const uint32_t n = *nruns;
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < n; r += gridDim.x * 256u) {
         const uint64_t c = keys[starts[r]];
-        const uint64_t s = sub_of(c, lo, SH);
-        uint32_t a = 0u, b = r;   // the first run of sub-range s
+        const uint32_t s = unit_of(ub, U, c);
+        uint32_t a = 0u, b = r;   // the first run of unit s
         while (a < b) {
             const uint32_t mid = (a + b) / 2u;
-            if (sub_of(keys[starts[mid]], lo, SH) < s) a = mid + 1u;
+            if (unit_of(ub, U, keys[starts[mid]]) < s) a = mid + 1u;
             else b = mid;
         }
         const unsigned long long col = colbase[s] + (r - a);
@@ -448,6 +537,7 @@ int rows_compact(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, co
 
 int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
                 uint64_t hi_incl, uint64_t* d_columns, int64_t* d_indices, uint64_t* ncols, hipStream_t s) {
+    static_assert(kShMaxRows <= kShTarget, "a cell's units are never narrower than one code");
     if (R < 1 || R > kShMaxRows) return fail(ctx, KMH_ERR_UNSUPPORTED, "a shard holds 1 to 4096 organism rows");
     if (!d_codes || !row_off || !ncols || hi_incl < lo) return fail(ctx, KMH_ERR_INVALID, "bad shard arguments");
     const uint64_t T = row_off[R] - row_off[0];
@@ -457,44 +547,71 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     *ncols = 0;
     if (T == 0) return KMH_OK;
     if (!d_columns || !d_indices) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
-    // sub-ranges of 2^SH codes: ~kShTarget entries each, at most 2^24 of them
-    const unsigned __int128 span = (unsigned __int128)(hi_incl - lo) + 1u;
-    uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(T / kShTarget, 1ull << 24));
-    int SH = 0;
-    while (SH < 64 && (span >> SH) > (unsigned __int128)want) ++SH;
-    const uint32_t S = (uint32_t)((span + ((unsigned __int128)1 << SH) - 1) >> SH);
+    // coarse cells of 2^CSH codes: span <= 2^nbits, at most 2^kShCoarseBits cells
+    const uint64_t span1 = hi_incl - lo;   // span - 1
+    const int nbits = span1 ? 64 - __builtin_clzll(span1) : 0;
+    // (at most 2^25 coarse starts: 2^16 cells up to 512 rows, fewer beyond)
+    int rbits = 0;
+    while ((1 << rbits) < R) ++rbits;
+    const int qb = std::min(std::min(kShCoarseBits, 25 - rbits), nbits), CSH = nbits - qb;
+    const uint32_t Q = (uint32_t)((span1 >> CSH) + 1u);
 
-    const size_t stb = (((size_t)R * (S + 1) * 4) + 255) & ~(size_t)255;
+    const size_t csb = (((size_t)R * (Q + 1) * 4) + 255) & ~(size_t)255;
     const size_t rb = (((size_t)R + 1) * 8 + 255) & ~(size_t)255;
-    const size_t ub = (((size_t)S + 1) * 4 + 255) & ~(size_t)255;
-    const size_t cb = (((size_t)S + 1) * 8 + 255) & ~(size_t)255;
-    // + the fallback's list of sub-ranges, their sizes and gather offsets
-    int rc = ensure(ctx, ctx->sparse[0], stb + rb + 4 * ub + 2 * cb + 1024);
+    const size_t qb4 = (((size_t)Q + 1) * 4 + 255) & ~(size_t)255, qb8 = (((size_t)Q + 1) * 8 + 255) & ~(size_t)255;
+    int rc = ensure(ctx, ctx->sparse[0], csb + rb + qb4 + qb8 + 1024);
     if (rc) return rc;
     char* p = static_cast<char*>(ctx->sparse[0].ptr);
-    uint32_t* d_st = reinterpret_cast<uint32_t*>(p);
-    uint64_t* d_roff = reinterpret_cast<uint64_t*>(p + stb);
-    uint32_t* d_ucount = reinterpret_cast<uint32_t*>(p + stb + rb);
-    uint32_t* d_big = reinterpret_cast<uint32_t*>(p + stb + rb + ub);   // [0] = count, then sub-ranges
-    unsigned long long* d_colbase = reinterpret_cast<unsigned long long*>(p + stb + rb + 2 * ub);
-    uint32_t* d_bigs = reinterpret_cast<uint32_t*>(p + stb + rb + 2 * ub + cb);
-    uint32_t* d_sizes = reinterpret_cast<uint32_t*>(p + stb + rb + 3 * ub + cb);
-    unsigned long long* d_goff = reinterpret_cast<unsigned long long*>(p + stb + rb + 4 * ub + cb);
+    uint32_t* d_cs = reinterpret_cast<uint32_t*>(p);
+    uint64_t* d_roff = reinterpret_cast<uint64_t*>(p + csb);
+    uint32_t* d_nu = reinterpret_cast<uint32_t*>(p + csb + rb);
+    unsigned long long* d_ubase = reinterpret_cast<unsigned long long*>(p + csb + rb + qb4);
     std::vector<uint64_t> rel(R + 1);
     for (int r = 0; r <= R; ++r) rel[r] = row_off[r] - row_off[0];
     const uint64_t* codes = d_codes + row_off[0];
     KMH_HIP(ctx, hipMemcpyAsync(d_roff, rel.data(), (R + 1) * 8, hipMemcpyHostToDevice, s));
-    KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));
-    uint64_t maxlen = 0;
-    for (int r = 0; r < R; ++r) maxlen = std::max(maxlen, rel[r + 1] - rel[r]);
-    const unsigned gx = (unsigned)std::min<uint64_t>(std::max<uint64_t>((maxlen + 2047) / 2048, 1), 65535);
-    time_begin(ctx, s, "k_shard_starts");
-    hipLaunchKernelGGL(k_shard_starts, dim3(gx, (unsigned)R), dim3(256), 0, s, codes, d_roff, lo, SH, S, d_st);
-    time_end(ctx, s);
+    time_begin(ctx, s, "k_shard_plan");
+    const uint64_t ncs = (uint64_t)(Q + 1) * (uint64_t)R;
+    hipLaunchKernelGGL(k_shard_coarse, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, s, codes, d_roff, R, lo, CSH, Q,
+                       d_cs);
     KMH_HIP(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_cells, dim3((Q + 255) / 256), dim3(256), 0, s, d_cs, R, Q, d_nu);
+    KMH_HIP(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShThreads), 0, s, d_nu, Q, d_ubase);
+    KMH_HIP(ctx, hipGetLastError());
+    unsigned long long U64 = 0;
+    KMH_HIP(ctx, hipMemcpyAsync(&U64, d_ubase + Q, 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    if (U64 == 0 || U64 >= (1ull << 31)) return fail(ctx, KMH_ERR_UNSUPPORTED, "shard: unit count out of range");
+    const uint32_t S = (uint32_t)U64;
+
+    // units: first / last codes, cells; the rows' starts; union sizes, fallback list, column bases
+    const size_t stb = (((size_t)R * (S + 1) * 4) + 255) & ~(size_t)255;
+    const size_t u8 = (((size_t)S + 1) * 8 + 255) & ~(size_t)255, u4 = (((size_t)S + 1) * 4 + 255) & ~(size_t)255;
+    if ((rc = ensure(ctx, ctx->sparse[1], stb + 2 * u8 + 5 * u4 + 2 * u8 + 1024))) return rc;
+    char* p1 = static_cast<char*>(ctx->sparse[1].ptr);
+    uint32_t* d_st = reinterpret_cast<uint32_t*>(p1);
+    uint64_t* d_ub = reinterpret_cast<uint64_t*>(p1 + stb);
+    uint64_t* d_ue = reinterpret_cast<uint64_t*>(p1 + stb + u8);
+    uint32_t* d_ucell = reinterpret_cast<uint32_t*>(p1 + stb + 2 * u8);
+    uint32_t* d_ucount = reinterpret_cast<uint32_t*>(p1 + stb + 2 * u8 + u4);
+    uint32_t* d_big = reinterpret_cast<uint32_t*>(p1 + stb + 2 * u8 + 2 * u4);   // [0] = count, then units
+    uint32_t* d_bigs = reinterpret_cast<uint32_t*>(p1 + stb + 2 * u8 + 3 * u4);
+    uint32_t* d_sizes = reinterpret_cast<uint32_t*>(p1 + stb + 2 * u8 + 4 * u4);
+    unsigned long long* d_colbase = reinterpret_cast<unsigned long long*>(p1 + stb + 2 * u8 + 5 * u4);
+    unsigned long long* d_goff = reinterpret_cast<unsigned long long*>(p1 + stb + 3 * u8 + 5 * u4);
+    hipLaunchKernelGGL(k_shard_units, dim3((Q + 255) / 256), dim3(256), 0, s, d_nu, d_ubase, Q, lo, hi_incl, CSH, d_ub,
+                       d_ue, d_ucell);
+    KMH_HIP(ctx, hipGetLastError());
+    const uint64_t nus = (uint64_t)(S + 1) * (uint64_t)R;
+    hipLaunchKernelGGL(k_shard_ustarts, dim3((unsigned)((nus + 255) / 256)), dim3(256), 0, s, codes, d_roff, R, d_cs, Q,
+                       d_ub, d_ucell, S, d_st);
+    KMH_HIP(ctx, hipGetLastError());
+    KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));
+    time_end(ctx, s);
     const unsigned ug = (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * 2);
     time_begin(ctx, s, "k_shard_union");
-    hipLaunchKernelGGL(k_shard_union<false>, dim3(ug), dim3(kShThreads), 0, s, codes, d_roff, R, d_st, S, lo, SH,
+    hipLaunchKernelGGL(k_shard_union<false>, dim3(ug), dim3(kShThreads), 0, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
                        d_ucount, d_big, nullptr, nullptr, nullptr);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
@@ -521,7 +638,7 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
         for (uint32_t j = 0; j < nbig; ++j) goff[j + 1] = goff[j] + sizes[j];
         m = goff[nbig];
         if (m >= 0xFFFFFFFFull)
-            return fail(ctx, KMH_ERR_UNSUPPORTED, "shard: 2^32 or more entries in sub-ranges the LDS cannot hold");
+            return fail(ctx, KMH_ERR_UNSUPPORTED, "shard: 2^32 or more entries in units the LDS cannot hold");
         KMH_HIP(ctx, hipMemcpyAsync(d_goff, goff.data(), (nbig + 1) * 8, hipMemcpyHostToDevice, s));
         const size_t m8 = ((size_t)m * 8 + 255) & ~(size_t)255, m4 = ((size_t)m * 4 + 255) & ~(size_t)255;
         if ((rc = ensure(ctx, ctx->order, 3 * m8 + 6 * m4 + 1024))) return rc;
@@ -550,7 +667,7 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
         }
         rc = run_starts<uint64_t>(ctx, gcode, m, flags, ex, starts, nruns, s);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_shard_big_count, dim3(1024), dim3(256), 0, s, gcode, starts, nruns, lo, SH, d_ucount);
+        hipLaunchKernelGGL(k_shard_big_count, dim3(1024), dim3(256), 0, s, gcode, starts, nruns, d_ub, S, d_ucount);
         KMH_HIP(ctx, hipGetLastError());
     }
     hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShThreads), 0, s, d_ucount, S, d_colbase);
@@ -558,12 +675,12 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
     time_begin(ctx, s, "k_shard_union");
-    hipLaunchKernelGGL(k_shard_union<true>, dim3(ug), dim3(kShThreads), 0, s, codes, d_roff, R, d_st, S, lo, SH,
+    hipLaunchKernelGGL(k_shard_union<true>, dim3(ug), dim3(kShThreads), 0, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
                        d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (nbig) {
-        hipLaunchKernelGGL(k_shard_big_write, dim3(1024), dim3(256), 0, s, gcode, gval, m, starts, nruns, lo, SH,
+        hipLaunchKernelGGL(k_shard_big_write, dim3(1024), dim3(256), 0, s, gcode, gval, m, starts, nruns, d_ub, S,
                            d_colbase, gpos, d_columns, d_indices + row_off[0]);
         KMH_HIP(ctx, hipGetLastError());
     }
