@@ -1366,67 +1366,92 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
             lds_barrier();
             if constexpr (ORD) {
-                // each bin's keys in ascending order.  Bins of 2..4 keys (almost every bin that
-                // needs it: ~1 key per bin) by a sorting network in registers -- four reads per bin
-                // at addresses clamped into the bin, all of a thread's 16 bins issued together,
-                // missing keys as the largest value -- and bins of 5..BIG keys (rare; more fail the
-                // item below) by insertion in place.  (An insertion sort of every bin was a chain of
-                // dependent LDS round trips per bin slot, taken by the whole wave whenever one of
-                // its lanes had a bin to sort: the sorted count ran 2.3x the unsorted one.)
+                // each bin's keys in ascending order.  ~76 % of the bins hold 0 or 1 key, so each
+                // wave lists its threads' bins of 2..BIG keys (~250 of its 1024) in LDS (the hash
+                // table's space: ORD never hashes) and its lanes take them 64 at a time: bins of up
+                // to 4 keys by a sorting network in registers (four reads clamped into the bin, the
+                // missing keys as the largest value), larger ones (rare) by insertion.  (Sorting
+                // every bin slot of every thread, empty or not, cost 13.7 of the count's 31.8 Mcyc
+                // per wave; an insertion sort per bin before that was a chain of dependent LDS round
+                // trips per bin slot.)  A wave whose list would overflow sorts its bins in place.
                 constexpr E kTop = ~(E)0;
                 auto cswap = [](E& a, E& b) {
                     const E lo = a < b ? a : b, hi = a < b ? b : a;
                     a = lo;
                     b = hi;
                 };
-#pragma unroll
-                for (int q = 0; q < BQ; ++q) {
-                    const uint4 rq = h4[swzh_slot(BQ * tid + q)];
-                    const uint32_t rg[4] = {rq.x, rq.y, rq.z, rq.w};
-                    E kv[4][4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t bs = rg[i] & 0xFFFFu, be = rg[i] >> 16;
+                auto sort_bin = [&](uint32_t bs, uint32_t be) {   // one lane, one bin of 2..BIG keys
+                    const uint32_t n = be - bs;
+                    if (n <= 4u) {
+                        E kv[4];
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
                             const uint32_t y = bs + (uint32_t)t;
-                            kv[i][t] = sorted[swz<EPC>(y < be ? y : bs)];
+                            kv[t] = (uint32_t)t < n ? sorted[swz<EPC>(y < be ? y : bs)] : kTop;
                         }
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t bs = rg[i] & 0xFFFFu, n = (rg[i] >> 16) - bs;
-                        E a = kv[i][0], b = n > 1u ? kv[i][1] : kTop, c = n > 2u ? kv[i][2] : kTop,
-                          d = n > 3u ? kv[i][3] : kTop;
-                        cswap(a, b);
-                        cswap(c, d);
-                        cswap(a, c);
-                        cswap(b, d);
-                        cswap(b, c);
-                        if (n >= 2u && n <= 4u) {
-                            sorted[swz<EPC>(bs)] = a;
-                            sorted[swz<EPC>(bs + 1u)] = b;
-                            if (n > 2u) sorted[swz<EPC>(bs + 2u)] = c;
-                            if (n > 3u) sorted[swz<EPC>(bs + 3u)] = d;
-                        }
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t bs = rg[i] & 0xFFFFu, be = rg[i] >> 16;
-                        if (be - bs > 4u && be - bs <= (uint32_t)BIG) {
-                            for (uint32_t x = bs + 1u; x < be; ++x) {
-                                const E key = sorted[swz<EPC>(x)];
-                                uint32_t y = x;
-                                while (y > bs) {
-                                    const E o = sorted[swz<EPC>(y - 1u)];
-                                    if (o <= key) break;
-                                    sorted[swz<EPC>(y)] = o;
-                                    --y;
-                                }
-                                sorted[swz<EPC>(y)] = key;
+                        cswap(kv[0], kv[1]);
+                        cswap(kv[2], kv[3]);
+                        cswap(kv[0], kv[2]);
+                        cswap(kv[1], kv[3]);
+                        cswap(kv[1], kv[2]);
+                        sorted[swz<EPC>(bs)] = kv[0];
+                        sorted[swz<EPC>(bs + 1u)] = kv[1];
+                        if (n > 2u) sorted[swz<EPC>(bs + 2u)] = kv[2];
+                        if (n > 3u) sorted[swz<EPC>(bs + 3u)] = kv[3];
+                    } else {
+                        for (uint32_t x = bs + 1u; x < be; ++x) {
+                            const E key = sorted[swz<EPC>(x)];
+                            uint32_t y = x;
+                            while (y > bs) {
+                                const E o = sorted[swz<EPC>(y - 1u)];
+                                if (o <= key) break;
+                                sorted[swz<EPC>(y)] = o;
+                                --y;
                             }
+                            sorted[swz<EPC>(y)] = key;
                         }
                     }
+                };
+                constexpr uint32_t kList = (uint32_t)(kHSlots * sizeof(unsigned long long) / 2u / kNW);   // u16 per wave
+                uint16_t* const lst = reinterpret_cast<uint16_t*>(htab) + (uint32_t)wave * kList;
+                // (the bin ranges are read twice rather than held: 16 more registers spilled the
+                // u64 variant)
+                auto bin_range = [&](int q, int i) {
+                    const uint4 rq = h4[swzh_slot(BQ * tid + q)];
+                    return i == 0 ? rq.x : (i == 1 ? rq.y : (i == 2 ? rq.z : rq.w));
+                };
+                uint32_t need = 0u;
+#pragma unroll
+                for (int q = 0; q < BQ; ++q)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t rg = bin_range(q, i), n = (rg >> 16) - (rg & 0xFFFFu);
+                        need += (n >= 2u && n <= (uint32_t)BIG) ? 1u : 0u;
+                    }
+                const uint32_t incl = scan64(need);
+                const uint32_t wtotal = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                if (wtotal <= kList) {   // (wave-uniform)
+                    uint32_t at = incl - need;
+#pragma unroll
+                    for (int q = 0; q < BQ; ++q)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t rg = bin_range(q, i), n = (rg >> 16) - (rg & 0xFFFFu);
+                            if (n >= 2u && n <= (uint32_t)BIG) lst[at++] = (uint16_t)(BPT * tid + 4 * q + i);
+                        }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (uint32_t x = (uint32_t)lane; x < wtotal; x += 64u) {
+                        const uint32_t hb = hist[swzh((uint32_t)lst[x])];
+                        sort_bin(hb & 0xFFFFu, hb >> 16);
+                    }
+                } else {
+                    for (int q = 0; q < BQ; ++q)
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t rg = bin_range(q, i), bs = rg & 0xFFFFu, be = rg >> 16;
+                            if (be - bs >= 2u && be - bs <= (uint32_t)BIG) sort_bin(bs, be);
+                        }
                 }
                 lds_barrier();
             }

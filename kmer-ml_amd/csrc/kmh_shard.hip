@@ -29,14 +29,15 @@
 namespace kmh {
 namespace {
 
-constexpr int kShThreads = 1024;
-constexpr int kShCap = 8192;        // entries of one sub-range in LDS
-constexpr int kShBinBits = 13;
+constexpr int kShThreads = 512;     // two union workgroups per CU (~58 KiB of LDS each for up to ~500 rows)
+constexpr int kShScanThreads = 1024;
+constexpr int kShCap = 4096;        // entries of one unit in LDS
+constexpr int kShBinBits = 12;
 constexpr int kShBins = 1 << kShBinBits;
 constexpr int kShBin = 64;          // entries of one bin sorted in place (more: fallback)
 constexpr int kShMaxRows = 4096;    // organisms of one shard (LDS piece table)
 constexpr int kShRoffCache = 1024;  // row offsets kept in LDS
-constexpr int kShTarget = 6144;     // entries per unit (units of one coarse cell share its entries)
+constexpr int kShTarget = 3072;     // entries per unit (units of one coarse cell share its entries)
 constexpr int kShCoarseBits = 16;   // coarse cells: at most 2^16
 
 // First entry of row[a, b) that is >= c (row ascending).
@@ -64,12 +65,17 @@ __global__ __launch_bounds__(256) void k_shard_coarse(const uint64_t* __restrict
 
 // Units of coarse cell q: nu[q] = ceil(its entries (all rows) / kShTarget).
 __global__ __launch_bounds__(256) void k_shard_cells(const uint32_t* __restrict__ cs, int R, uint32_t Q,
+                                                     uint64_t lo, uint64_t hi_incl, int CSH,
                                                      uint32_t* __restrict__ nu) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= Q) return;
     uint64_t e = 0;
     for (int r = 0; r < R; ++r) e += cs[(uint64_t)r * (Q + 1u) + q + 1u] - cs[(uint64_t)r * (Q + 1u) + q];
-    nu[q] = (uint32_t)((e + kShTarget - 1) / kShTarget);
+    // at most one unit per code (a unit of one code holds <= R <= kShCap entries)
+    const uint64_t c0 = lo + ((uint64_t)q << CSH);
+    const uint64_t w1 = (q + 1u == Q ? hi_incl : c0 + ((1ull << CSH) - 1u)) - c0;   // width - 1
+    const uint64_t n = (e + kShTarget - 1) / kShTarget;
+    nu[q] = (uint32_t)(n == 0u ? 0u : (n - 1u > w1 ? w1 + 1u : n));
 }
 
 // The units of cell q (ubase[q] .. + nu[q]): equal code spans [ub, ue] of the cell [lo + q 2^CSH,
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(256) void k_shard_units(const uint32_t* __restrict_
     if (!n) return;
     const uint64_t c0 = lo + ((uint64_t)q << CSH);
     const uint64_t last = q + 1u == Q ? hi_incl : c0 + ((1ull << CSH) - 1u);   // the cell's last code
-    const uint64_t W = last - c0 + 1u;   // <= 2^63 (CSH <= 63); n <= W (a cell of W codes holds <= R W entries, R <= kShTarget)
+    const uint64_t W = last - c0 + 1u;   // <= 2^63 (CSH <= 63); n <= W (k_shard_cells)
     const uint64_t qw = W / n, rw = W % n;
     const uint64_t u0 = ubase[q];
     for (uint32_t j = 0; j < n; ++j) {
@@ -164,9 +170,12 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
     __shared__ __attribute__((aligned(16))) uint64_t scode[kShCap];
     __shared__ uint16_t sidx[kShCap];
     __shared__ uint32_t hist[kShBins];
-    __shared__ uint32_t pfx[kShMaxRows + 1];   // the rows' pieces: exclusive prefix of their sizes
-    __shared__ uint32_t pa[kShMaxRows];        // the pieces' first entries (relative to their rows)
-    __shared__ uint64_t sroff[kShRoffCache];  // the first rows' offsets (the rest read from memory)
+    // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), the pieces'
+    // exclusive prefix of their sizes (R + 1) and their first entries (relative to their rows)
+    extern __shared__ __attribute__((aligned(16))) uint64_t sdyn[];
+    uint64_t* const sroff = sdyn;
+    uint32_t* const pfx = reinterpret_cast<uint32_t*>(sdyn + (R < kShRoffCache ? R : kShRoffCache));
+    uint32_t* const pa = pfx + R + 1;
     __shared__ uint32_t ws[kShThreads / 64];
     __shared__ uint32_t flag;
     constexpr int PER = kShCap / kShThreads;   // entries per thread
@@ -185,6 +194,22 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
             else b = m - 1;
         }
         return a;
+    };
+    // the rows of PER gathered entries at once: up to 64 rows by counting the row starts <= i
+    // (uniform LDS reads, broadcast; no data-dependent loop), beyond by binary search
+    auto rows_of = [&](const uint32_t (&iv)[PER], int (&rv)[PER]) {
+        if (R <= 64) {   // (uniform)
+#pragma unroll
+            for (int u = 0; u < PER; ++u) rv[u] = 0;
+            for (int j = 1; j < R; ++j) {
+                const uint32_t pj = pfx[j];
+#pragma unroll
+                for (int u = 0; u < PER; ++u) rv[u] += pj <= iv[u] ? 1 : 0;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) rv[u] = row_of(iv[u]);
+        }
     };
 
     for (uint32_t s = blockIdx.x; s < S; s += gridDim.x) {
@@ -236,13 +261,17 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
         uint64_t cv[PER];
         uint32_t bv[PER];
         {
-            uint64_t at[PER];
+            uint32_t iv[PER];
+            int rv[PER];
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
-                const uint32_t i = (uint32_t)(u * kShThreads + tid), ic = i < T ? i : T - 1u;   // (T >= 1)
-                const int r = row_of(ic);
-                at[u] = row_base(r) + pa[r] + (ic - pfx[r]);
+                const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                iv[u] = i < T ? i : T - 1u;   // (T >= 1)
             }
+            rows_of(iv, rv);
+            uint64_t at[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
 #pragma unroll
             for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
         }
@@ -290,21 +319,51 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
             }
         }
         __syncthreads();
-        // 5. each bin in code order (insertion sort; ~0.5 entries per bin, at most kShBin)
+        // 5. each bin in code order, by rank: position p of a bin [bs, be) moves to bs + the
+        //    number of the bin's entries ordered before it (smaller code, or the same code at an
+        //    earlier position).  Bins of up to 4 entries (~0.75 per bin; nearly all) read those
+        //    4 slots at addresses clamped into the bin, all of a thread's positions together and
+        //    branch-free; larger bins (at most kShBin) loop.  Reads, barrier, writes.  (An
+        //    insertion sort per bin was a chain of dependent LDS round trips that the whole wave
+        //    took for every bin slot in which one of its lanes had a bin to sort.)
+        {
+            uint64_t key[PER];
+            uint16_t kix[PER];
+            uint32_t dst[PER];
 #pragma unroll
-        for (int q = 0; q < BPT; ++q) {
-            const uint32_t h = hist[BPT * tid + q], bs = h & 0xFFFFu, be = h >> 16;
-            for (uint32_t x = bs + 1u; x < be; ++x) {
-                const uint64_t key = scode[x];
-                const uint16_t ix = sidx[x];
-                uint32_t y = x;
-                while (y > bs && scode[y - 1u] > key) {
-                    scode[y] = scode[y - 1u];
-                    sidx[y] = sidx[y - 1u];
-                    --y;
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
+                key[u] = scode[pc];
+                kix[u] = sidx[pc];
+            }
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
+                const uint32_t b = (uint32_t)min((key[u] - base) >> bsh, (uint64_t)(kShBins - 1));
+                const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
+                uint32_t rk = 0u;
+                if (be - bs <= 4u) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t y = bs + (uint32_t)t;
+                        const uint64_t o = scode[y < be ? y : bs];
+                        rk += (y < be && (o < key[u] || (o == key[u] && y < pc))) ? 1u : 0u;
+                    }
+                } else {
+                    for (uint32_t y = bs; y < be; ++y) {
+                        const uint64_t o = scode[y];
+                        rk += (o < key[u] || (o == key[u] && y < pc)) ? 1u : 0u;
+                    }
                 }
-                scode[y] = key;
-                sidx[y] = ix;
+                dst[u] = p < T && be - bs > 1u ? bs + rk : 0xFFFFFFFFu;   // (single entries stay)
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                if (dst[u] != 0xFFFFFFFFu) {
+                    scode[dst[u]] = key[u];
+                    sidx[dst[u]] = kix[u];
+                }
             }
         }
         __syncthreads();
@@ -323,6 +382,14 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
             if (tid == 0) ucount[s] = U;
         } else {
             uint32_t run = hp;   // heads before this thread's positions
+            uint32_t iv[PER];
+            int rv[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t p = (uint32_t)(PER * tid + u);
+                iv[u] = p < T ? (uint32_t)sidx[p] : 0u;
+            }
+            rows_of(iv, rv);
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t p = (uint32_t)(PER * tid + u);
@@ -331,9 +398,7 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
                         columns[cb + run] = scode[p];
                         ++run;
                     }
-                    const uint32_t i = sidx[p];
-                    const int r = row_of(i);
-                    indices[row_base(r) + pa[r] + (i - pfx[r])] = (int64_t)(cb + run - 1u);
+                    indices[row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]])] = (int64_t)(cb + run - 1u);
                 }
             }
         }
@@ -342,11 +407,11 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
 }
 
 // Exclusive u64 scan of n u32 (one workgroup): out[i] = sum of in[0 .. i), out[n] = the total.
-__global__ __launch_bounds__(kShThreads) void k_shard_scan(const uint32_t* __restrict__ in, uint32_t n,
+__global__ __launch_bounds__(kShScanThreads) void k_shard_scan(const uint32_t* __restrict__ in, uint32_t n,
                                                            unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long ws[kShThreads / 64];
+    __shared__ unsigned long long ws[kShScanThreads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t per = (n + kShThreads - 1u) / kShThreads, a = min(n, tid * per), e = min(n, a + per);
+    const uint32_t per = (n + kShScanThreads - 1u) / kShScanThreads, a = min(n, tid * per), e = min(n, a + per);
     unsigned long long s = 0ull;
     for (uint32_t i = a; i < e; ++i) s += in[i];
     unsigned long long incl = s;
@@ -363,7 +428,7 @@ __global__ __launch_bounds__(kShThreads) void k_shard_scan(const uint32_t* __res
         out[i] = p;
         p += in[i];
     }
-    if (tid == kShThreads - 1u) out[n] = p;
+    if (tid == kShScanThreads - 1u) out[n] = p;
 }
 
 // Fallback, sizes: entries of every listed sub-range (big[1 .. nbig]).
@@ -537,7 +602,7 @@ int rows_compact(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, co
 
 int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
                 uint64_t hi_incl, uint64_t* d_columns, int64_t* d_indices, uint64_t* ncols, hipStream_t s) {
-    static_assert(kShMaxRows <= kShTarget, "a cell's units are never narrower than one code");
+    static_assert(kShMaxRows <= kShCap, "a unit of one code fits the LDS");
     if (R < 1 || R > kShMaxRows) return fail(ctx, KMH_ERR_UNSUPPORTED, "a shard holds 1 to 4096 organism rows");
     if (!d_codes || !row_off || !ncols || hi_incl < lo) return fail(ctx, KMH_ERR_INVALID, "bad shard arguments");
     const uint64_t T = row_off[R] - row_off[0];
@@ -575,9 +640,9 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     hipLaunchKernelGGL(k_shard_coarse, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, s, codes, d_roff, R, lo, CSH, Q,
                        d_cs);
     KMH_HIP(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_shard_cells, dim3((Q + 255) / 256), dim3(256), 0, s, d_cs, R, Q, d_nu);
+    hipLaunchKernelGGL(k_shard_cells, dim3((Q + 255) / 256), dim3(256), 0, s, d_cs, R, Q, lo, hi_incl, CSH, d_nu);
     KMH_HIP(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShThreads), 0, s, d_nu, Q, d_ubase);
+    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShScanThreads), 0, s, d_nu, Q, d_ubase);
     KMH_HIP(ctx, hipGetLastError());
     unsigned long long U64 = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&U64, d_ubase + Q, 8, hipMemcpyDeviceToHost, s));
@@ -610,8 +675,9 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));
     time_end(ctx, s);
     const unsigned ug = (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * 2);
+    const size_t dyn = (size_t)std::min(R, kShRoffCache) * 8 + (((size_t)2 * R + 1) * 4 + 15) / 16 * 16;
     time_begin(ctx, s, "k_shard_union");
-    hipLaunchKernelGGL(k_shard_union<false>, dim3(ug), dim3(kShThreads), 0, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
+    hipLaunchKernelGGL(k_shard_union<false>, dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
                        d_ucount, d_big, nullptr, nullptr, nullptr);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
@@ -670,12 +736,12 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
         hipLaunchKernelGGL(k_shard_big_count, dim3(1024), dim3(256), 0, s, gcode, starts, nruns, d_ub, S, d_ucount);
         KMH_HIP(ctx, hipGetLastError());
     }
-    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShThreads), 0, s, d_ucount, S, d_colbase);
+    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShScanThreads), 0, s, d_ucount, S, d_colbase);
     KMH_HIP(ctx, hipGetLastError());
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
     time_begin(ctx, s, "k_shard_union");
-    hipLaunchKernelGGL(k_shard_union<true>, dim3(ug), dim3(kShThreads), 0, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
+    hipLaunchKernelGGL(k_shard_union<true>, dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
                        d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
