@@ -158,7 +158,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
 // every unit into ucount (0 for a unit left to the fallback, which is listed in big).  WRITE =
 // true: the columns [colbase[s], colbase[s + 1]) and the column index of every entry.
 template <bool WRITE>
-__global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __restrict__ codes,
+__global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
                                                             const uint32_t* __restrict__ st, uint32_t S,
                                                             const uint64_t* __restrict__ ub,
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
     __shared__ __attribute__((aligned(16))) uint64_t scode[kShCap];
     __shared__ uint16_t sidx[kShCap];
     __shared__ uint32_t hist[kShBins];
+    __shared__ uint32_t colrel[WRITE ? kShCap : 1];   // WRITE: column of gathered entry i - the unit's first
     // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), the pieces'
     // exclusive prefix of their sizes (R + 1) and their first entries (relative to their rows)
     extern __shared__ __attribute__((aligned(16))) uint64_t sdyn[];
@@ -381,15 +382,11 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
         if constexpr (!WRITE) {
             if (tid == 0) ucount[s] = U;
         } else {
+            // the columns from the heads; every entry's column (relative to the unit's first)
+            // into LDS by its gathered index, then stored in gathered order: consecutive threads
+            // write consecutive entries of a row's piece (stored by sorted position they scattered
+            // over the rows' pieces)
             uint32_t run = hp;   // heads before this thread's positions
-            uint32_t iv[PER];
-            int rv[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const uint32_t p = (uint32_t)(PER * tid + u);
-                iv[u] = p < T ? (uint32_t)sidx[p] : 0u;
-            }
-            rows_of(iv, rv);
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t p = (uint32_t)(PER * tid + u);
@@ -398,22 +395,58 @@ __global__ __launch_bounds__(kShThreads) void k_shard_union(const uint64_t* __re
                         columns[cb + run] = scode[p];
                         ++run;
                     }
-                    indices[row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]])] = (int64_t)(cb + run - 1u);
+                    colrel[sidx[p]] = run - 1u;
                 }
+            }
+            __syncthreads();
+            uint32_t iv[PER];
+            int rv[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                iv[u] = i < T ? i : 0u;
+            }
+            rows_of(iv, rv);
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (int64_t)(cb + colrel[i]);
             }
         }
         __syncthreads();   // the LDS tables are rewritten by the next sub-range
     }
 }
 
-// Exclusive u64 scan of n u32 (one workgroup): out[i] = sum of in[0 .. i), out[n] = the total.
-__global__ __launch_bounds__(kShScanThreads) void k_shard_scan(const uint32_t* __restrict__ in, uint32_t n,
-                                                           unsigned long long* __restrict__ out) {
+// Exclusive u64 scan of n u32: out[i] = sum of in[0 .. i), out[n] = the total.  Blocks of 4096
+// (256 threads x 16): block sums, one workgroup scans them, then every block scans itself from its
+// base.  (A single workgroup walking 1/1024 of the input per thread took 1.45 ms for the 1.3 M
+// units of config 5.)
+constexpr int kScPer = 16, kScBlock = 256 * kScPer;
+
+__global__ __launch_bounds__(256) void k_shard_scan_sums(const uint32_t* __restrict__ in, uint32_t n,
+                                                         unsigned long long* __restrict__ bsum) {
+    __shared__ unsigned long long ws[4];
+    const uint32_t base = blockIdx.x * (uint32_t)kScBlock;
+    unsigned long long t = 0ull;
+#pragma unroll
+    for (int j = 0; j < kScPer; ++j) {
+        const uint32_t i = base + (uint32_t)j * 256u + threadIdx.x;
+        t += i < n ? in[i] : 0u;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d);
+    if ((threadIdx.x & 63u) == 0u) ws[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// In place: bsum[b] = the sum of the blocks before b; bsum[nb] = the total (one workgroup).
+__global__ __launch_bounds__(kShScanThreads) void k_shard_scan_top(unsigned long long* __restrict__ bsum, uint32_t nb) {
     __shared__ unsigned long long ws[kShScanThreads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t per = (n + kShScanThreads - 1u) / kShScanThreads, a = min(n, tid * per), e = min(n, a + per);
+    const uint32_t per = (nb + kShScanThreads - 1u) / kShScanThreads, a = min(nb, tid * per), e = min(nb, a + per);
     unsigned long long s = 0ull;
-    for (uint32_t i = a; i < e; ++i) s += in[i];
+    for (uint32_t i = a; i < e; ++i) s += bsum[i];
     unsigned long long incl = s;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -425,10 +458,42 @@ __global__ __launch_bounds__(kShScanThreads) void k_shard_scan(const uint32_t* _
     unsigned long long p = incl - s;
     for (uint32_t w = 0; w < wave; ++w) p += ws[w];
     for (uint32_t i = a; i < e; ++i) {
-        out[i] = p;
-        p += in[i];
+        const unsigned long long x = bsum[i];
+        bsum[i] = p;
+        p += x;
     }
-    if (tid == kShScanThreads - 1u) out[n] = p;
+    if (tid == kShScanThreads - 1u) bsum[nb] = p;
+}
+
+__global__ __launch_bounds__(256) void k_shard_scan_down(const uint32_t* __restrict__ in, uint32_t n,
+                                                         const unsigned long long* __restrict__ bsum, uint32_t nb,
+                                                         unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long ws[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t a = blockIdx.x * (uint32_t)kScBlock + threadIdx.x * (uint32_t)kScPer;
+    uint32_t v[kScPer];
+    unsigned long long t = 0ull;
+#pragma unroll
+    for (int j = 0; j < kScPer; ++j) {
+        v[j] = a + (uint32_t)j < n ? in[a + j] : 0u;
+        t += v[j];
+    }
+    unsigned long long incl = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long x = __shfl_up(incl, d);
+        if ((int)lane >= d) incl += x;
+    }
+    if (lane == 63u) ws[wave] = incl;
+    __syncthreads();
+    unsigned long long p = bsum[blockIdx.x] + incl - t;
+    for (uint32_t w = 0; w < wave; ++w) p += ws[w];
+#pragma unroll
+    for (int j = 0; j < kScPer; ++j) {
+        if (a + (uint32_t)j < n) out[a + j] = p;
+        p += v[j];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = bsum[nb];
 }
 
 // Fallback, sizes: entries of every listed sub-range (big[1 .. nbig]).
@@ -571,6 +636,21 @@ __global__ __launch_bounds__(256) void k_cmp_scatter(const uint64_t* __restrict_
 
 }  // namespace
 
+// out[0 .. n] = the exclusive u64 scan of in[0 .. n) and its total (k_shard_scan_*; ctx->scan_tmp).
+int scan_u32_u64(Ctx* ctx, const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s) {
+    const uint32_t nb = std::max<uint32_t>(1u, (n + kScBlock - 1) / kScBlock);
+    int rc = ensure(ctx, ctx->scan_tmp, ((size_t)nb + 1) * 8 + 256);
+    if (rc) return rc;
+    unsigned long long* bsum = static_cast<unsigned long long*>(ctx->scan_tmp.ptr);
+    hipLaunchKernelGGL(k_shard_scan_sums, dim3(nb), dim3(256), 0, s, in, n, bsum);
+    KMH_HIP(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_scan_top, dim3(1), dim3(kShScanThreads), 0, s, bsum, nb);
+    KMH_HIP(ctx, hipGetLastError());
+    hipLaunchKernelGGL(k_shard_scan_down, dim3(nb), dim3(256), 0, s, in, n, bsum, nb, out);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
 int rows_compact(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* src_off,
                  const uint64_t* src_len, int R, uint64_t* d_out_codes, uint32_t* d_out_counts,
                  const uint64_t* dst_off, hipStream_t s) {
@@ -642,8 +722,7 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     KMH_HIP(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_shard_cells, dim3((Q + 255) / 256), dim3(256), 0, s, d_cs, R, Q, lo, hi_incl, CSH, d_nu);
     KMH_HIP(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShScanThreads), 0, s, d_nu, Q, d_ubase);
-    KMH_HIP(ctx, hipGetLastError());
+    if ((rc = scan_u32_u64(ctx, d_nu, Q, d_ubase, s))) return rc;
     unsigned long long U64 = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&U64, d_ubase + Q, 8, hipMemcpyDeviceToHost, s));
     KMH_HIP(ctx, hipStreamSynchronize(s));
@@ -736,8 +815,7 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
         hipLaunchKernelGGL(k_shard_big_count, dim3(1024), dim3(256), 0, s, gcode, starts, nruns, d_ub, S, d_ucount);
         KMH_HIP(ctx, hipGetLastError());
     }
-    hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShScanThreads), 0, s, d_ucount, S, d_colbase);
-    KMH_HIP(ctx, hipGetLastError());
+    if ((rc = scan_u32_u64(ctx, d_ucount, S, d_colbase, s))) return rc;
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
     time_begin(ctx, s, "k_shard_union");
