@@ -1370,10 +1370,12 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 // wave lists its threads' bins of 2..BIG keys (~250 of its 1024) in LDS (the hash
                 // table's space: ORD never hashes) and its lanes take them 64 at a time: bins of up
                 // to 4 keys by a sorting network in registers (four reads clamped into the bin, the
-                // missing keys as the largest value), larger ones (rare) by insertion.  (Sorting
-                // every bin slot of every thread, empty or not, cost 13.7 of the count's 31.8 Mcyc
-                // per wave; an insertion sort per bin before that was a chain of dependent LDS round
-                // trips per bin slot.)  A wave whose list would overflow sorts its bins in place.
+                // missing keys as the largest value), of 5..8 by an 8-key network, larger ones (~1e-5
+                // of the bins) by insertion.  (Sorting every bin slot of every thread, empty or not,
+                // cost 13.7 of the count's 31.8 Mcyc per wave; an insertion sort per bin before that
+                // was a chain of dependent LDS round trips per bin slot, and so was insertion for the
+                // ~4 bins of 5..8 keys per wave and item, holding up a whole round of its wave.)  A
+                // wave whose list would overflow sorts its bins in place.
                 constexpr E kTop = ~(E)0;
                 auto cswap = [](E& a, E& b) {
                     const E lo = a < b ? a : b, hi = a < b ? b : a;
@@ -1398,6 +1400,21 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         sorted[swz<EPC>(bs + 1u)] = kv[1];
                         if (n > 2u) sorted[swz<EPC>(bs + 2u)] = kv[2];
                         if (n > 3u) sorted[swz<EPC>(bs + 3u)] = kv[3];
+                    } else if (n <= 8u) {   // (Batcher's 19-comparator network: no chain of LDS round trips)
+                        E kv[8];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) {
+                            const uint32_t y = bs + (uint32_t)t;
+                            kv[t] = (uint32_t)t < n ? sorted[swz<EPC>(y < be ? y : bs)] : kTop;
+                        }
+                        constexpr int net[19][2] = {{0, 1}, {2, 3}, {4, 5}, {6, 7}, {0, 2}, {1, 3}, {4, 6},
+                                                    {5, 7}, {1, 2}, {5, 6}, {0, 4}, {3, 7}, {1, 5}, {2, 6},
+                                                    {1, 4}, {3, 6}, {2, 4}, {3, 5}, {3, 4}};
+#pragma unroll
+                        for (int c = 0; c < 19; ++c) cswap(kv[net[c][0]], kv[net[c][1]]);
+#pragma unroll
+                        for (int t = 0; t < 8; ++t)
+                            if ((uint32_t)t < n) sorted[swz<EPC>(bs + (uint32_t)t)] = kv[t];
                     } else {
                         for (uint32_t x = bs + 1u; x < be; ++x) {
                             const E key = sorted[swz<EPC>(x)];

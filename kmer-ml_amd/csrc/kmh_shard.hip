@@ -157,7 +157,11 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
 // row r's piece = entries st[r][s] .. st[r][s + 1]).  WRITE = false: the number of distinct codes of
 // every unit into ucount (0 for a unit left to the fallback, which is listed in big).  WRITE =
 // true: the columns [colbase[s], colbase[s + 1]) and the column index of every entry.
-template <bool WRITE>
+// Software-pipelined over units: the next unit's row starts are loaded when a unit begins, its
+// pieces are scanned (into the other of two LDS tables) and its codes loaded right after this
+// unit's scatter, so they land during this unit's sort, heads and stores (one unit at a time per
+// workgroup waited for two global round trips per unit: latency-bound).
+template <bool WRITE, typename K>
 __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
                                                             const uint32_t* __restrict__ st, uint32_t S,
@@ -167,38 +171,31 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                             const unsigned long long* __restrict__ colbase,
                                                             uint64_t* __restrict__ columns,
                                                             int64_t* __restrict__ indices) {
-    __shared__ __attribute__((aligned(16))) uint64_t scode[kShCap];
+    // the unit's codes as offsets from its first code: u32 whenever every unit spans < 2^32 codes
+    __shared__ __attribute__((aligned(16))) K scode[kShCap];
     __shared__ uint16_t sidx[kShCap];
     __shared__ uint32_t hist[kShBins];
     __shared__ uint32_t colrel[WRITE ? kShCap : 1];   // WRITE: column of gathered entry i - the unit's first
-    // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), the pieces'
-    // exclusive prefix of their sizes (R + 1) and their first entries (relative to their rows)
+    // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), and two
+    // piece tables (this unit's, the next unit's): the pieces' exclusive prefix of their sizes
+    // (R + 1) and their first entries (relative to their rows)
     extern __shared__ __attribute__((aligned(16))) uint64_t sdyn[];
     uint64_t* const sroff = sdyn;
-    uint32_t* const pfx = reinterpret_cast<uint32_t*>(sdyn + (R < kShRoffCache ? R : kShRoffCache));
-    uint32_t* const pa = pfx + R + 1;
+    uint32_t* const ptab = reinterpret_cast<uint32_t*>(sdyn + (R < kShRoffCache ? R : kShRoffCache));
+    auto pfx_of = [&](int k) { return ptab + (uint32_t)k * (2u * (uint32_t)R + 1u); };
+    auto pa_of = [&](int k) { return ptab + (uint32_t)k * (2u * (uint32_t)R + 1u) + (uint32_t)R + 1u; };
     __shared__ uint32_t ws[kShThreads / 64];
     __shared__ uint32_t flag;
     constexpr int PER = kShCap / kShThreads;   // entries per thread
     constexpr int BPT = kShBins / kShThreads;  // bins per thread
     const int tid = threadIdx.x;
     for (int r = tid; r < R && r < kShRoffCache; r += kShThreads) sroff[r] = roff[r];
-    // (made visible by the first unit's barriers)
+    // (made visible by the first barriers)
     auto row_base = [&](int r) { return r < kShRoffCache ? sroff[r] : roff[r]; };
 
-    // row of gathered entry i: the last row whose prefix is <= i
-    auto row_of = [&](uint32_t i) {
-        int a = 0, b = R - 1;
-        while (a < b) {
-            const int m = (a + b + 1) >> 1;
-            if (pfx[m] <= i) a = m;
-            else b = m - 1;
-        }
-        return a;
-    };
-    // the rows of PER gathered entries at once: up to 64 rows by counting the row starts <= i
-    // (uniform LDS reads, broadcast; no data-dependent loop), beyond by binary search
-    auto rows_of = [&](const uint32_t (&iv)[PER], int (&rv)[PER]) {
+    // the rows of PER gathered entries at once (table k): up to 64 rows by counting the row
+    // starts <= i (uniform LDS reads, broadcast; no data-dependent loop), beyond by binary search
+    auto rows_of = [&](const uint32_t* pfx, const uint32_t (&iv)[PER], int (&rv)[PER]) {
         if (R <= 64) {   // (uniform)
 #pragma unroll
             for (int u = 0; u < PER; ++u) rv[u] = 0;
@@ -209,211 +206,292 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         } else {
 #pragma unroll
-            for (int u = 0; u < PER; ++u) rv[u] = row_of(iv[u]);
+            for (int u = 0; u < PER; ++u) {
+                int a = 0, b = R - 1;
+                while (a < b) {
+                    const int m = (a + b + 1) >> 1;
+                    if (pfx[m] <= iv[u]) a = m;
+                    else b = m - 1;
+                }
+                rv[u] = a;
+            }
         }
     };
-
-    for (uint32_t s = blockIdx.x; s < S; s += gridDim.x) {
-        // WRITE: the unit's first column, loaded now and first used after the sort
-        const unsigned long long cb = WRITE ? colbase[s] : 0ull;
-        // 1. the pieces of the rows in unit s
-        // this thread's rows: a contiguous run of at most 4 (R <= kShMaxRows), so that the
-        // block scan of the threads' sums is the rows' prefix in row order
+    // next unit's row starts: prefetched into registers when there is one row per thread
+    const bool pipe_st = R <= kShThreads;   // (uniform)
+    uint32_t sta = 0u, stb = 0u;
+    auto issue_st = [&](uint32_t u) {
+        if (pipe_st && tid < R) {
+            const uint64_t o = (uint64_t)tid * (S + 1u) + u;
+            sta = st[o];
+            stb = st[o + 1];
+        }
+    };
+    // the pieces of unit u into table k (block scan: every thread calls it); returns the entries
+    auto build = [&](uint32_t u, int k) -> uint32_t {
+        uint32_t* const pfx = pfx_of(k);
+        uint32_t* const pa = pa_of(k);
+        // (R > kShThreads: a contiguous run of rows per thread, so that the block scan of the
+        // threads' sums is the rows' prefix in row order)
         const int rq = (R + kShThreads - 1) / kShThreads, r0 = min(R, tid * rq), r1 = min(R, r0 + rq);
         uint32_t mine = 0u;
-        for (int r = r0; r < r1; ++r) {
-            const uint64_t o = (uint64_t)r * (S + 1u) + s;
-            pa[r] = st[o];
-            mine += st[o + 1] - st[o];
+        if (pipe_st) {
+            if (tid < R) {
+                pa[tid] = sta;
+                mine = stb - sta;
+            }
+        } else {
+            for (int r = r0; r < r1; ++r) {
+                const uint64_t o = (uint64_t)r * (S + 1u) + u;
+                pa[r] = st[o];
+                mine += st[o + 1] - st[o];
+            }
         }
         uint32_t T;
         uint32_t pre = block_scan(mine, ws, &T);
-        for (int r = r0; r < r1; ++r) {
-            const uint64_t o = (uint64_t)r * (S + 1u) + s;
-            pfx[r] = pre;
-            pre += st[o + 1] - st[o];
-        }
-        if (tid == 0) {
-            pfx[R] = T;
-            flag = 0u;
-        }
-        for (int q = 0; q < BPT; ++q) hist[q * kShThreads + tid] = 0u;
-        if (T > (uint32_t)kShCap) {   // (uniform) too many entries: the fallback's
-            if (!WRITE && tid == 0) {
-                ucount[s] = 0u;
-                big[1 + atomicAdd(big, 1u)] = s;
+        if (pipe_st) {
+            if (tid < R) pfx[tid] = pre;
+        } else {
+            for (int r = r0; r < r1; ++r) {
+                const uint64_t o = (uint64_t)r * (S + 1u) + u;
+                pfx[r] = pre;
+                pre += st[o + 1] - st[o];
             }
-            __syncthreads();
-            continue;
         }
-        if (T == 0u) {   // (uniform) an empty unit (a part of a coarse cell with no entries)
-            if (!WRITE && tid == 0) ucount[s] = 0u;
-            __syncthreads();
-            continue;
+        if (tid == 0) pfx[R] = T;
+        return T;
+    };
+    // the codes of a unit of T (1 .. kShCap) entries, table k (visible), all loads in flight
+    auto gather = [&](uint32_t T, int k, uint64_t (&cv)[PER]) {
+        const uint32_t* const pfx = pfx_of(k);
+        const uint32_t* const pa = pa_of(k);
+        uint32_t iv[PER];
+        int rv[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = (uint32_t)(u * kShThreads + tid);
+            iv[u] = i < T ? i : T - 1u;
         }
+        rows_of(pfx, iv, rv);
+        uint64_t at[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
+#pragma unroll
+        for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
+    };
+
+    uint32_t s = blockIdx.x;
+    if (s >= S) return;   // (whole workgroup)
+    issue_st(s);
+    uint32_t Tc = build(s, 0);
+    __syncthreads();
+    uint64_t cv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) cv[u] = 0ull;
+    if (Tc >= 1u && Tc <= (uint32_t)kShCap) gather(Tc, 0, cv);
+    unsigned long long cb = WRITE ? colbase[s] : 0ull;
+    int k = 0;
+    for (;;) {
+        const uint32_t s2 = s + gridDim.x;
+        const bool has2 = s2 < S;   // (uniform)
+        if (has2) issue_st(s2);
+        const unsigned long long cb2 = WRITE && has2 ? colbase[s2] : 0ull;
+        for (int q = 0; q < BPT; ++q) hist[q * kShThreads + tid] = 0u;
+        if (tid == 0) flag = 0u;
         __syncthreads();
-        // 2. the codes into registers, their bins counted: 13 bits over the unit's span
-        const uint64_t base = ub[s], span1 = ue[s] - base;   // span - 1
-        const int sbits = span1 ? 64 - __builtin_clzll(span1) : 0;
-        const int bsh = sbits > kShBinBits ? sbits - kShBinBits : 0;
-        // every load in flight at once: addresses first (LDS), then the loads (a load whose
-        // result feeds an LDS atomic before the next load is issued made the 8 loads of a thread
-        // 8 serial round trips), then the bins
-        uint64_t cv[PER];
-        uint32_t bv[PER];
-        {
-            uint32_t iv[PER];
-            int rv[PER];
+        const uint32_t T = Tc;
+        const bool ok = T >= 1u && T <= (uint32_t)kShCap;   // (uniform)
+        if (!ok && !WRITE && tid == 0) {   // empty (a part of a coarse cell with no entries) or too big
+            ucount[s] = 0u;
+            if (T > (uint32_t)kShCap) big[1 + atomicAdd(big, 1u)] = s;
+        }
+        bool sorted_ok = false;
+        uint64_t base = 0ull;
+        int bsh = 0;
+        if (ok) {
+            // 2. bins: 12 bits over the unit's span, counted
+            base = ub[s];
+            const uint64_t span1 = ue[s] - base;   // span - 1
+            const int sbits = span1 ? 64 - __builtin_clzll(span1) : 0;
+            bsh = sbits > kShBinBits ? sbits - kShBinBits : 0;
+            uint32_t bv[PER];
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                iv[u] = i < T ? i : T - 1u;   // (T >= 1)
+                bv[u] = (uint32_t)min((K)(cv[u] - base) >> bsh, (K)(kShBins - 1));
+                if (i < T) atomicAdd(&hist[bv[u]], 1u);
             }
-            rows_of(iv, rv);
-            uint64_t at[PER];
+            __syncthreads();
+            // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
+            {
+                uint32_t v[BPT], sum = 0u;
 #pragma unroll
-            for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
+                for (int q = 0; q < BPT; ++q) {
+                    v[q] = hist[BPT * tid + q];
+                    sum += v[q];
+                    if (v[q] > (uint32_t)kShBin) flag = 1u;
+                }
+                uint32_t tot;
+                uint32_t o = block_scan(sum, ws, &tot);
 #pragma unroll
-            for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t i = (uint32_t)(u * kShThreads + tid);
-            bv[u] = (uint32_t)min((cv[u] - base) >> bsh, (uint64_t)(kShBins - 1));
-            if (i < T) atomicAdd(&hist[bv[u]], 1u);
-        }
-        __syncthreads();
-        // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
-        {
-            uint32_t v[BPT], sum = 0u;
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) {
-                v[q] = hist[BPT * tid + q];
-                sum += v[q];
-                if (v[q] > (uint32_t)kShBin) flag = 1u;
+                for (int q = 0; q < BPT; ++q) {
+                    hist[BPT * tid + q] = o * 0x10001u;
+                    o += v[q];
+                }
             }
-            uint32_t tot;
-            uint32_t o = block_scan(sum, ws, &tot);
-#pragma unroll
-            for (int q = 0; q < BPT; ++q) {
-                hist[BPT * tid + q] = o * 0x10001u;
-                o += v[q];
-            }
-        }
-        __syncthreads();
-        if (flag) {   // (uniform)
-            if (!WRITE && tid == 0) {
+            __syncthreads();
+            sorted_ok = flag == 0u;   // (uniform)
+            if (!sorted_ok && !WRITE && tid == 0) {
                 ucount[s] = 0u;
                 big[1 + atomicAdd(big, 1u)] = s;
             }
-            __syncthreads();
-            continue;
-        }
-        // 4. scatter by bin (hist ends as start | end << 16)
+            if (sorted_ok) {
+                // 4. scatter by bin (hist ends as start | end << 16)
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t i = (uint32_t)(u * kShThreads + tid);
-            if (i < T) {
-                const uint32_t at = atomicAdd(&hist[bv[u]], 0x10000u) >> 16;
-                scode[at] = cv[u];
-                sidx[at] = (uint16_t)i;
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                    if (i < T) {
+                        const uint32_t at = atomicAdd(&hist[bv[u]], 0x10000u) >> 16;
+                        scode[at] = (K)(cv[u] - base);
+                        sidx[at] = (uint16_t)i;
+                    }
+                }
             }
         }
+        // this unit's codes are dead: the next unit's pieces, then its loads (landing during
+        // this unit's sort, heads and stores)
+        uint32_t T2 = 0u;
+        if (has2) T2 = build(s2, k ^ 1);   // (its barriers also order the scatter before the sort)
         __syncthreads();
-        // 5. each bin in code order, by rank: position p of a bin [bs, be) moves to bs + the
-        //    number of the bin's entries ordered before it (smaller code, or the same code at an
-        //    earlier position).  Bins of up to 4 entries (~0.75 per bin; nearly all) read those
-        //    4 slots at addresses clamped into the bin, all of a thread's positions together and
-        //    branch-free; larger bins (at most kShBin) loop.  Reads, barrier, writes.  (An
-        //    insertion sort per bin was a chain of dependent LDS round trips that the whole wave
-        //    took for every bin slot in which one of its lanes had a bin to sort.)
-        {
-            uint64_t key[PER];
-            uint16_t kix[PER];
-            uint32_t dst[PER];
+        if (has2 && T2 >= 1u && T2 <= (uint32_t)kShCap) gather(T2, k ^ 1, cv);
+        if (!WRITE && sorted_ok) {
+            // the union's size needs no order: position p counts iff no earlier position of its
+            // bin holds its code (bins of up to 4 entries: 4 reads clamped into the bin)
+            uint32_t nf = 0u;
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
-                key[u] = scode[pc];
-                kix[u] = sidx[pc];
-            }
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
-                const uint32_t b = (uint32_t)min((key[u] - base) >> bsh, (uint64_t)(kShBins - 1));
+                const K key = scode[pc];
+                const uint32_t b = (uint32_t)min(key >> bsh, (K)(kShBins - 1));
                 const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
-                uint32_t rk = 0u;
+                bool first = true;
                 if (be - bs <= 4u) {
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         const uint32_t y = bs + (uint32_t)t;
-                        const uint64_t o = scode[y < be ? y : bs];
-                        rk += (y < be && (o < key[u] || (o == key[u] && y < pc))) ? 1u : 0u;
+                        const K o = scode[y < be ? y : bs];
+                        first = first && !(y < pc && o == key);
                     }
                 } else {
-                    for (uint32_t y = bs; y < be; ++y) {
-                        const uint64_t o = scode[y];
-                        rk += (o < key[u] || (o == key[u] && y < pc)) ? 1u : 0u;
+                    for (uint32_t y = bs; y < pc; ++y) first = first && scode[y] != key;
+                }
+                nf += (p < T && first) ? 1u : 0u;
+            }
+            uint32_t U;
+            block_scan(nf, ws, &U);
+            if (tid == 0) ucount[s] = U;
+        }
+        if (WRITE && sorted_ok) {
+            const uint32_t* const pfx = pfx_of(k);
+            const uint32_t* const pa = pa_of(k);
+            // 5. each bin in code order, by rank: position p of a bin [bs, be) moves to bs + the
+            //    number of the bin's entries ordered before it (smaller code, or the same code at
+            //    an earlier position).  Bins of up to 4 entries (~0.75 per bin; nearly all) read
+            //    those 4 slots at addresses clamped into the bin, all of a thread's positions
+            //    together and branch-free; larger bins (at most kShBin) loop.  Reads, barrier,
+            //    writes.  (An insertion sort per bin was a chain of dependent LDS round trips that
+            //    the whole wave took for every bin slot in which one of its lanes had a bin to sort.)
+            {
+                K key[PER];
+                uint16_t kix[PER];
+                uint32_t dst[PER];
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
+                    key[u] = scode[pc];
+                    kix[u] = sidx[pc];
+                }
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
+                    const uint32_t b = (uint32_t)min(key[u] >> bsh, (K)(kShBins - 1));
+                    const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
+                    uint32_t rk = 0u;
+                    if (be - bs <= 4u) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const uint32_t y = bs + (uint32_t)t;
+                            const K o = scode[y < be ? y : bs];
+                            rk += (y < be && (o < key[u] || (o == key[u] && y < pc))) ? 1u : 0u;
+                        }
+                    } else {
+                        for (uint32_t y = bs; y < be; ++y) {
+                            const K o = scode[y];
+                            rk += (o < key[u] || (o == key[u] && y < pc)) ? 1u : 0u;
+                        }
+                    }
+                    dst[u] = p < T && be - bs > 1u ? bs + rk : 0xFFFFFFFFu;   // (single entries stay)
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    if (dst[u] != 0xFFFFFFFFu) {
+                        scode[dst[u]] = key[u];
+                        sidx[dst[u]] = kix[u];
                     }
                 }
-                dst[u] = p < T && be - bs > 1u ? bs + rk : 0xFFFFFFFFu;   // (single entries stay)
             }
             __syncthreads();
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                if (dst[u] != 0xFFFFFFFFu) {
-                    scode[dst[u]] = key[u];
-                    sidx[dst[u]] = kix[u];
-                }
-            }
-        }
-        __syncthreads();
-        // 6. run heads = the distinct codes; thread t owns positions PER t .. PER t + PER - 1
-        uint32_t hm = 0u, nh = 0u;
-#pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const uint32_t p = (uint32_t)(PER * tid + u);
-            const bool h = p < T && (p == 0u || scode[p] != scode[p - 1u]);
-            hm |= (uint32_t)h << u;
-            nh += (uint32_t)h;
-        }
-        uint32_t U;
-        const uint32_t hp = block_scan(nh, ws, &U);
-        if constexpr (!WRITE) {
-            if (tid == 0) ucount[s] = U;
-        } else {
-            // the columns from the heads; every entry's column (relative to the unit's first)
-            // into LDS by its gathered index, then stored in gathered order: consecutive threads
-            // write consecutive entries of a row's piece (stored by sorted position they scattered
-            // over the rows' pieces)
-            uint32_t run = hp;   // heads before this thread's positions
+            // 6. run heads = the distinct codes; thread t owns positions PER t .. PER t + PER - 1
+            uint32_t hm = 0u, nh = 0u;
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t p = (uint32_t)(PER * tid + u);
-                if (p < T) {
-                    if ((hm >> u) & 1u) {
-                        columns[cb + run] = scode[p];
-                        ++run;
+                const bool h = p < T && (p == 0u || scode[p] != scode[p - 1u]);
+                hm |= (uint32_t)h << u;
+                nh += (uint32_t)h;
+            }
+            uint32_t U;
+            const uint32_t hp = block_scan(nh, ws, &U);
+            {
+                // the columns from the heads; every entry's column (relative to the unit's
+                // first) into LDS by its gathered index, then stored in gathered order:
+                // consecutive threads write consecutive entries of a row's piece (stored by
+                // sorted position they scattered over the rows' pieces)
+                uint32_t run = hp;   // heads before this thread's positions
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t p = (uint32_t)(PER * tid + u);
+                    if (p < T) {
+                        if ((hm >> u) & 1u) {
+                            columns[cb + run] = base + (uint64_t)scode[p];
+                            ++run;
+                        }
+                        colrel[sidx[p]] = run - 1u;
                     }
-                    colrel[sidx[p]] = run - 1u;
+                }
+                __syncthreads();
+                uint32_t iv[PER];
+                int rv[PER];
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                    iv[u] = i < T ? i : 0u;
+                }
+                rows_of(pfx, iv, rv);
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                    if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (int64_t)(cb + colrel[i]);
                 }
             }
-            __syncthreads();
-            uint32_t iv[PER];
-            int rv[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                iv[u] = i < T ? i : 0u;
-            }
-            rows_of(iv, rv);
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (int64_t)(cb + colrel[i]);
-            }
         }
-        __syncthreads();   // the LDS tables are rewritten by the next sub-range
+        if (!has2) break;
+        __syncthreads();   // the LDS tables are rewritten by the next unit
+        s = s2;
+        Tc = T2;
+        k ^= 1;
+        cb = cb2;
     }
 }
 
@@ -754,10 +832,16 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));
     time_end(ctx, s);
     const unsigned ug = (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * 2);
-    const size_t dyn = (size_t)std::min(R, kShRoffCache) * 8 + (((size_t)2 * R + 1) * 4 + 15) / 16 * 16;
+    const size_t dyn = (size_t)std::min(R, kShRoffCache) * 8 + ((2 * ((size_t)2 * R + 1)) * 4 + 15) / 16 * 16;
     time_begin(ctx, s, "k_shard_union");
-    hipLaunchKernelGGL(k_shard_union<false>, dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
-                       d_ucount, d_big, nullptr, nullptr, nullptr);
+    // every unit lies inside one coarse cell of 2^CSH codes: u32 offsets when CSH <= 32
+    const bool narrow = CSH <= 32;
+    if (narrow)
+        hipLaunchKernelGGL((k_shard_union<false, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
+                           d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL((k_shard_union<false, uint64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
+                           d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     uint32_t nbig = 0;
@@ -819,8 +903,12 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
     time_begin(ctx, s, "k_shard_union");
-    hipLaunchKernelGGL(k_shard_union<true>, dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S, d_ub, d_ue,
-                       d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
+    if (narrow)
+        hipLaunchKernelGGL((k_shard_union<true, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
+                           d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
+    else
+        hipLaunchKernelGGL((k_shard_union<true, uint64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
+                           d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (nbig) {
