@@ -914,7 +914,7 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
     if not getattr(a, "no_matrix", False) and g_local:
         # the column-sharded matrix of these genomes, device-resident: sorted
-        # rows (kmh_count_sparse_sorted_dev), padding dropped, at N > 1 the all-to-all of code
+        # rows (kmh_count_sparse_sorted_dev, back to back), at N > 1 the all-to-all of code
         # ranges, the shard's union and CSR indices (kmh_shard_union_dev); timed apart
         del d_codes, d_counts
         torch.cuda.empty_cache()
@@ -983,7 +983,7 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
             "sorted_rows_phases": {key: round(float(np.mean([p.get(key, 0.0) for p in phases])), 2)
                                    for key in phases[-1]} if phases else {},
             "what": f"this rank's {g_local} genomes -> its column shard of the organisms x k-mers matrix "
-                    "(features.py:96-111): kmh_count_sparse_sorted_dev, padding dropped, "
+                    "(features.py:96-111): kmh_count_sparse_sorted_dev (rows in code order, back to back), "
                     + ("all-to-all of code ranges, " if world > 1 else "") + "kmh_shard_union_dev (columns + CSR)",
             "ncols": int(cols.numel()), "nnz": m.nnz, "shard_checked": ok}
 

@@ -195,26 +195,20 @@ int kmh_count_sparse_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* off
                          uint64_t* d_nkmers, void* stream);
 /* kmh_count_sparse_dev with every genome's rows in ascending code order (the organism rows of
  * the column-sharded matrix, /root/reference/kmerml/ml/features.py:96-111: its columns are the
- * sorted union of labels).  Genome g's rows are d_codes / d_counts [out_off[g], out_off[g] +
- * d_nrows[g]); d_nrows[g] counts its distinct k-mers plus padding rows, which have count 0 and
- * repeat a neighbouring code (codes stay non-decreasing; the padding is the k-mers that occur
- * more than once, so a uniform genome has almost none); d_ndistinct[g] (device) receives the
- * distinct k-mers alone.  Same arguments and limits otherwise. */
+ * sorted union of labels).  The genomes' rows are back to back from entry 0: genome g's are
+ * d_codes / d_counts [sum of d_nrows[0 .. g), + d_nrows[g]), codes strictly ascending, every
+ * count nonzero; d_nrows[g] and d_ndistinct[g] (device) both receive its distinct k-mers (since
+ * round 5 a distinct-count pass places every item first: no padding, no compaction).  The
+ * buffers need kmh_sparse_out_offsets' total, as for kmh_count_sparse_dev.  Same arguments and
+ * limits otherwise. */
 int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G,
                                 int k, int canonical, uint64_t* d_codes, uint32_t* d_counts,
                                 uint64_t* d_nrows, uint64_t* d_ndistinct, void* stream);
-/* The rows of kmh_count_sparse_sorted_dev without their padding: row r = d_codes / d_counts
- * [src_off[r], src_off[r] + src_len[r]) is written to d_out_codes / d_out_counts from dst_off[r]
- * on, its entries of count 0 dropped and the others kept in order (host offset arrays of R
- * entries; dst_off[r + 1] - dst_off[r] must hold row r's nonzero entries, d_ndistinct[r]). */
-int kmh_rows_compact_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* src_off,
-                         const uint64_t* src_len, int R, uint64_t* d_out_codes, uint32_t* d_out_counts,
-                         const uint64_t* dst_off, void* stream);
 /* One rank's column shard of the organisms x k-mers matrix for sparse k (features.py:96-111:
  * columns = the sorted union of the organisms' labels).  d_codes holds R organism rows back to
  * back, row r = d_codes[row_off[r], row_off[r + 1]) (row_off: host, R + 1 entries), each sorted
- * by code, every code in [lo_code, hi_code_incl] (the rows of kmh_count_sparse_sorted_dev without
- * their padding, cut to the rank's code range).  Writes the sorted union of the codes to
+ * by code, every code in [lo_code, hi_code_incl] (the rows of kmh_count_sparse_sorted_dev, cut to
+ * the rank's code range).  Writes the sorted union of the codes to
  * d_columns (room for row_off[R] - row_off[0] entries), the column index of every row entry to
  * d_indices[row_off[0] ..] (so row_off, these indices and the rows' counts form the shard's CSR),
  * and the union's size to *ncols (host).  1 <= R <= 4096.  Synchronises `stream`. */

@@ -366,17 +366,6 @@ int kmh_shard_union_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* r
     });
 }
 
-int kmh_rows_compact_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* src_off,
-                         const uint64_t* src_len, int R, uint64_t* d_out_codes, uint32_t* d_out_counts,
-                         const uint64_t* dst_off, void* stream) {
-    if (!ctx) return KMH_ERR_INVALID;
-    ctx->err.clear();
-    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
-    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
-        return kmh::rows_compact(ctx, d_codes, d_counts, src_off, src_len, R, d_out_codes, d_out_counts, dst_off, s);
-    });
-}
-
 uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off) {
     if (!offsets || G < 0) return 0;
     return kmh::sparse_windows(offsets, G, k, out_off);

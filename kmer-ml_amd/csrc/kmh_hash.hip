@@ -1127,7 +1127,7 @@ __device__ unsigned long long g_sp_prof[16];   // KMH_SP_PROF: per-phase clocks 
 // holds its keys; the slots past its distinct k-mers are padding (count 0, code = the pass's last
 // code, so the row stays non-decreasing).  An item with a bin of more than kBigN keys fails (the
 // sorted fallback recounts it).
-template <typename E, bool POS, bool ORD>
+template <typename E, bool POS, bool ORD, bool CNT = false>
 __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_sp_count(
     const E* __restrict__ split, const uint32_t* __restrict__ opos, const uint32_t* __restrict__ pfill,
     const CountItem* __restrict__ items, uint32_t nitems, int R, uint32_t limit,
@@ -1135,6 +1135,9 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t* __restrict__ counts, uint32_t* __restrict__ firsts, unsigned long long* __restrict__ nk,
     const uint32_t* __restrict__ gb_fail, uint32_t* __restrict__ failed) {
     static_assert(!(POS && ORD), "code order without positions only");
+    static_assert(!CNT || ORD, "the distinct-count pass belongs to the ordered count");
+    // CNT (the ordered count's first pass): no order, no stores -- each item's distinct k-mers go
+    // to firsts[item] (unused without positions), so that the second pass writes compact rows
     // ORD: out_off holds the output base of every item (item_off), not of every genome, and nk
     // receives every genome's distinct k-mers (its row length is written by k_sp_item_offsets)
     constexpr int NT = kCntThreads, kNW = NT / 64, C = Cnt<E, POS>::CAP, BPT = kBins / NT, HPT = kHSlots / NT;
@@ -1365,7 +1368,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                 if constexpr (POS) spos[at] = kp[u];
             }
             lds_barrier();
-            if constexpr (ORD) {
+            if constexpr (ORD && !CNT) {
                 // each bin's keys in ascending order.  ~76 % of the bins hold 0 or 1 key, so each
                 // wave lists its threads' bins of 2..BIG keys (~250 of its 1024) in LDS (the hash
                 // table's space: ORD never hashes) and its lanes take them 64 at a time: bins of up
@@ -1724,6 +1727,8 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
             if (fail_item) {
                 const uint32_t at = atomicAdd(&failed[0], 1u);
                 failed[1 + at] = item;
+            } else if (CNT) {
+                firsts[item] = used;
             } else if (used) {   // (ORD: nk counts the distinct k-mers; the base is item_off)
                 // (the address laundered through a VGPR: with a uniform address the compiler
                 // rewrites the atomic into a wave reduction whose result is waited for at once)
@@ -1763,7 +1768,7 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
 
         // 7. this item's stores, compacted per wave with ballot + mbcnt so that they are
         //    coalesced; keys re-read from `sorted` (the next scatter comes after a barrier)
-        if (!fail_item && used) {   // uniform
+        if (!CNT && !fail_item && used) {   // uniform
             // the wave's output base, made scalar (readfirstlane): every store below is that base
             // plus a 32-bit byte offset (no 64-bit address arithmetic per key)
             const uint64_t at = rfl64(obase + before);
@@ -1835,17 +1840,6 @@ __global__ __launch_bounds__(kCntThreads) __attribute__((amdgpu_waves_per_eu(4))
                         if constexpr (POS) firsts[o] = hmin[q * NT + tid];
                     }
                     run += (uint32_t)__popcll(m);
-                }
-            }
-            if constexpr (ORD) {
-                // padding past the item's distinct k-mers: count 0, the item's largest code (its
-                // last sorted key), so the genome's row stays non-decreasing
-                if (used < ntot) {   // (uniform)
-                    const uint64_t pad = hib | (uint64_t)sorted[swz<EPC>(ntot - 1u)];
-                    for (uint32_t i = used + (uint32_t)tid; i < ntot; i += NT) {
-                        codes[obase + i] = pad;
-                        counts[obase + i] = 0u;
-                    }
                 }
             }
         }
@@ -1933,15 +1927,15 @@ __global__ __launch_bounds__(256) void k_sp_append(const E* __restrict__ keys, c
 }
 
 // ORD: output base of every count item of a batch (items in (genome, bucket, pass) order) = the
-// genome's row offset + the keys of its earlier items, and every genome's row length nk[g] (its
-// items' keys: distinct k-mers + padding).  Three launches over chunks of kIoChunk items (one
-// workgroup each; the single-workgroup version walked 512 items per thread with uncoalesced loads:
-// 5 ms per config-5 batch): (1) chunk sums and the genomes' totals (nk, one atomic per wave when its
-// items share a genome), (2) one workgroup scans the chunk sums (cpre) and the batch's genome totals
-// (gst), (3) every item's base.
+// rows written so far (rowbase: earlier batches) + the distinct k-mers of the batch's earlier
+// items, so every genome's row follows the previous genome's, and every genome's row length
+// nk[g].  Three launches over chunks of kIoChunk items (one workgroup each; a single-workgroup
+// version walked 512 items per thread with uncoalesced loads: 5 ms per config-5 batch): (1) chunk
+// sums and the genomes' totals (nk, one atomic per wave when its items share a genome), (2) one
+// workgroup scans the chunk sums from rowbase and advances rowbase, (3) every item's base.
 constexpr int kIoPer = 16, kIoChunk = 256 * kIoPer;
 
-__global__ __launch_bounds__(256) void k_sp_io_sums(const uint32_t* __restrict__ pfill,
+__global__ __launch_bounds__(256) void k_sp_io_sums(const uint32_t* __restrict__ cnt,
                                                     const CountItem* __restrict__ items, uint32_t nci,
                                                     unsigned long long* __restrict__ csum,
                                                     unsigned long long* __restrict__ nk) {
@@ -1953,7 +1947,7 @@ __global__ __launch_bounds__(256) void k_sp_io_sums(const uint32_t* __restrict__
     bool split = false;   // this thread's items span two genomes or more
     for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) {
         const uint32_t i = a + j, gi = items[i].g;
-        const unsigned long long v = pfill[i];
+        const unsigned long long v = cnt[i];
         if (gi != g) {
             atomicAdd(&nk[g], run);
             run = 0ull;
@@ -1981,12 +1975,15 @@ __global__ __launch_bounds__(256) void k_sp_io_sums(const uint32_t* __restrict__
     if (threadIdx.x == 0) csum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// One workgroup: exclusive scans of n u64 values in place (sequential runs per thread + a block scan).
-__device__ void block_scan_u64_inplace(unsigned long long* v, uint32_t n, unsigned long long* ws) {
+// One workgroup: csum[c] = *rowbase + the sums of the chunks before c; then *rowbase += all of them.
+__global__ __launch_bounds__(1024) void k_sp_io_scan(unsigned long long* __restrict__ csum, uint32_t nch,
+                                                     unsigned long long* __restrict__ rowbase) {
+    __shared__ unsigned long long ws[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t per = (n + 1023u) / 1024u, a = min(n, tid * per), e = min(n, a + per);
+    const unsigned long long base = *rowbase;
+    const uint32_t per = (nch + 1023u) / 1024u, a = min(nch, tid * per), e = min(nch, a + per);
     unsigned long long s = 0ull;
-    for (uint32_t i = a; i < e; ++i) s += v[i];
+    for (uint32_t i = a; i < e; ++i) s += csum[i];
     unsigned long long incl = s;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1994,39 +1991,25 @@ __device__ void block_scan_u64_inplace(unsigned long long* v, uint32_t n, unsign
         if ((int)lane >= d) incl += x;
     }
     if (lane == 63u) ws[wave] = incl;
-    __syncthreads();
-    unsigned long long p = incl - s;
+    __syncthreads();   // (every thread has read *rowbase)
+    unsigned long long p = base + incl - s;
     for (uint32_t w = 0; w < wave; ++w) p += ws[w];
     for (uint32_t i = a; i < e; ++i) {
-        const unsigned long long x = v[i];
-        v[i] = p;
+        const unsigned long long x = csum[i];
+        csum[i] = p;
         p += x;
     }
-    __syncthreads();
+    if (tid == 1023u) *rowbase = p;
 }
 
-// cpre[c] = the keys of the chunks before c; gst[j] = the keys of the batch's genomes before g0 + j.
-__global__ __launch_bounds__(1024) void k_sp_io_scan(unsigned long long* __restrict__ csum, uint32_t nch,
-                                                     const unsigned long long* __restrict__ nk, int g0, int nG,
-                                                     unsigned long long* __restrict__ gst) {
-    __shared__ unsigned long long ws[16];
-    for (uint32_t j = threadIdx.x; j < (uint32_t)nG; j += 1024u) gst[j] = nk[g0 + (int)j];
-    __syncthreads();
-    block_scan_u64_inplace(csum, nch, ws);
-    block_scan_u64_inplace(gst, (uint32_t)nG, ws);
-}
-
-__global__ __launch_bounds__(256) void k_sp_io_write(const uint32_t* __restrict__ pfill,
-                                                     const CountItem* __restrict__ items, uint32_t nci,
+__global__ __launch_bounds__(256) void k_sp_io_write(const uint32_t* __restrict__ cnt, uint32_t nci,
                                                      const unsigned long long* __restrict__ cpre,
-                                                     const unsigned long long* __restrict__ gst, int g0,
-                                                     const uint64_t* __restrict__ out_off,
                                                      uint64_t* __restrict__ item_off) {
     __shared__ unsigned long long ws[4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t a = blockIdx.x * (uint32_t)kIoChunk + threadIdx.x * (uint32_t)kIoPer;
     unsigned long long s = 0ull;
-    for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) s += pfill[a + j];
+    for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) s += cnt[a + j];
     unsigned long long incl = s;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -2038,25 +2021,24 @@ __global__ __launch_bounds__(256) void k_sp_io_write(const uint32_t* __restrict_
     unsigned long long p = cpre[blockIdx.x] + incl - s;
     for (uint32_t w = 0; w < wave; ++w) p += ws[w];
     for (uint32_t j = 0; j < (uint32_t)kIoPer && a + j < nci; ++j) {
-        const uint32_t i = a + j, g = items[i].g;
-        item_off[i] = out_off[g] + (p - gst[g - (uint32_t)g0]);
-        p += pfill[i];
+        item_off[a + j] = p;
+        p += cnt[a + j];
     }
 }
 
 // ORD fallback, step 3: the runs of the sorted keys of one (genome, bucket)'s failed passes (keys
-// ascend, so their passes ascend too) into those passes' item ranges in order, then each range's
-// padding (count 0, the pass's largest code).  Count item of pass p: cbase + p.
+// ascend, so their passes ascend too) into those passes' item ranges in order (count item of pass
+// p: cbase + p).  item_n != nullptr: the count-only first pass -- each failed pass's runs (its
+// distinct k-mers) into item_n[cbase + p], nothing written.
 template <typename E>
 __global__ __launch_bounds__(256) void k_sp_append_ord(const E* __restrict__ keys, uint32_t m,
                                                        const uint32_t* __restrict__ starts,
                                                        const uint32_t* __restrict__ nruns, const uint32_t* __restrict__ pmask,
                                                        uint32_t np, int R, uint64_t hib, uint32_t cbase,
-                                                       const uint64_t* __restrict__ item_off,
-                                                       const uint32_t* __restrict__ pfill, uint64_t* __restrict__ codes,
-                                                       uint32_t* __restrict__ counts, unsigned long long* __restrict__ ndist) {
+                                                       const uint64_t* __restrict__ item_off, uint32_t* __restrict__ item_n,
+                                                       uint64_t* __restrict__ codes, uint32_t* __restrict__ counts,
+                                                       unsigned long long* __restrict__ ndist) {
     const uint32_t n = *nruns;
-    if (threadIdx.x == 0) atomicAdd(ndist, (unsigned long long)n);
     auto run_pass = [&](uint32_t r) { return pass_of<E>(keys[starts[r]], np, R); };
     auto first_run = [&](uint32_t p) {   // the first run whose pass is >= p
         uint32_t lo = 0u, hi = n;
@@ -2067,23 +2049,18 @@ __global__ __launch_bounds__(256) void k_sp_append_ord(const E* __restrict__ key
         }
         return lo;
     };
+    if (item_n) {
+        for (uint32_t p = threadIdx.x; p < np; p += 256u)
+            if ((pmask[p >> 5] >> (p & 31u)) & 1u) item_n[cbase + p] = first_run(p + 1u) - first_run(p);
+        return;
+    }
+    if (threadIdx.x == 0) atomicAdd(ndist, (unsigned long long)n);
     for (uint32_t r = threadIdx.x; r < n; r += 256u) {
         const uint32_t a = starts[r], e = r + 1u < n ? starts[r + 1u] : m;
         const uint32_t p = run_pass(r);
         const uint64_t o = item_off[cbase + p] + (r - first_run(p));
         codes[o] = hib | (uint64_t)keys[a];
         counts[o] = e - a;
-    }
-    for (uint32_t p = 0; p < np; ++p) {   // (uniform)
-        if (!((pmask[p >> 5] >> (p & 31u)) & 1u)) continue;
-        const uint32_t f = first_run(p), l = first_run(p + 1u), tot = pfill[cbase + p];
-        if (l == f || l - f >= tot) continue;
-        const uint64_t pad = hib | (uint64_t)keys[starts[l - 1u]];
-        const uint64_t base = item_off[cbase + p];
-        for (uint32_t i = l - f + threadIdx.x; i < tot; i += 256u) {
-            codes[base + i] = pad;
-            counts[base + i] = 0u;
-        }
     }
 }
 
@@ -2131,7 +2108,7 @@ template <typename E, bool POS, bool ORD>
 int fallback_passes(Ctx* ctx, uint32_t g, uint32_t b, const std::vector<uint32_t>& passes, uint32_t np, uint32_t n,
                     const E* ent, const uint32_t* epos, const uint16_t* toff, uint32_t ldt, uint64_t ta, uint64_t tb,
                     int R, uint64_t out_off, unsigned long long* nk, uint64_t* codes, uint32_t* counts,
-                    uint32_t* firsts, const uint64_t* item_off, const uint32_t* pfill, uint32_t cbase, hipStream_t s) {
+                    uint32_t* firsts, const uint64_t* item_off, uint32_t* item_n, uint32_t cbase, hipStream_t s) {
     const size_t ne = ((size_t)n * sizeof(E) + 255) & ~(size_t)255, n4 = ((size_t)n * 4 + 255) & ~(size_t)255;
     const size_t mb = ((size_t)(np + 31) / 32 * 4 + 255) & ~(size_t)255;
     int rc = ensure(ctx, ctx->sparse[5], 2 * ne + 7 * n4 + mb + 1024);
@@ -2191,7 +2168,7 @@ int fallback_passes(Ctx* ctx, uint32_t g, uint32_t b, const std::vector<uint32_t
     if (rc) return rc;
     if constexpr (ORD)
         hipLaunchKernelGGL(k_sp_append_ord<E>, dim3(1), dim3(256), 0, s, keys, m, starts, small + 1, d_mask, np, R,
-                           (uint64_t)b << R, cbase, item_off, pfill, codes, counts, nk + g);
+                           (uint64_t)b << R, cbase, item_off, item_n, codes, counts, nk + g);
     else
         hipLaunchKernelGGL((k_sp_append<E, POS>), dim3(1), dim3(256), 0, s, keys, pos, m, starts, small + 1,
                            (uint64_t)b << R, out_off, nk + g, codes, counts, firsts);
@@ -2232,7 +2209,15 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
     rc = upload_layout(ctx, L, s, &d_goff, &d_tbase);
     if (rc) return rc;
     KMH_HIP(ctx, hipMemsetAsync(d_nkmers, 0, (size_t)G * sizeof(uint64_t), s));
-    if (ORD) KMH_HIP(ctx, hipMemsetAsync(d_ndist, 0, (size_t)G * sizeof(uint64_t), s));
+    // ORD: the rows written by earlier batches (every genome's row follows the previous one's)
+    unsigned long long* d_rowbase = nullptr;
+    if (ORD) {
+        KMH_HIP(ctx, hipMemsetAsync(d_ndist, 0, (size_t)G * sizeof(uint64_t), s));
+        rc = ensure(ctx, ctx->sparse[0], 256);
+        if (rc) return rc;
+        d_rowbase = static_cast<unsigned long long*>(ctx->sparse[0].ptr);
+        KMH_HIP(ctx, hipMemsetAsync(d_rowbase, 0, 8, s));
+    }
     if (L.ntiles == 0) return KMH_OK;
     unsigned long long* const d_nk = reinterpret_cast<unsigned long long*>(ORD ? d_ndist : d_nkmers);
 
@@ -2345,7 +2330,7 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         // ORD: the items' output bases and a genome-start scratch
         const size_t nch = (nci + kIoChunk - 1) / kIoChunk;
         const size_t iob = ORD ? ((nci * 8 + 255) & ~(size_t)255) + (((size_t)nG * 8 + 255) & ~(size_t)255) +
-                                     ((nch * 8 + 255) & ~(size_t)255)
+                                     ((nch * 8 + 255) & ~(size_t)255) + ((nci * 4 + 255) & ~(size_t)255)
                                : 0;
         rc = ensure(ctx, ctx->sparse[1], sib + cib + ob + fb + iob);
         if (rc) return rc;
@@ -2385,20 +2370,91 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
             KMH_HIP(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_split_prof), z, sizeof(z)));
         }
 #endif
-        if constexpr (ORD) {   // every item's output base (its genome's earlier items' keys) and row lengths
+        // passes left to the fallback: count items whose table overflowed, and every pass of a
+        // bucket whose split overflowed; grouped by (genome, bucket): one gather + sort per bucket,
+        // however many of its passes failed (a skewed organism's largest buckets can fail every
+        // pass).  ORD's first pass (item_n set): each failed pass's distinct k-mers only.
+        std::vector<uint32_t> ids;
+        auto run_fallback = [&](uint32_t* item_n) -> int {
+            uint32_t nfail = 0;
+            std::vector<uint32_t> gbf(ngb);
+            KMH_HIP(ctx, hipMemcpyAsync(&nfail, d_failed, 4, hipMemcpyDeviceToHost, s));
+            KMH_HIP(ctx, hipMemcpyAsync(gbf.data(), d_gbfail, ngb * 4, hipMemcpyDeviceToHost, s));
+            KMH_HIP(ctx, hipStreamSynchronize(s));
+            ids.assign(nfail, 0u);
+            if (nfail) {
+                KMH_HIP(ctx, hipMemcpyAsync(ids.data(), d_failed + 1, (size_t)nfail * 4, hipMemcpyDeviceToHost, s));
+                KMH_HIP(ctx, hipStreamSynchronize(s));
+            }
+            bool any_gbf = false;
+            for (uint32_t f : gbf) any_gbf |= f != 0u;
+#ifdef KMH_EXPERIMENTS
+            if (env_long("KMH_SP_NO_FALLBACK", 0)) {   // what-if builds whose counts are wrong by design
+                nfail = 0;
+                ids.clear();
+                any_gbf = false;
+            }
+#endif
+            std::vector<CountItem> citems;
+            if (nfail || any_gbf) {  // items are only needed on the host to recount failed passes
+                citems.resize(nci);
+                KMH_HIP(ctx, hipMemcpyAsync(citems.data(), d_citems, nci * sizeof(CountItem), hipMemcpyDeviceToHost, s));
+                KMH_HIP(ctx, hipStreamSynchronize(s));
+                for (const CountItem& it : citems)
+                    if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
+            }
+            std::sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t c) {
+                return citems[a].gb != citems[c].gb ? citems[a].gb < citems[c].gb : citems[a].p < citems[c].p;
+            });
+            ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+            std::vector<uint32_t> passes;
+            for (size_t i = 0; i < ids.size();) {
+                const CountItem& it = citems[ids[i]];
+                passes.clear();
+                size_t j = i;
+                for (; j < ids.size() && citems[ids[j]].gb == it.gb; ++j) passes.push_back(citems[ids[j]].p);
+                if (!item_n) {
+                    ctx->fb_passes += passes.size();
+                    ctx->fb_groups += 1;
+                }
+                const int frc = fallback_passes<E, POS, ORD>(
+                    ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt, L.tbase[it.g] - L.tbase[g0],
+                    L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g], d_nk, d_codes, d_counts, d_firsts, d_item_off,
+                    item_n, ids[i] - it.p, s);
+                if (frc) return frc;
+                i = j;
+            }
+            return KMH_OK;
+        };
+        const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
+        if constexpr (ORD) {
+            // first pass: every item's distinct k-mers (k_sp_count without order or stores, the
+            // fallback's runs for its failed passes), then every item's output base (its genome's
+            // row offset + the distinct k-mers of its earlier items) and the row lengths: rows come
+            // out compact, no padding to drop
+            uint32_t* const d_item_n = reinterpret_cast<uint32_t*>(
+                reinterpret_cast<char*>(d_gstart) + (((size_t)nG * 8 + 255) & ~(size_t)255) + ((nch * 8 + 255) & ~(size_t)255));
+            KMH_HIP(ctx, hipMemsetAsync(d_item_n, 0, nci * 4, s));
+            time_begin(ctx, s, "k_sp_count_n");
+            hipLaunchKernelGGL((k_sp_count<E, POS, ORD, true>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos,
+                               d_pfill, d_citems, (uint32_t)nci, R, limit, d_item_off, d_codes, d_counts, d_item_n, d_nk,
+                               d_gbfail, d_failed);
+            time_end(ctx, s);
+            KMH_HIP(ctx, hipGetLastError());
+            if ((rc = run_fallback(d_item_n))) return rc;
             unsigned long long* const d_csum = d_gstart + (((size_t)nG * 8 + 255) & ~(size_t)255) / 8;
             unsigned long long* const d_rows = reinterpret_cast<unsigned long long*>(d_nkmers);
-            hipLaunchKernelGGL(k_sp_io_sums, dim3((unsigned)nch), dim3(256), 0, s, d_pfill, d_citems, (uint32_t)nci, d_csum,
-                               d_rows);
+            hipLaunchKernelGGL(k_sp_io_sums, dim3((unsigned)nch), dim3(256), 0, s, d_item_n, d_citems, (uint32_t)nci,
+                               d_csum, d_rows);
             KMH_HIP(ctx, hipGetLastError());
-            hipLaunchKernelGGL(k_sp_io_scan, dim3(1), dim3(1024), 0, s, d_csum, (uint32_t)nch, d_rows, g0, nG, d_gstart);
+            hipLaunchKernelGGL(k_sp_io_scan, dim3(1), dim3(1024), 0, s, d_csum, (uint32_t)nch, d_rowbase);
             KMH_HIP(ctx, hipGetLastError());
-            hipLaunchKernelGGL(k_sp_io_write, dim3((unsigned)nch), dim3(256), 0, s, d_pfill, d_citems, (uint32_t)nci,
-                               d_csum, d_gstart, g0, d_out_off, d_item_off);
+            hipLaunchKernelGGL(k_sp_io_write, dim3((unsigned)nch), dim3(256), 0, s, d_item_n, (uint32_t)nci, d_csum,
+                               d_item_off);
             KMH_HIP(ctx, hipGetLastError());
+            KMH_HIP(ctx, hipMemsetAsync(d_failed, 0, 4, s));
         }
         time_begin(ctx, s, "k_sp_count");
-        const unsigned cgrid = (unsigned)std::min<size_t>(nci, (size_t)std::max(1, ctx->num_cu) * 2);
         hipLaunchKernelGGL((k_sp_count<E, POS, ORD>), dim3(cgrid), dim3(kCntThreads), 0, s, d_split, d_spos, d_pfill,
                            d_citems, (uint32_t)nci, R, limit, ORD ? d_item_off : d_out_off, d_codes, d_counts, d_firsts,
                            d_nk, d_gbfail, d_failed);
@@ -2419,56 +2475,8 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
         }
 #endif
         const double h3 = hprof ? now_ms() : 0.0;
-        // passes left to the fallback: count items whose table overflowed, and every pass of
-        // a bucket whose split overflowed
-        uint32_t nfail = 0;
-        std::vector<uint32_t> gbf(ngb);
-        KMH_HIP(ctx, hipMemcpyAsync(&nfail, d_failed, 4, hipMemcpyDeviceToHost, s));
-        KMH_HIP(ctx, hipMemcpyAsync(gbf.data(), d_gbfail, ngb * 4, hipMemcpyDeviceToHost, s));
-        KMH_HIP(ctx, hipStreamSynchronize(s));
-        std::vector<uint32_t> ids(nfail);
-        if (nfail) {
-            KMH_HIP(ctx, hipMemcpyAsync(ids.data(), d_failed + 1, (size_t)nfail * 4, hipMemcpyDeviceToHost, s));
-            KMH_HIP(ctx, hipStreamSynchronize(s));
-        }
-        bool any_gbf = false;
-        for (uint32_t f : gbf) any_gbf |= f != 0u;
-#ifdef KMH_EXPERIMENTS
-        if (env_long("KMH_SP_NO_FALLBACK", 0)) {   // what-if builds whose counts are wrong by design
-            nfail = 0;
-            ids.clear();
-            any_gbf = false;
-        }
-#endif
-        std::vector<CountItem> citems;
-        if (nfail || any_gbf) {  // items are only needed on the host to recount failed passes
-            citems.resize(nci);
-            KMH_HIP(ctx, hipMemcpyAsync(citems.data(), d_citems, nci * sizeof(CountItem), hipMemcpyDeviceToHost, s));
-            KMH_HIP(ctx, hipStreamSynchronize(s));
-            for (const CountItem& it : citems)
-                if (gbf[it.gb]) ids.push_back((uint32_t)(&it - citems.data()));
-        }
-        const double h4 = hprof ? now_ms() : 0.0;
-        // the failed passes grouped by (genome, bucket): one gather + sort per bucket, however many
-        // of its passes failed (a skewed organism's largest buckets can fail every pass)
-        std::sort(ids.begin(), ids.end(), [&](uint32_t a, uint32_t c) {
-            return citems[a].gb != citems[c].gb ? citems[a].gb < citems[c].gb : citems[a].p < citems[c].p;
-        });
-        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-        std::vector<uint32_t> passes;
-        for (size_t i = 0; i < ids.size();) {
-            const CountItem& it = citems[ids[i]];
-            passes.clear();
-            size_t j = i;
-            for (; j < ids.size() && citems[ids[j]].gb == it.gb; ++j) passes.push_back(citems[ids[j]].p);
-            ctx->fb_passes += passes.size();
-            ctx->fb_groups += 1;
-            rc = fallback_passes<E, POS, ORD>(ctx, it.g, it.b, passes, it.np, it.n, ent, epos, toff, ldt,
-                                              L.tbase[it.g] - L.tbase[g0], L.tbase[it.g + 1] - L.tbase[g0], R, out_off[it.g],
-                                              d_nk, d_codes, d_counts, d_firsts, d_item_off, d_pfill, ids[i] - it.p, s);
-            if (rc) return rc;
-            i = j;
-        }
+        const double h4 = h3;
+        if ((rc = run_fallback(nullptr))) return rc;
         if (hprof)
             std::fprintf(stderr, "sparse batch host phases (ms): partition+sizes wait %.2f, items %.2f (%zu split, "
                          "%zu count), uploads+launches %.2f, split+count wait %.2f, fallback %.2f (%zu passes)\n",

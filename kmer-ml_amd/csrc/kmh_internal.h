@@ -177,11 +177,7 @@ int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offse
 // codes, d_indices[e] (for every entry e of the rows) its column; *ncols the union's size.
 int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
                 uint64_t hi_incl, uint64_t* d_columns, int64_t* d_indices, uint64_t* ncols, hipStream_t s);
-// Rows without their count-0 entries: row r = [src_off[r], + src_len[r]) of (d_codes, d_counts)
-// to [dst_off[r], ...) of the outputs, kept entries in order (host offsets).
-int rows_compact(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* src_off,
-                 const uint64_t* src_len, int R, uint64_t* d_out_codes, uint32_t* d_out_counts,
-                 const uint64_t* dst_off, hipStream_t s);
+
 
 // ---- feature columns of the feature CSV (kmh_features.hip) ----
 int feature_columns(Ctx* ctx, const uint64_t* d_codes, uint64_t n, int k, const int32_t* d_order, const double* d_lg,

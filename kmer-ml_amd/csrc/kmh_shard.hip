@@ -647,71 +647,6 @@ __global__ __launch_bounds__(256) void k_shard_big_write(const uint64_t* __restr
     }
 }
 
-// Padding out of sorted rows (kmh_count_sparse_sorted_dev's rows hold count-0 padding for the
-// k-mers that occur more than once): 4096 entries per block, kept entries in order.
-constexpr int kCmpBlock = 4096;
-constexpr int kCmpPer = kCmpBlock / 256;
-
-__global__ __launch_bounds__(256) void k_cmp_count(const uint32_t* __restrict__ counts, uint64_t n,
-                                                   uint32_t* __restrict__ bc) {
-    const uint64_t base = (uint64_t)blockIdx.x * kCmpBlock;
-    uint32_t c = 0u;
-#pragma unroll
-    for (int i = 0; i < kCmpPer; ++i) {
-        const uint64_t p = base + (uint64_t)i * 256u + threadIdx.x;
-        c += (uint32_t)(p < n && counts[p] != 0u);
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-    __shared__ uint32_t ws[4];
-    if ((threadIdx.x & 63u) == 0u) ws[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) bc[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-// Entry p = base + 256 i + t (lane-consecutive, coalesced) goes to boff[block] + (kept entries
-// before it in position order: rows i, then waves, then lanes).
-__global__ __launch_bounds__(256) void k_cmp_scatter(const uint64_t* __restrict__ codes,
-                                                     const uint32_t* __restrict__ counts, uint64_t n,
-                                                     const uint32_t* __restrict__ boff, uint64_t* __restrict__ oc,
-                                                     uint32_t* __restrict__ on) {
-    __shared__ uint32_t cw[kCmpPer * 4], pw[kCmpPer * 4];
-    const uint64_t base = (uint64_t)blockIdx.x * kCmpBlock;
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t cv[kCmpPer];
-    uint64_t mk[kCmpPer];
-#pragma unroll
-    for (int i = 0; i < kCmpPer; ++i) {
-        const uint64_t p = base + (uint64_t)i * 256u + threadIdx.x;
-        cv[i] = p < n ? counts[p] : 0u;
-        mk[i] = __ballot(cv[i] != 0u);
-        if (lane == 0u) cw[i * 4 + wave] = (uint32_t)__popcll(mk[i]);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64u) {   // exclusive scan of the 64 (row, wave) counts in position order
-        const uint32_t v = cw[threadIdx.x];
-        uint32_t x = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d);
-            if ((int)lane >= d) x += y;
-        }
-        pw[threadIdx.x] = x - v;
-    }
-    __syncthreads();
-    const uint32_t b0 = boff[blockIdx.x];
-#pragma unroll
-    for (int i = 0; i < kCmpPer; ++i) {
-        if (cv[i] != 0u) {
-            const uint64_t p = base + (uint64_t)i * 256u + threadIdx.x;
-            const uint64_t o = (uint64_t)b0 + pw[i * 4 + wave] +
-                               __builtin_amdgcn_mbcnt_hi((uint32_t)(mk[i] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk[i], 0u));
-            oc[o] = codes[p];
-            on[o] = cv[i];
-        }
-    }
-}
-
 }  // namespace
 
 // out[0 .. n] = the exclusive u64 scan of in[0 .. n) and its total (k_shard_scan_*; ctx->scan_tmp).
@@ -726,35 +661,6 @@ int scan_u32_u64(Ctx* ctx, const uint32_t* in, uint32_t n, unsigned long long* o
     KMH_HIP(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_shard_scan_down, dim3(nb), dim3(256), 0, s, in, n, bsum, nb, out);
     KMH_HIP(ctx, hipGetLastError());
-    return KMH_OK;
-}
-
-int rows_compact(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* src_off,
-                 const uint64_t* src_len, int R, uint64_t* d_out_codes, uint32_t* d_out_counts,
-                 const uint64_t* dst_off, hipStream_t s) {
-    if (R < 0 || (R && (!src_off || !src_len || !dst_off))) return fail(ctx, KMH_ERR_INVALID, "bad row arguments");
-    uint64_t maxb = 1;
-    for (int r = 0; r < R; ++r) {
-        if (src_len[r] >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "rows below 2^32 - 1 entries");
-        maxb = std::max<uint64_t>(maxb, (src_len[r] + kCmpBlock - 1) / kCmpBlock);
-    }
-    const size_t bb = ((size_t)maxb * 4 + 255) & ~(size_t)255;
-    int rc = ensure(ctx, ctx->out2, 2 * bb);
-    if (rc) return rc;
-    uint32_t* bc = static_cast<uint32_t*>(ctx->out2.ptr);
-    uint32_t* boff = reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->out2.ptr) + bb);
-    for (int r = 0; r < R; ++r) {
-        const uint64_t n = src_len[r];
-        if (!n) continue;
-        if (!d_codes || !d_counts || !d_out_codes || !d_out_counts) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
-        const unsigned nb = (unsigned)((n + kCmpBlock - 1) / kCmpBlock);
-        hipLaunchKernelGGL(k_cmp_count, dim3(nb), dim3(256), 0, s, d_counts + src_off[r], n, bc);
-        KMH_HIP(ctx, hipGetLastError());
-        if ((rc = scan_exclusive_u32(ctx, bc, boff, nb, nullptr, s))) return rc;
-        hipLaunchKernelGGL(k_cmp_scatter, dim3(nb), dim3(256), 0, s, d_codes + src_off[r], d_counts + src_off[r], n, boff,
-                           d_out_codes + dst_off[r], d_out_counts + dst_off[r]);
-        KMH_HIP(ctx, hipGetLastError());
-    }
     return KMH_OK;
 }
 

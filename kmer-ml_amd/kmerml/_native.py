@@ -66,7 +66,6 @@ SIGNATURES = [
     ("kmh_count_sparse_sorted_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp,
                                                _vp]),
     ("kmh_shard_union_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _u64, _u64, _vp, _vp, _u64p, _vp]),
-    ("kmh_rows_compact_dev", _c.c_int, [_vp, _vp, _vp, _vp, _vp, _c.c_int, _vp, _vp, _vp, _vp]),
     ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
     ("kmh_rows_encode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
@@ -291,25 +290,14 @@ class Context:
     def count_sparse_sorted_dev(self, d_seq, offsets, k, canonical, d_codes, d_counts, d_nrows, d_ndistinct,
                                 stream=None):
         """count_sparse_dev with every genome's rows in ascending code order (kmh_count_sparse_sorted_dev):
-        genome g's rows are [sparse_out_offsets(offsets, k)[g], + d_nrows[g]); rows of count 0 are
-        padding; d_ndistinct[g] = its distinct k-mers.  Synchronises the stream."""
+        the genomes' rows are back to back from entry 0 (genome g's after rows 0 .. g - 1), strictly
+        ascending; d_nrows[g] = d_ndistinct[g] = its distinct k-mers.  Synchronises the stream."""
         off = np.ascontiguousarray(offsets, dtype=np.uint64)
         _check(lib().kmh_count_sparse_sorted_dev(self._h, ctypes.c_void_p(d_seq), _ptr(off), off.size - 1, int(k),
                                                  int(bool(canonical)), ctypes.c_void_p(d_codes),
                                                  ctypes.c_void_p(d_counts), ctypes.c_void_p(d_nrows),
                                                  ctypes.c_void_p(d_ndistinct),
                                                  ctypes.c_void_p(stream) if stream else None), self._h)
-
-    @_locked
-    def rows_compact_dev(self, d_codes, d_counts, src_off, src_len, d_out_codes, d_out_counts, dst_off, stream=None):
-        """kmh_rows_compact_dev: the rows without their count-0 entries (host offset arrays)."""
-        so = np.ascontiguousarray(src_off, dtype=np.uint64)
-        sl = np.ascontiguousarray(src_len, dtype=np.uint64)
-        do = np.ascontiguousarray(dst_off, dtype=np.uint64)
-        _check(lib().kmh_rows_compact_dev(self._h, ctypes.c_void_p(d_codes), ctypes.c_void_p(d_counts), _ptr(so),
-                                          _ptr(sl), so.size, ctypes.c_void_p(d_out_codes),
-                                          ctypes.c_void_p(d_out_counts), _ptr(do),
-                                          ctypes.c_void_p(stream) if stream else None), self._h)
 
     @_locked
     def shard_union_dev(self, d_codes, row_off, lo_code, hi_code_incl, d_columns, d_indices, stream=None):

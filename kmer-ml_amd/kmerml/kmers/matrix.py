@@ -607,7 +607,7 @@ def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows
 
 def sorted_rows_dev(genome_files, k, canonical=True, device=None, group=None):
     """This rank's block of genomes counted on the GPU with every row in code order
-    (kmh_count_sparse_sorted_dev, 13 <= k <= 32), its padding dropped: returns (lo, codes, counts,
+    (kmh_count_sparse_sorted_dev, 13 <= k <= 32), back to back: returns (lo, codes, counts,
     roff) with codes / counts device tensors (int64 / int32 storage of u64 / u32) holding the rows
     back to back, row i = genome lo + i = [roff[i], roff[i + 1]) (roff: host uint64)."""
     import torch
@@ -663,18 +663,11 @@ def sorted_rows_from_device(d_seq, offsets, k, canonical=True, timings=None):
                                 nrows.data_ptr(), ndist.data_ptr(), s)
     nr, nd = nrows.cpu().numpy(), ndist.cpu().numpy()
     phase("count_ms")
+    if not np.array_equal(nr, nd):   # (the library's contract: compact rows)
+        raise RuntimeError(f"kmh_count_sparse_sorted_dev: rows of {nr.tolist()} entries for {nd.tolist()} distinct")
     roff = np.zeros(n + 1, np.uint64)
     roff[1:] = np.cumsum(nd)
-    if all(int(out_off[g]) == int(roff[g]) and nr[g] == nd[g] for g in range(n)):
-        return codes, counts, roff   # back to back already, no padding: no copy
-    c2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int64, device=dev)
-    n2 = torch.empty(max(int(roff[-1]), 1), dtype=torch.int32, device=dev)
-    phase("alloc_ms")
-    # the padding (count-0 rows) dropped on the device, rows back to back (kmh_rows_compact_dev)
-    ctx.rows_compact_dev(codes.data_ptr(), counts.data_ptr(), out_off[:n], nr.astype(np.uint64), c2.data_ptr(),
-                         n2.data_ptr(), roff[:n], s)
-    phase("compact_ms")
-    return c2, n2, roff
+    return codes, counts, roff   # back to back from entry 0
 
 
 def _row_histogram(codes, roff, k, nbits=16):

@@ -1279,9 +1279,10 @@ def test_sparse_skewed_bucket_fallback_grouped(ctx, oracle_lib, monkeypatch):
 
 # ---------------------------------------------------------------- sorted rows and the column shard (config 5's matrix)
 def _sparse_sorted(ctx, dev, genomes, k, canonical):
-    """kmh_count_sparse_sorted_dev on host genomes -> per genome (codes, counts) with the padding
-    dropped, after checking the row contract: codes non-decreasing over the whole row (padding
-    included), padding = count 0, d_ndistinct = the rows of nonzero count."""
+    """kmh_count_sparse_sorted_dev on host genomes -> per genome (codes, counts), after checking the
+    row contract: rows back to back from entry 0 (row g starts after rows 0 .. g - 1), d_nrows[g] =
+    d_ndistinct[g] entries (no padding since round 5: a distinct-count pass places every item),
+    codes strictly ascending, every count nonzero, nothing written past the rows."""
     buf, offs = _layout(genomes)
     d_seq = torch.from_numpy(buf.copy()).to(dev)
     out_off = _native.sparse_out_offsets(offs, k)
@@ -1297,15 +1298,16 @@ def _sparse_sorted(ctx, dev, genomes, k, canonical):
     codes = d_codes.cpu().numpy().view(np.uint64)
     counts = d_counts.cpu().numpy().view(np.uint32)
     res = []
+    a = 0
+    assert np.all(counts[int(nr.sum()):] == np.uint32(0xFFFFFFF9))   # (the -7 fill)
     for g in range(len(genomes)):
-        a, n = int(out_off[g]), int(nr[g])
-        assert 0 <= nd[g] <= n <= int(out_off[g + 1]) - a, g
+        n = int(nr[g])
+        assert 0 <= n == int(nd[g]) <= int(out_off[g + 1]) - int(out_off[g]), g
         c, m = codes[a:a + n], counts[a:a + n]
-        assert np.all(c[1:] >= c[:-1]), g                  # the row in code order, padding included
-        keep = m != 0
-        assert int(keep.sum()) == int(nd[g]), g
-        assert np.all(c[keep][1:] > c[keep][:-1]), g       # distinct k-mers strictly ascending
-        res.append((c[keep], m[keep]))
+        a += n
+        assert np.all(c[1:] > c[:-1]), g                   # distinct k-mers strictly ascending
+        assert np.all(m != 0), g
+        res.append((c, m))
     return res
 
 
@@ -1365,13 +1367,17 @@ def _shard_union(ctx, dev, rows, lo, hi_incl):
     return c, [ix[int(roff[r]):int(roff[r + 1])] for r in range(len(rows))]
 
 
-@pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow"])
+@pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow", "wide", "many_rows", "dense_cell"])
 def test_shard_union_vs_numpy(ctx, dev, case):
     """kmh_shard_union_dev (the column union and CSR indices of a shard) against numpy's
     union1d / searchsorted: rows of distinct codes (the LDS path), rows sharing half their codes,
-    100 identical rows (every bin over its limit: the radix-sort fallback for every sub-range),
-    a mixture with empty rows, and a narrow code range (sub-ranges of one code)."""
-    rng = np.random.default_rng({"distinct": 1, "shared": 2, "identical": 3, "mixed": 4, "narrow": 5}[case])
+    100 identical rows (every bin over its limit: the radix-sort fallback for every unit; rows
+    found by binary search, R > 64), a mixture with empty rows, a narrow code range (units of one
+    code), the whole 64-bit code space (coarse cells of 2^48 codes: u64 offsets in the union),
+    600 rows (R > 512: row starts read without prefetch) and one dense cluster of codes inside a
+    sparse range (a coarse cell cut into many units)."""
+    rng = np.random.default_rng({"distinct": 1, "shared": 2, "identical": 3, "mixed": 4, "narrow": 5, "wide": 6,
+                                 "many_rows": 7, "dense_cell": 8}[case])
     lo, hi = 1 << 40, (1 << 41) - 1
     if case == "distinct":
         rows = [np.unique(rng.integers(lo, hi, 200_000, dtype=np.uint64)) for _ in range(7)]
@@ -1386,9 +1392,20 @@ def test_shard_union_vs_numpy(ctx, dev, case):
         one = np.unique(rng.integers(lo, hi, 30_000, dtype=np.uint64))
         rows = [np.zeros(0, np.uint64), one, np.unique(rng.integers(lo, hi, 90_000, dtype=np.uint64))] + \
                [one.copy() for _ in range(40)] + [np.zeros(0, np.uint64)]
-    else:
+    elif case == "narrow":
         lo, hi = 5_000_000, 5_003_999
         rows = [np.unique(rng.integers(lo, hi + 1, 3_000, dtype=np.uint64)) for _ in range(9)]
+    elif case == "wide":
+        lo, hi = 0, (1 << 64) - 1
+        rows = [np.unique(rng.integers(0, 1 << 63, 150_000, dtype=np.uint64) * np.uint64(2) + np.uint64(r % 2))
+                for r in range(6)]
+        rows[0] = np.unique(np.concatenate([rows[0], np.array([0, hi], np.uint64)]))   # both ends of the range
+    elif case == "many_rows":
+        pool = rng.integers(lo, hi, 200_000, dtype=np.uint64)
+        rows = [np.unique(rng.choice(pool, 500)) for _ in range(600)]
+    else:   # dense_cell: 400 K codes in a 1 M-code window of a 2^40 range, plus a sparse background
+        dense = lo + (1 << 39) + rng.integers(0, 1 << 20, 400_000, dtype=np.uint64)
+        rows = [np.unique(np.concatenate([dense[r::3], rng.integers(lo, hi, 5_000, dtype=np.uint64)])) for r in range(3)]
     cols, idx = _shard_union(ctx, dev, rows, lo, hi)
     want = np.unique(np.concatenate(rows))
     assert np.array_equal(cols, want)
