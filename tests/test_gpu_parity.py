@@ -1328,8 +1328,9 @@ def test_sparse_sorted_dev_vs_oracle(ctx, dev, oracle_lib, k, canonical):
 @pytest.mark.parametrize("k", [21, 27])
 def test_sparse_sorted_dev_fallback_and_repeats(ctx, dev, oracle_lib, monkeypatch, k):
     """The sorted rows when passes fail: tables capped so that most passes go to the sort
-    fallback (whose runs land in their passes' ranges in order, padding behind them), repeats
-    whose big bins fail an item in sorted mode, one genome per batch, and low-complexity genomes."""
+    fallback (counted in the distinct-count pass, then its runs placed in their passes' ranges in
+    order), repeats whose big bins fail an item in sorted mode, one genome per batch (rows back to
+    back across batches), and low-complexity genomes."""
     rng = np.random.default_rng(77 + k)
     seg = osynth.synth_bases(2000, osynth.genome_seed(71))
     parts = []
