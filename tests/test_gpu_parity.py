@@ -1368,17 +1368,19 @@ def _shard_union(ctx, dev, rows, lo, hi_incl):
     return c, [ix[int(roff[r]):int(roff[r + 1])] for r in range(len(rows))]
 
 
-@pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow", "wide", "many_rows", "dense_cell"])
+@pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow", "wide", "many_rows", "dense_cell",
+                                  "max_rows"])
 def test_shard_union_vs_numpy(ctx, dev, case):
     """kmh_shard_union_dev (the column union and CSR indices of a shard) against numpy's
     union1d / searchsorted: rows of distinct codes (the LDS path), rows sharing half their codes,
     100 identical rows (every bin over its limit: the radix-sort fallback for every unit; rows
     found by binary search, R > 64), a mixture with empty rows, a narrow code range (units of one
     code), the whole 64-bit code space (coarse cells of 2^48 codes: u64 offsets in the union),
-    600 rows (R > 512: row starts read without prefetch) and one dense cluster of codes inside a
-    sparse range (a coarse cell cut into many units)."""
+    600 rows (R > 512: row starts read without prefetch), one dense cluster of codes inside a
+    sparse range (a coarse cell cut into many units) and the API's 4096 rows (row offsets past the
+    first 1024 read from memory; ~74 KiB of dynamic LDS beside the static tables)."""
     rng = np.random.default_rng({"distinct": 1, "shared": 2, "identical": 3, "mixed": 4, "narrow": 5, "wide": 6,
-                                 "many_rows": 7, "dense_cell": 8}[case])
+                                 "many_rows": 7, "dense_cell": 8, "max_rows": 9}[case])
     lo, hi = 1 << 40, (1 << 41) - 1
     if case == "distinct":
         rows = [np.unique(rng.integers(lo, hi, 200_000, dtype=np.uint64)) for _ in range(7)]
@@ -1404,6 +1406,10 @@ def test_shard_union_vs_numpy(ctx, dev, case):
     elif case == "many_rows":
         pool = rng.integers(lo, hi, 200_000, dtype=np.uint64)
         rows = [np.unique(rng.choice(pool, 500)) for _ in range(600)]
+    elif case == "max_rows":
+        pool = rng.integers(lo, hi, 100_000, dtype=np.uint64)
+        rows = [np.unique(rng.choice(pool, 40)) for _ in range(4096)]
+        rows[4000] = np.zeros(0, np.uint64)
     else:   # dense_cell: 400 K codes in a 1 M-code window of a 2^40 range, plus a sparse background
         dense = lo + (1 << 39) + rng.integers(0, 1 << 20, 400_000, dtype=np.uint64)
         rows = [np.unique(np.concatenate([dense[r::3], rng.integers(lo, hi, 5_000, dtype=np.uint64)])) for r in range(3)]
