@@ -161,7 +161,7 @@ def test_format_lines_empty():
 
 def test_write_file_plain_and_parallel_gzip(tmp_path):
     """kmh_write_file: plain bytes, and multi-member gzip that any reader decompresses to the
-    same bytes (blocks of 8 MiB deflated on several threads)."""
+    same bytes (blocks of 2 MiB deflated on several threads)."""
     import gzip
     rng = np.random.default_rng(0)
     data = ("".join(f"{x}\t{y}\n" for x, y in zip(rng.integers(0, 10**12, 1_300_000),
