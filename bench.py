@@ -582,8 +582,10 @@ def main():
             qlo, qhi = (am.G * q) // span, (am.G * (q + 1)) // span
             full[q * B:q * B + (qhi - qlo)] = am.rows(qlo, qhi)
     if sim:
-        rows = full.view(span, B, bins)[:, :g_local].reshape(-1, bins)
-        ok_sim = all(torch.equal(full[q * B:q * B + g_local], last[:g_local]) for q in range(span))
+        # (--sim-copy none writes only the rank's own slot: the others stay unwritten)
+        nq = span if a.sim_copy == "torch" else 1
+        rows = full.view(span, B, bins)[:nq, :g_local].reshape(-1, bins)
+        ok_sim = all(torch.equal(full[q * B:q * B + g_local], last[:g_local]) for q in range(nq))
     elif assemble:   # every rank's block of the assembled matrix (blocks padded to B rows)
         idx = [q * B + i for q in range(world) for i in range((G * (q + 1)) // world - (G * q) // world)]
         rows = full[torch.tensor(idx, dtype=torch.long, device=full.device)]
