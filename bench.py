@@ -46,6 +46,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--min-warmup-ms", type=float, default=60.0,
+                   help="dense workload: after the --warmup steps, more untimed steps until the warm-up "
+                        "has run this long (the same number on every rank).  The GPU takes ~30-50 ms "
+                        "of load to reach its steady rate: one N = 8 rank (1.2 ms steps) measured "
+                        "1.20-1.21 ms per step after 3 warm-up steps and 1.13-1.14 after 30 "
+                        "(profiles/r05/r05ae, r05af); config 3's 8 ms steps are steady after 3.  0 = off; "
+                        "the line reports the steps run as warmup_steps_run")
     p.add_argument("--workload", choices=["dense", "sparse"], default="dense",
                    help="dense = configs 3/4 (default); sparse = config 5 (k = 21 canonical, "
                         "250 Mbp genomes, 16 per GPU, no collective)")
@@ -533,10 +540,35 @@ def main():
             while pending:
                 finish(*pending.pop())
 
+    tw = time.perf_counter()
     for i in range(a.warmup):
         step(i)
     drain()
     torch.cuda.synchronize()
+    warm_run = a.warmup
+    if a.min_warmup_ms > 0:
+        # steps to add so that the warm-up lasts min_warmup_ms, agreed on by every rank (each step
+        # holds a collective at N > 1)
+        done_ms = (time.perf_counter() - tw) * 1e3
+        if a.warmup == 0:
+            t1 = time.perf_counter()
+            step(0)
+            drain()
+            torch.cuda.synchronize()
+            warm_run, per = 1, (time.perf_counter() - t1) * 1e3
+            done_ms += per
+        else:
+            per = done_ms / a.warmup
+        extra = min(10_000, max(0, int(np.ceil((a.min_warmup_ms - done_ms) / max(per, 1e-3)))))
+        if world > 1:
+            t = torch.tensor([extra], dtype=torch.int64, device=dev if not gloo else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            extra = int(t.item())
+        for i in range(warm_run, warm_run + extra):
+            step(i)
+        drain()
+        torch.cuda.synchronize()
+        warm_run += extra
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -645,8 +677,8 @@ def main():
         count_rate = g_local * L / (count_ms * 1e-3)
         out = {
             "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "steps": a.steps, "warmup": a.warmup, "warmup_steps_run": warm_run, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": workload_name(G, L, k, world, a.single_device, a.backend),
                        "genomes": G, "genome_len": L, "k": k,
                        "parallelism": f"genome-sharded x{world}" + (f" + {mode} allgather" if assemble else ""),
