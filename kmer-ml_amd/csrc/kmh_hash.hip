@@ -13,7 +13,7 @@
 //                     bucket-major offset table toff[bucket][tile] (u16 entry indices).
 //  2. k_sp_sizes      entries per (genome, bucket); k_sp_plan (one workgroup, on the device)
 //     k_sp_plan       splits every bucket into P = ceil(entries / 7680) passes over equal
-//     k_sp_fill       residue ranges (one count item each) and into split items of ~12K
+//     k_sp_fill       residue ranges (one count item each) and into split items of ~13-16K
 //                     entries (ranges of tiles); k_sp_fill writes the items.  The host reads
 //                     back only the two item totals.
 //  3. k_sp_split      one workgroup per split item: gathers the bucket's segments of its
@@ -2228,7 +2228,10 @@ int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offset
     // room for the spread of the pass sizes around it.
     const uint32_t target = (uint32_t)std::max<long>(
         1, env_long("KMH_SP_TARGET", (sizeof(E) == 4 ? 7680 : 3840) / (POS ? 2 : 1)));
-    const uint32_t split_target = (uint32_t)std::max<long>(1, std::min<long>(env_long("KMH_SP_SPLIT", 12288), kCaps));
+    // Entries per split item (capped by the staging, and by ts <= one queue step per wave in GbRule):
+    // 16384 against 12288 cut the config-5 split 10.9 -> 10.1 ms (fewer items: fewer reservation
+    // round trips and barriers; profiles/r05/r05ah, r05ai); 14336-20480 measured within 0.2 ms.
+    const uint32_t split_target = (uint32_t)std::max<long>(1, std::min<long>(env_long("KMH_SP_SPLIT", 16384), kCaps));
     // KMH_SP_LIMIT caps the distinct keys of one item (tests force the fallback with it)
     const uint32_t limit = (uint32_t)std::min<long>(std::max<long>(1, env_long("KMH_SP_LIMIT", Cnt<E, POS>::CAP)),
                                                     Cnt<E, POS>::CAP);

@@ -10,7 +10,7 @@ python3 -c "import sys; sys.path.insert(0, 'kmer-ml_amd'); from kmerml import _n
 timeout -k 10 400 python3 -u bench.py > $OUT/bench.log 2>&1 || exit 12
 tail -c 300 $OUT/bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 bench.py --steps 10 --warmup 3 --cpu-sample 0 --no-e2e --no-matrix > $OUT/trace.log 2>&1 || exit 13
-B="bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-e2e --no-matrix"
+B="bench.py --steps 2 --warmup 1 --min-warmup-ms 0 --cpu-sample 0 --no-e2e --no-matrix"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/f -o f -- python3 $B > $OUT/f.log 2>&1 || exit 14
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/w -o w -- python3 $B > $OUT/w.log 2>&1 || exit 15
 timeout -k 10 300 python3 -u bench.py --simulate-ranks 8 --steps 20 --warmup 5 --cpu-sample 0 --no-e2e --no-config5 > $OUT/sim8.log 2>&1 || exit 16
