@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                             int64_t* __restrict__ indices) {
     // the unit's codes as offsets from its first code: u32 whenever every unit spans < 2^32 codes
     __shared__ __attribute__((aligned(16))) K scode[kShCap];
-    __shared__ uint16_t sidx[kShCap];
+    __shared__ __attribute__((aligned(16))) uint16_t sidx[kShCap];
     __shared__ uint32_t hist[kShBins];
     __shared__ uint32_t colrel[WRITE ? kShCap : 1];   // WRITE: column of gathered entry i - the unit's first
     // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), and two
@@ -186,6 +186,8 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     auto pa_of = [&](int k) { return ptab + (uint32_t)k * (2u * (uint32_t)R + 1u) + (uint32_t)R + 1u; };
     __shared__ uint32_t ws[kShThreads / 64];
     __shared__ uint32_t flag;
+    // up to 64 rows: the row holding gathered entry 64 m of piece table k (rtab[k][m])
+    __shared__ uint8_t rtab[2][kShCap / 64];
     constexpr int PER = kShCap / kShThreads;   // entries per thread
     constexpr int BPT = kShBins / kShThreads;  // bins per thread
     const int tid = threadIdx.x;
@@ -193,16 +195,17 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     // (made visible by the first barriers)
     auto row_base = [&](int r) { return r < kShRoffCache ? sroff[r] : roff[r]; };
 
-    // the rows of PER gathered entries at once (table k): up to 64 rows by counting the row
-    // starts <= i (uniform LDS reads, broadcast; no data-dependent loop), beyond by binary search
-    auto rows_of = [&](const uint32_t* pfx, const uint32_t (&iv)[PER], int (&rv)[PER]) {
+    // the rows of PER gathered entries at once (table k): up to 64 rows, the row of the entry's
+    // 64-entry slot (rtab, written by build) and then over the row starts up to the entry (a
+    // 64-entry window crosses about T / R / 64 of them; counting all R row starts per entry cost
+    // 2 (R - 1) VALU operations); beyond 64 rows by binary search
+    auto rows_of = [&](const uint32_t* pfx, const uint8_t* rt, const uint32_t (&iv)[PER], int (&rv)[PER]) {
         if (R <= 64) {   // (uniform)
 #pragma unroll
-            for (int u = 0; u < PER; ++u) rv[u] = 0;
-            for (int j = 1; j < R; ++j) {
-                const uint32_t pj = pfx[j];
-#pragma unroll
-                for (int u = 0; u < PER; ++u) rv[u] += pj <= iv[u] ? 1 : 0;
+            for (int u = 0; u < PER; ++u) {
+                int r = rt[iv[u] >> 6];
+                while (r + 1 < R && pfx[r + 1] <= iv[u]) ++r;
+                rv[u] = r;
             }
         } else {
 #pragma unroll
@@ -259,10 +262,16 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
         if (tid == 0) pfx[R] = T;
+        if (R <= 64 && tid < R && mine) {   // (one row per thread) the 64-entry slots starting in this row
+            // (a unit over kShCap entries is not gathered: its slots past the table are skipped)
+            for (uint32_t m = (pre + 63u) >> 6; (m << 6) < pre + mine && m < (uint32_t)(kShCap / 64); ++m)
+                rtab[k][m] = (uint8_t)tid;
+        }
         return T;
     };
-    // the codes of a unit of T (1 .. kShCap) entries, table k (visible), all loads in flight
-    auto gather = [&](uint32_t T, int k, uint64_t (&cv)[PER]) {
+    // the codes of a unit of T (1 .. kShCap) entries, table k (visible), all loads in flight;
+    // WRITE with up to 64 rows: the entries' rows packed a byte each into rk, for the index stores
+    auto gather = [&](uint32_t T, int k, uint64_t (&cv)[PER], uint32_t (&rk)[2]) {
         const uint32_t* const pfx = pfx_of(k);
         const uint32_t* const pa = pa_of(k);
         uint32_t iv[PER];
@@ -272,7 +281,11 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             const uint32_t i = (uint32_t)(u * kShThreads + tid);
             iv[u] = i < T ? i : T - 1u;
         }
-        rows_of(pfx, iv, rv);
+        rows_of(pfx, rtab[k], iv, rv);
+        if (WRITE && R <= 64) {
+            rk[0] = (uint32_t)rv[0] | (uint32_t)rv[1] << 8 | (uint32_t)rv[2] << 16 | (uint32_t)rv[3] << 24;
+            rk[1] = (uint32_t)rv[4] | (uint32_t)rv[5] << 8 | (uint32_t)rv[6] << 16 | (uint32_t)rv[7] << 24;
+        }
         uint64_t at[PER];
 #pragma unroll
         for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
@@ -288,7 +301,8 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     uint64_t cv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) cv[u] = 0ull;
-    if (Tc >= 1u && Tc <= (uint32_t)kShCap) gather(Tc, 0, cv);
+    uint32_t rk[2] = {0u, 0u}, rk2[2] = {0u, 0u};   // (this unit's rows, the next unit's)
+    if (Tc >= 1u && Tc <= (uint32_t)kShCap) gather(Tc, 0, cv, rk);
     unsigned long long cb = WRITE ? colbase[s] : 0ull;
     int k = 0;
     for (;;) {
@@ -363,7 +377,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         uint32_t T2 = 0u;
         if (has2) T2 = build(s2, k ^ 1);   // (its barriers also order the scatter before the sort)
         __syncthreads();
-        if (has2 && T2 >= 1u && T2 <= (uint32_t)kShCap) gather(T2, k ^ 1, cv);
+        if (has2 && T2 >= 1u && T2 <= (uint32_t)kShCap) gather(T2, k ^ 1, cv, rk2);
         if (!WRITE && sorted_ok) {
             // the union's size needs no order: position p counts iff no earlier position of its
             // bin holds its code (bins of up to 4 entries: 4 reads clamped into the bin)
@@ -442,12 +456,32 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 }
             }
             __syncthreads();
-            // 6. run heads = the distinct codes; thread t owns positions PER t .. PER t + PER - 1
+            // 6. run heads = the distinct codes; thread t owns positions PER t .. PER t + PER - 1,
+            //    read as 16-byte vectors (PER single reads at a stride of PER words were 8-way bank
+            //    conflicts); positions past T hold stale codes and are masked
+            static_assert(PER == 8, "a thread's positions are two (u32) or four (u64) 16-byte reads");
+            K kv[PER];
+            {
+                const uint4* const sv = reinterpret_cast<const uint4*>(scode + PER * tid);
+                if constexpr (sizeof(K) == 4) {
+                    const uint4 a = sv[0], b = sv[1];
+                    kv[0] = a.x; kv[1] = a.y; kv[2] = a.z; kv[3] = a.w;
+                    kv[4] = b.x; kv[5] = b.y; kv[6] = b.z; kv[7] = b.w;
+                } else {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const uint4 a = sv[w];
+                        kv[2 * w] = (K)a.x | ((K)a.y << 32);
+                        kv[2 * w + 1] = (K)a.z | ((K)a.w << 32);
+                    }
+                }
+            }
+            const K prev = tid ? scode[PER * tid - 1] : (K)0;
             uint32_t hm = 0u, nh = 0u;
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t p = (uint32_t)(PER * tid + u);
-                const bool h = p < T && (p == 0u || scode[p] != scode[p - 1u]);
+                const bool h = p < T && (p == 0u || kv[u] != (u ? kv[u - 1] : prev));
                 hm |= (uint32_t)h << u;
                 nh += (uint32_t)h;
             }
@@ -459,26 +493,33 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 // consecutive threads write consecutive entries of a row's piece (stored by
                 // sorted position they scattered over the rows' pieces)
                 uint32_t run = hp;   // heads before this thread's positions
+                const uint4 ix = *reinterpret_cast<const uint4*>(sidx + PER * tid);
+                const uint32_t ixw[4] = {ix.x, ix.y, ix.z, ix.w};
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t p = (uint32_t)(PER * tid + u);
                     if (p < T) {
                         if ((hm >> u) & 1u) {
-                            columns[cb + run] = base + (uint64_t)scode[p];
+                            columns[cb + run] = base + (uint64_t)kv[u];
                             ++run;
                         }
-                        colrel[sidx[p]] = run - 1u;
+                        colrel[(ixw[u >> 1] >> (16 * (u & 1))) & 0xFFFFu] = run - 1u;
                     }
                 }
                 __syncthreads();
-                uint32_t iv[PER];
                 int rv[PER];
+                if (R <= 64) {   // (uniform) the rows found by the gather
 #pragma unroll
-                for (int u = 0; u < PER; ++u) {
-                    const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                    iv[u] = i < T ? i : 0u;
+                    for (int u = 0; u < PER; ++u) rv[u] = (int)((rk[u >> 2] >> (8 * (u & 3))) & 0xFFu);
+                } else {
+                    uint32_t iv[PER];
+#pragma unroll
+                    for (int u = 0; u < PER; ++u) {
+                        const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                        iv[u] = i < T ? i : 0u;
+                    }
+                    rows_of(pfx, rtab[k], iv, rv);
                 }
-                rows_of(pfx, iv, rv);
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t i = (uint32_t)(u * kShThreads + tid);
@@ -492,6 +533,8 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         Tc = T2;
         k ^= 1;
         cb = cb2;
+        rk[0] = rk2[0];
+        rk[1] = rk2[1];
     }
 }
 
