@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5: union A/B (tree vs build_ab/base = the committed union):
+# Round 5: union A/B (tree vs build_ab/base = the committed union), here the sizes pass counted bin by bin:
 # the shard union cases, then the union alone (tree vs base, twice) under a kernel trace.
 export TMPDIR=/tmp
 out=gpurun_out/${1:-r05am}
