@@ -10,12 +10,12 @@
 // entries' density: a coarse grid of 2^16 power-of-two cells (k_shard_coarse: every row's start
 // in every cell, by binary search), each cell cut into ceil(entries / kShTarget) equal code spans
 // (k_shard_cells, k_shard_units: the units' first and end codes), and every row's start in every
-// unit by a binary search inside its cell (k_shard_ustarts).  Then one workgroup per unit gathers
-// the rows' pieces into LDS and sorts them by a counting sort on 13 bits of the code (~0.75
-// entries per bin) followed by an insertion sort of each bin, after which equal codes are
-// adjacent: run heads are the union.  k_shard_union runs twice -- the union's size per unit, then
-// (after a scan) the columns and the indices -- so no entry moves through memory other than its
-// code being read.  A unit that overflows the LDS (more than kShCap entries, or a bin of more
+// unit by a binary search inside its cell (k_shard_ustarts).  Then a persistent grid (two
+// workgroups per CU) takes the units in turn: a workgroup gathers a unit's row pieces into
+// registers, sorts them in LDS by a counting sort on 12 bits of the code (~0.75 entries per bin),
+// puts each bin in order by rank, and equal codes are then adjacent: run heads are the union.
+// k_shard_union runs twice -- the union's size per unit, then (after a scan) the columns and the
+// indices -- so no entry moves through memory other than its code being read.  A unit that overflows the LDS (more than kShCap entries, or a bin of more
 // than kShBin: codes shared by many organisms, low-complexity data) is left to an exact
 // fallback: its entries are gathered, radix-sorted (kmh_sort.hip) and written the same way.
 // (Round 5: until then the units were uniform code spans of ~2048 entries on average and their
