@@ -8,7 +8,7 @@ CSRC     := kmer-ml_amd/csrc
 OUTDIR   := kmer-ml_amd/kmerml/_lib
 OBJDIR   := $(CSRC)/build
 LIB      := $(OUTDIR)/libkmerhip.so
-OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o $(OBJDIR)/kmh_hash.o $(OBJDIR)/kmh_io.o $(OBJDIR)/kmh_csv.o $(OBJDIR)/kmh_sort.o $(OBJDIR)/kmh_features.o $(OBJDIR)/kmh_shard.o
+OBJS     := $(OBJDIR)/kmh_api.o $(OBJDIR)/kmh_fasta.o $(OBJDIR)/kmh_dense.o $(OBJDIR)/kmh_sparse.o $(OBJDIR)/kmh_matrix.o $(OBJDIR)/kmh_hash.o $(OBJDIR)/kmh_io.o $(OBJDIR)/kmh_csv.o $(OBJDIR)/kmh_sort.o $(OBJDIR)/kmh_features.o $(OBJDIR)/kmh_shard.o $(OBJDIR)/kmh_wire.o
 HDRS     := $(CSRC)/kmh_internal.h $(CSRC)/kmh_device.h include/kmerhip.h
 SRCS     := $(wildcard $(CSRC)/*.hip $(CSRC)/*.cpp) $(HDRS)
 # Build id: hash of every product source, compiled into kmh_build_id(); bench.py prints a

@@ -80,9 +80,16 @@ def parse():
                    help="dense N = 1: skip the drop-in end-to-end leg (the reference CLI's call pattern on "
                         "synthetic FASTA files, per-stage clocks) that the default run appends as \"e2e\"")
     p.add_argument("--simulate-ranks", type=int, default=0,
-                   help="one process on one GPU doing what ONE rank of N does per step at config 4 "
+                   help="one process on one GPU doing what ONE rank of N does per step: dense = config 4 "
                         "(count G/N genomes, encode u4, and the all-gather's writes modelled as N - 1 "
-                        "device copies of the slot; no xGMI): a projection, labelled as such")
+                        "device copies of the slot; no xGMI); sparse = config 5's matrix (--genomes per "
+                        "rank, the other ranks' slices of its code range really counted and packed, "
+                        "unpacked and unioned at R = N x genomes rows): a projection, labelled as such")
+    p.add_argument("--config5-genomes-per-rank", type=int, default=16,
+                   help="the config-5 object of the dense line: genomes per rank (config 5: 128 / 8 = 16)")
+    p.add_argument("--config5-genome-len", type=int, default=250_000_000,
+                   help="the config-5 object of the dense line: genome length (config 5: 250 Mbp; smaller "
+                        "only for rehearsals, which the object then labels)")
     p.add_argument("--sim-copy", choices=("torch", "none"), default="torch",
                    help="--simulate-ranks: model the all-gather's writes by device copies (torch), or "
                         "leave them out (none: isolates the copies' contention with the count)")
@@ -340,6 +347,8 @@ def main():
             dist.init_process_group("gloo")
     k, G, L = a.k, a.genomes, a.genome_len
     if a.workload == "sparse":
+        if a.simulate_ranks > 1 and world == 1:
+            return run_sparse_sim(a, dev, dev_index)
         return run_sparse(a, world, rank, dev, dev_index)
     sim = a.simulate_ranks if world == 1 and a.simulate_ranks > 1 else 0
     span = sim or world                       # ranks the genomes are sharded over
@@ -639,6 +648,19 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 
+    c5_multi = None
+    c5_full = a.config5_genome_len == 250_000_000 and a.config5_genomes_per_rank == 16
+    if (world > 1 and not sim and not a.no_config5
+            and ((G == 64 and L == 100_000_000 and k == 12 and not a.single_device) or not c5_full)):
+        # BASELINE config 5 at this N in the same run: every rank counts its 16
+        # genomes, then the matrix leg's all-to-all in the compact wire; rank 0 attaches the object
+        torch.cuda.empty_cache()
+        sa = argparse.Namespace(k=21, genomes=a.config5_genomes_per_rank * world, genome_len=a.config5_genome_len,
+                                steps=3, warmup=1, cpu_sample=0, forward=False, backend=a.backend,
+                                pmc_summary=a.pmc_summary, cpu=None, no_matrix=a.no_matrix,
+                                single_device=a.single_device)
+        c5_multi = run_sparse(sa, world, rank, dev, dev_index, emit=False)
+
     if rank == 0:
         ms = elapsed / a.steps * 1e3
         total_bases = G * L if ((assemble or world == 1) and not sim) else g_local * L * world
@@ -704,12 +726,14 @@ def main():
             "cpu_procs_baseline": cpu_p,
             "cpu_threads_baseline": cpu_mt,
         }
+        if c5_multi is not None:
+            out["config5"] = c5_multi
         if world == 1 and not sim and not a.no_config5 and G == 64 and L == 100_000_000 and k == 12:
             # BASELINE config 5 measured in the same run (its own line: bench.py --workload sparse)
             torch.cuda.empty_cache()
-            sa = argparse.Namespace(k=21, genomes=16, genome_len=250_000_000, steps=3, warmup=1,
-                                    cpu_sample=0, forward=False, backend=a.backend, pmc_summary=a.pmc_summary,
-                                    cpu=cpu5, no_matrix=a.no_matrix)
+            sa = argparse.Namespace(k=21, genomes=a.config5_genomes_per_rank, genome_len=a.config5_genome_len,
+                                    steps=3, warmup=1, cpu_sample=0, forward=False, backend=a.backend,
+                                    pmc_summary=a.pmc_summary, cpu=cpu5, no_matrix=a.no_matrix, single_device=False)
             try:
                 out["config5"] = run_sparse(sa, 1, 0, dev, dev_index, emit=False)
             except Exception as e:   # never lose the config-3 line over the extra measurement
@@ -840,8 +864,11 @@ def run_e2e(dev, dev_index, cpu):
 
 def run_sparse(a, world, rank, dev, dev_index, emit=True):
     """Config 5: k = 21 canonical k-mers of 250 Mbp genomes counted with the device hash-table
-    path (kmh_count_sparse_dev); each rank counts its contiguous block of genomes and keeps
-    its sparse rows (the full 4^21-column matrix would not fit: no all-gather)."""
+    path (kmh_count_sparse_dev); each rank counts its contiguous block of genomes (the count step,
+    no collective: the full 4^21-column matrix would not fit), then the matrix leg
+    (matrix_leg): rows in code order, at N > 1 one all-to-all of code-range slices in the compact
+    wire, each rank's column shard.  emit=False: return the object (rank 0) and leave the process
+    group up (the dense line's config5 object)."""
     k, G, L = a.k, a.genomes, a.genome_len
     lo, hi = (G * rank) // world, (G * (rank + 1)) // world
     g_local = hi - lo
@@ -929,9 +956,13 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
             "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": f"config5: {G} synthetic {L // 1_000_000} Mbp genomes, k={k} "
-                                   f"{'forward' if a.forward else 'canonical'} sparse counts "
-                                   f"({g_local} per GPU, hash-table path)",
+            "config": {"workload": (("config5" if L == 250_000_000 and G == 16 * world and not
+                                     getattr(a, "single_device", False) else
+                                     f"rehearsal ({world} rank(s){' sharing cuda:0' if getattr(a, 'single_device', False) else ''}, "
+                                     "not a config-5 measurement)")
+                                    + f": {G} synthetic {L / 1e6:g} Mbp genomes, k={k} "
+                                    f"{'forward' if a.forward else 'canonical'} sparse counts "
+                                    f"({g_local} per GPU, hash-table path)"),
                        "genomes": G, "genome_len": L, "k": k, "parallelism": f"genome-sharded x{world}"},
             "roofline": roof,
             "step_roofline": {"algorithmic_bytes": algo_step,
@@ -946,32 +977,37 @@ def run_sparse(a, world, rank, dev, dev_index, emit=True):
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
-    if not getattr(a, "no_matrix", False) and g_local:
+    mx = None
+    if not getattr(a, "no_matrix", False):
         # the column-sharded matrix of these genomes, device-resident: sorted
         # rows (kmh_count_sparse_sorted_dev, back to back), at N > 1 the all-to-all of code
-        # ranges, the shard's union and CSR indices (kmh_shard_union_dev); timed apart
+        # ranges in the compact wire, the shard's union and CSR indices; timed apart
         del d_codes, d_counts
         torch.cuda.empty_cache()
         mx = matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev)
         if rank == 0:
             out["matrix"] = mx
+    if not emit:   # (the dense line's config5 object: the process group stays up for the caller)
+        if not ok or (mx is not None and not mx["shard_checked"]):
+            raise SystemExit("config-5 check failed (sparse counts or the sharded matrix)")
+        return out if rank == 0 else None
     if rank == 0:
-        if not emit:
-            return out
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if not ok:
+    if not ok or (mx is not None and not mx["shard_checked"]):
         raise SystemExit("sparse count check failed")
 
 
 def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
     """Time the device-resident column-sharded matrix of this rank's genomes (count in code order +
-    shard) over `steps` runs after one warm-up; check the shard (columns ascending, every column
-    used, counts summing to the windows)."""
-    from kmerml.kmers.matrix import shard_from_rows, sorted_rows_from_device
-    t_rows, t_all, phases = [], [], []
+    shard: at N > 1 the code ranges' all-to-all in the compact wire format) over `steps` runs after
+    one warm-up; check it globally (kmerml.kmers.matrix.shard_check: within every rank columns
+    ascending and all used; across ranks the values sum to every window of every genome, so a slice
+    lost or duplicated by the exchange fails, and the ranks' column ranges are in order)."""
+    from kmerml.kmers import matrix as kmatrix
+    t_rows, t_all, phases, shard_ph, exch = [], [], [], [], []
     m = None
     # the first run is a warm-up: its torch.empty calls reach hipMalloc (~23 GB/s for these
     # 32-48 GB buffers: 4.2 s of the first run); later runs reuse the caching allocator's blocks
@@ -981,14 +1017,14 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        ph = {}
+        ph, sph = {}, {}
         st0 = _native.context(dev.index).stats()
-        codes, counts, roff = sorted_rows_from_device(d_seq, offsets, k, canonical, timings=ph)
+        codes, counts, roff = kmatrix.sorted_rows_from_device(d_seq, offsets, k, canonical, timings=ph)
         st1 = _native.context(dev.index).stats()
         ph["fallback_passes"] = st1["fallback_passes"] - st0["fallback_passes"]
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        m = shard_from_rows(codes, counts, roff, G, k)
+        m = kmatrix.shard_from_rows(codes, counts, roff, G, k, timings=sph)
         del codes, counts
         torch.cuda.synchronize()
         if world > 1:
@@ -996,30 +1032,199 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
         t2 = time.perf_counter()
         if i:
             phases.append(ph)
+            shard_ph.append(sph)
             t_rows.append((t1 - t0) * 1e3)
             t_all.append((t2 - t0) * 1e3)
-    cols = m.columns
-    ok = bool(torch.all(cols[1:] > cols[:-1]).item()) if cols.numel() > 1 else True
-    used = torch.zeros(cols.numel(), dtype=torch.int32, device=dev)
-    used[m.indices] = 1
-    ok = ok and bool(torch.all(used == 1).item())
-    tot = int(m.values.to(torch.int64).sum().item())
-    g_local = len(offsets) - 1
-    want = g_local * (a.genome_len - k + 1) if world == 1 else None
-    ok = ok and (want is None or tot == want)
+            exch.append(kmatrix.LAST_EXCHANGE)
+    windows = G * max(a.genome_len - k + 1, 0)
+    ok, summ = kmatrix.shard_check(m, windows)
     ms = float(np.mean(t_all))
+    ex_ms = float(np.mean([p.get("exchange_ms", 0.0) for p in shard_ph])) if shard_ph else 0.0
     if world > 1:
-        t = torch.tensor([ms, 0.0 if ok else 1.0], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        t = torch.tensor([ms, ex_ms, 0.0 if ok else 1.0], dtype=torch.float64,
+                         device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, ok = float(t[0]), float(t[1]) == 0.0
-    return {"matrix_ms": round(ms, 2), "sorted_rows_ms": round(float(np.mean(t_rows)), 2),
-            "shard_ms": round(ms - float(np.mean(t_rows)), 2), "steps": steps,
-            "sorted_rows_phases": {key: round(float(np.mean([p.get(key, 0.0) for p in phases])), 2)
-                                   for key in phases[-1]} if phases else {},
-            "what": f"this rank's {g_local} genomes -> its column shard of the organisms x k-mers matrix "
-                    "(features.py:96-111): kmh_count_sparse_sorted_dev (rows in code order, back to back), "
-                    + ("all-to-all of code ranges, " if world > 1 else "") + "kmh_shard_union_dev (columns + CSR)",
-            "ncols": int(cols.numel()), "nnz": m.nnz, "shard_checked": ok}
+        ms, ex_ms, ok = float(t[0]), float(t[1]), float(t[2]) == 0.0
+    g_local = len(offsets) - 1
+    out = {"matrix_ms": round(ms, 2), "sorted_rows_ms": round(float(np.mean(t_rows)), 2),
+           "shard_ms": round(ms - float(np.mean(t_rows)), 2), "steps": steps,
+           "sorted_rows_phases": {key: round(float(np.mean([p.get(key, 0.0) for p in phases])), 2)
+                                  for key in phases[-1]} if phases else {},
+           "shard_phases_rank0": {key: round(float(np.mean([p.get(key, 0.0) for p in shard_ph])), 2)
+                                  for key in shard_ph[-1]} if shard_ph else {},
+           "what": f"this rank's {g_local} genomes -> its column shard of the organisms x k-mers matrix "
+                   "(features.py:96-111): kmh_count_sparse_sorted_dev (rows in code order, back to back), "
+                   + ("code ranges from the rows' device cuts, one all-to-all of the slices in the compact wire "
+                      "(kmh_wire_encode/decode_dev), " if world > 1 else "")
+                   + "kmh_shard_union_u32_dev (columns + u32 CSR indices)",
+           "ncols_rank0": int(m.columns.numel()), "nnz_rank0": m.nnz, "index_dtype": str(m.indices.dtype),
+           "global": summ, "global_windows": windows, "shard_checked": ok}
+    if world > 1 and exch and exch[-1]:
+        e = exch[-1]
+        rb = e["received_bytes"]
+        gbs = rb / (ex_ms * 1e-3) / 1e9 if ex_ms > 0 else None
+        out["exchange"] = dict(e, **{
+            "exchange_ms_rank_max": round(ex_ms, 2),
+            "received_GBs_per_gpu": round(gbs, 1) if gbs else None,
+            "frac_of_7_links": round(gbs / (7 * XGMI_LINK_GBS), 4) if gbs else None,
+            "bytes_per_entry": round(e["sent_bytes"] / max(1, e["raw_sent_bytes"] / 12), 3),
+            "timing": ("gloo host-staged (validation only)" if a.backend == "gloo" else
+                       "wall clock around one all_to_all_single (RCCL over xGMI), synchronised, max over ranks")})
+    return out
+
+
+def run_sparse_sim(a, dev, dev_index):
+    """--workload sparse --simulate-ranks N: what ONE rank of config 5 at N GPUs does per matrix step,
+    on one GPU: its 16 genomes counted in code order, cut at the N code ranges
+    (bounds from the histogram of all N x 16 genomes), the slices for the other N - 1 ranks packed in
+    the compact wire, the bytes that would arrive from the other ranks unpacked -- really the other
+    ranks' genomes (counted, cut to this rank's range and packed before timing) -- and the union of
+    this rank's shard at its N = 8 shape: R = N x 16 organism rows over 1/N of the code space.  The
+    xGMI transfer itself is not run: its HBM side is modelled by a device copy of the packed bytes,
+    and the line prints the bytes and the step time at a stated link rate (a projection)."""
+    from kmerml.kmers import matrix as kmatrix
+    N, k, L = a.simulate_ranks, a.k, a.genome_len
+    gpr = a.genomes          # genomes per rank (--genomes; 16 by default, config 5's 128 / 8)
+    G = N * gpr
+    canonical = 0 if a.forward else 1
+    ctx = _native.context(dev_index)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    stride = (L + 15) // 16 * 16
+    d_seq = torch.empty(gpr * stride, dtype=torch.uint8, device=dev)
+    if stride != L:
+        d_seq.fill_(ord("N"))
+    offsets = np.arange(gpr + 1, dtype=np.uint64) * np.uint64(stride)
+
+    def batch_rows(b):
+        ctx.synth_dev(d_seq.data_ptr(), L, stride, gpr, SEED_BASE + b * gpr, s)
+        return kmatrix.sorted_rows_from_device(d_seq, offsets, k, canonical)
+
+    t_setup = time.perf_counter()
+    hist = None
+    for b in range(N):   # the global histogram the all-reduce would give
+        codes, counts, roff = batch_rows(b)
+        h = kmatrix._row_histogram(codes, roff, k)
+        hist = h if hist is None else hist + h
+        del codes, counts
+    bounds = kmatrix._splitters_from_hist(hist.cpu().numpy(), k, N)
+    # what arrives from the other ranks: their genomes' slices of range 0, packed by them
+    parts, rs_n, rs_b = [], [], []
+    for b in range(1, N):
+        codes, counts, roff = batch_rows(b)
+        send_len, starts = kmatrix.shard_plan(codes, roff, bounds, b)
+        st, sn = starts[:, 0].astype(np.uint64), send_len[:, 0].astype(np.uint64)
+        sb = ctx.wire_size_dev(codes.data_ptr(), counts.data_ptr(), st, sn, s)
+        buf = torch.empty(max(int(sb.sum()), 16), dtype=torch.uint8, device=dev)
+        ctx.wire_encode_dev(codes.data_ptr(), counts.data_ptr(), st, sn, buf.data_ptr(), int(sb.sum()), s)
+        parts.append(buf[:int(sb.sum())])
+        rs_n += sn.tolist()
+        rs_b += sb.tolist()
+        del codes, counts
+    recv = torch.cat(parts)
+    del parts
+    ctx.synth_dev(d_seq.data_ptr(), L, stride, gpr, SEED_BASE, s)   # this rank's genomes, resident
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+
+    def step(ph):
+        t = [time.perf_counter()]
+
+        def mark(name):
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            ph[name] = ph.get(name, 0.0) + (now - t[0]) * 1e3
+            t[0] = now
+        codes, counts, roff = kmatrix.sorted_rows_from_device(d_seq, offsets, k, canonical)
+        mark("sorted_rows_ms")
+        h = kmatrix._row_histogram(codes, roff, k)   # (its all-reduce is not modelled)
+        send_len, starts = kmatrix.shard_plan(codes, roff, bounds, 0)
+        del h
+        mark("plan_ms")
+        st = np.concatenate([starts[:, q] for q in range(1, N)]).astype(np.uint64)
+        sn = np.concatenate([send_len[:, q] for q in range(1, N)]).astype(np.uint64)
+        sb = ctx.wire_size_dev(codes.data_ptr(), counts.data_ptr(), st, sn, s)
+        nbytes = int(sb.sum())
+        send = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
+        ctx.wire_encode_dev(codes.data_ptr(), counts.data_ptr(), st, sn, send.data_ptr(), nbytes, s)
+        mark("encode_ms")
+        # receive layout: genome-major, this rank's genomes first (it is rank 0)
+        gl = np.concatenate([send_len[:, 0], np.array(rs_n, np.int64)])
+        indptr = np.zeros(G + 1, np.int64)
+        np.cumsum(gl, out=indptr[1:])
+        total = int(indptr[-1])
+        rc = torch.empty(total, dtype=torch.int64, device=dev)
+        rn = torch.empty(total, dtype=torch.int32, device=dev)
+        for j in range(gpr):
+            a0, m_, d = int(starts[j, 0]), int(send_len[j, 0]), int(indptr[j])
+            rc[d:d + m_].copy_(codes[a0:a0 + m_])
+            rn[d:d + m_].copy_(counts[a0:a0 + m_])
+        del codes, counts
+        mark("own_copy_ms")
+        if a.sim_copy == "torch":   # the wire's HBM side: the packed bytes written once more on arrival
+            scratch = torch.empty_like(recv)
+            scratch.copy_(recv)
+            del scratch
+        del send
+        mark("wire_model_ms")
+        ctx.wire_decode_dev(recv.data_ptr(), recv.numel(), np.array(rs_n, np.uint64), np.array(rs_b, np.uint64),
+                            indptr[gpr:G].astype(np.uint64), rc.data_ptr(), rn.data_ptr(), s)
+        mark("decode_ms")
+        columns = torch.empty(total, dtype=torch.int64, device=dev)
+        indices = torch.empty(total, dtype=torch.int32, device=dev)
+        ncols = ctx.shard_union_dev(rc.data_ptr(), indptr.astype(np.uint64), bounds[0], bounds[1] - 1,
+                                    columns.data_ptr(), indices.data_ptr(), s, idx32=True)
+        mark("union_ms")
+        m = kmatrix.ShardedSparseMatrix(k, G, bounds[0], bounds[1], columns[:ncols], indptr, indices, rn, 0, N)
+        return m, nbytes, total
+
+    times, phs = [], []
+    for i in range(a.steps + 1):
+        ph = {}
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        m, sent, total = step(ph)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) * 1e3
+        if i:
+            times.append(dt)
+            phs.append(ph)
+        if i < a.steps:
+            del m
+    ok = m.all_columns_used()
+    cols = m.columns
+    ok = ok and (bool(torch.all(cols[1:] > cols[:-1]).item()) if cols.numel() > 1 else True)
+    # every entry of range 0 of all N x 16 genomes arrived: the rows' cuts of range 0 summed
+    want_entries = int(hist.cpu().numpy()[:bounds[1] >> max(2 * k - 16, 0)].sum())
+    ok = ok and total == want_entries
+    ms = float(np.mean(times))
+    received = int(recv.numel())
+    rate = 0.5 * 7 * XGMI_LINK_GBS   # GB/s assumed for the projection: half of the 7 links' peak
+    xfer_ms = max(sent, received) / (rate * 1e9) * 1e3
+    proj_ms = ms + xfer_ms
+    out = {"metric": METRIC, "value": None, "unit": "bases/s", "n_gpus": 1, "steps": a.steps, "warmup": 1,
+           "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic",
+           "config": {"workload": (f"projection: ONE rank of config 5's matrix at N = {N} on one GPU (its {gpr} of "
+                                   f"{G} synthetic {L / 1e6:g} Mbp genomes, k={k} "
+                                   f"{'forward' if a.forward else 'canonical'}: count in code order, cut, pack the "
+                                   f"slices of the other {N - 1} ranks, unpack the other ranks' real slices of its "
+                                   f"range, union at R = {G} rows); no xGMI traffic, no other ranks"),
+                      "genomes": G, "genome_len": L, "k": k, "parallelism": f"code-range sharded x{N} (simulated)"},
+           "simulated_ranks": N, "simulated_copies": a.sim_copy,
+           "phases_ms": {key: round(float(np.mean([p[key] for p in phs])), 2) for key in phs[-1]},
+           "shard": {"rows": G, "entries": total, "columns": int(cols.numel()), "lo_code": bounds[0],
+                     "hi_code": bounds[1], "checked": ok},
+           "exchange": {"wire": "compact", "sent_bytes": sent, "received_bytes": received,
+                        "raw_received_bytes": int(sum(rs_n)) * 12,
+                        "bytes_per_entry": round(received / max(1, sum(rs_n)), 3),
+                        "assumed_xgmi_GBs": rate, "transfer_ms_at_assumed_rate": round(xfer_ms, 2),
+                        "required_GBs_to_hide_in_step": round(received / (ms * 1e-3) / 1e9, 1)},
+           "projected_ms_per_step": round(proj_ms, 2),
+           "projected_value_at_n": G * L / (proj_ms * 1e-3),
+           "setup_s": round(setup_s, 1)}
+    print(json.dumps(out), flush=True)
+    if not ok:
+        raise SystemExit("simulated shard check failed")
 
 
 if __name__ == "__main__":

@@ -215,6 +215,43 @@ int kmh_count_sparse_sorted_dev(kmh_ctx* ctx, const uint8_t* d_seq, const uint64
 int kmh_shard_union_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R,
                         uint64_t lo_code, uint64_t hi_code_incl, uint64_t* d_columns, int64_t* d_indices,
                         uint64_t* ncols, void* stream);
+/* kmh_shard_union_dev with u32 column indices (half the index bytes): the rows must hold fewer than
+ * 2^32 - 1 entries (KMH_ERR_INVALID otherwise), so every column index fits.  The shard's default
+ * (kmerml.kmers.matrix.shard_from_rows). */
+int kmh_shard_union_u32_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R,
+                            uint64_t lo_code, uint64_t hi_code_incl, uint64_t* d_columns, uint32_t* d_indices,
+                            uint64_t* ncols, void* stream);
+
+/* ---- the exchange of the column-sharded sparse matrix (multi-GPU, config 5) ---- */
+/* Each rank owns a contiguous code range of the matrix's columns (features.py:96-111's sorted union
+ * of labels); a rank's organism rows are sorted by code, so what it sends a peer is one slice per
+ * row, between two cuts.  d_cuts[r * nb + b] (device, R x nb u64) = the first entry of row r
+ * (relative to the row) whose code is >= bounds[b]: rows as for kmh_shard_union_dev (host row_off,
+ * R + 1 entries), bounds a host array of nb codes.  Also gives a code histogram (cuts at the
+ * histogram's edges) without a pass over the entries. */
+int kmh_rows_cuts_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, const uint64_t* bounds,
+                      int nb, uint64_t* d_cuts, void* stream);
+/* Compact wire format of S row slices for the all-to-all: slice i = entries [slice_start[i],
+ * slice_start[i] + slice_n[i]) of d_codes / d_counts (device; host slice arrays), codes ascending
+ * within a slice.  Per 1024 entries one 2192-byte record (the first code, u16 gaps, a bit per count
+ * that is not 1) and, per slice, 16-byte escapes for gaps >= 65535 and counts != 1: exact for any
+ * codes and counts, ~2.2 bytes per entry for config 5's rows against 12 raw.  kmh_wire_size_dev
+ * writes every slice's byte size to slice_bytes (host; synchronises the stream); kmh_wire_encode_dev
+ * writes the slices back to back to d_out (out_bytes >= the sum), reusing the sizing of a
+ * kmh_wire_size_dev call with the same arguments just before it (the data must not change in
+ * between).  KMH_ERR_UNSUPPORTED past 2^24 slices, 2^32 chunks or 2^32 escapes in one slice. */
+int kmh_wire_size_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* slice_start,
+                      const uint64_t* slice_n, int S, uint64_t* slice_bytes, void* stream);
+int kmh_wire_encode_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* slice_start,
+                        const uint64_t* slice_n, int S, uint8_t* d_out, uint64_t out_bytes, void* stream);
+/* Decode S slices back to back in d_in (slice i: slice_n[i] entries in slice_bytes[i] bytes, as the
+ * sender's kmh_wire_size_dev reported; host arrays) into d_codes / d_counts at entry slice_dst[i]
+ * (the caller's output must hold them).  A slice whose bytes do not match its entries is
+ * KMH_ERR_INVALID; escape fields are clamped to their slice, so damaged bytes cannot move a read or
+ * write outside it. */
+int kmh_wire_decode_dev(kmh_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* slice_n,
+                        const uint64_t* slice_bytes, const uint64_t* slice_dst, int S, uint64_t* d_codes,
+                        uint32_t* d_counts, void* stream);
 /* Output offsets of kmh_count_sparse_dev: out_off[g] for g = 0..G (out_off nullable);
  * returns out_off[G], the total capacity in entries. */
 uint64_t kmh_sparse_out_offsets(const uint64_t* offsets, int G, int k, uint64_t* out_off);

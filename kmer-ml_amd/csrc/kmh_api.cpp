@@ -190,6 +190,8 @@ static void free_workspace(kmh_ctx* ctx) {
                            &ctx->redo, &ctx->order, &ctx->sort_tmp, &ctx->scan_tmp, &ctx->first})
         drop(*b);
     for (auto& b : ctx->sparse) drop(b);
+    for (auto& b : ctx->wire) drop(b);
+    ctx->wire_valid = false;
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     ctx->pinned = nullptr;
     ctx->pinned_bytes = 0;
@@ -203,6 +205,7 @@ static uint64_t workspace_bytes(const kmh_ctx* ctx) {
                                  &ctx->redo, &ctx->order, &ctx->sort_tmp, &ctx->scan_tmp, &ctx->first})
         t += b->bytes;
     for (const auto& b : ctx->sparse) t += b.bytes;
+    for (const auto& b : ctx->wire) t += b.bytes;
     return t;
 }
 
@@ -362,7 +365,59 @@ int kmh_shard_union_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* r
     ctx->err.clear();
     if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
     return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
-        return kmh::shard_union(ctx, d_codes, row_off, R, lo_code, hi_code_incl, d_columns, d_indices, ncols, s);
+        return kmh::shard_union(ctx, d_codes, row_off, R, lo_code, hi_code_incl, d_columns, d_indices, false, ncols, s);
+    });
+}
+
+int kmh_shard_union_u32_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R,
+                            uint64_t lo_code, uint64_t hi_code_incl, uint64_t* d_columns, uint32_t* d_indices,
+                            uint64_t* ncols, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::shard_union(ctx, d_codes, row_off, R, lo_code, hi_code_incl, d_columns, d_indices, true, ncols, s);
+    });
+}
+
+int kmh_rows_cuts_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, const uint64_t* bounds,
+                      int nb, uint64_t* d_cuts, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::rows_cuts(ctx, d_codes, row_off, R, bounds, nb, d_cuts, s);
+    });
+}
+
+int kmh_wire_size_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* slice_start,
+                      const uint64_t* slice_n, int S, uint64_t* slice_bytes, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::wire_size(ctx, d_codes, d_counts, slice_start, slice_n, S, slice_bytes, s);
+    });
+}
+
+int kmh_wire_encode_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* slice_start,
+                        const uint64_t* slice_n, int S, uint8_t* d_out, uint64_t out_bytes, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::wire_encode(ctx, d_codes, d_counts, slice_start, slice_n, S, d_out, out_bytes, s);
+    });
+}
+
+int kmh_wire_decode_dev(kmh_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* slice_n,
+                        const uint64_t* slice_bytes, const uint64_t* slice_dst, int S, uint64_t* d_codes,
+                        uint32_t* d_counts, void* stream) {
+    if (!ctx) return KMH_ERR_INVALID;
+    ctx->err.clear();
+    if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, KMH_ERR_HIP, "hipSetDevice failed");
+    return on_stream(ctx, pick_stream(ctx, stream), [&](hipStream_t s) {
+        return kmh::wire_decode(ctx, d_in, in_bytes, slice_n, slice_bytes, slice_dst, S, d_codes, d_counts, s);
     });
 }
 

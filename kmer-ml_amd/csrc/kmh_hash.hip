@@ -2192,7 +2192,8 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 
 namespace {
 
-// ORD: d_nkmers receives the row lengths (distinct + padding) and d_ndist the distinct k-mers.
+// ORD: every genome's rows compact, in code order and back to back from entry 0; d_nkmers (the row
+// lengths) and d_ndist both receive the distinct k-mers (no padding rows since round 5).
 template <typename E, bool POS, bool ORD = false>
 int sparse_count_dev_impl(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                           int canonical, uint64_t* d_codes, uint32_t* d_counts, uint32_t* d_firsts,

@@ -40,6 +40,13 @@ struct Ctx {
     std::string err;
     // device workspace
     DevBuf seq, suf, toff, meta, out, out2, fix, redo, sparse[8], order, sort_tmp, scan_tmp, first;
+    // the config-5 exchange (kmh_wire.hip): [0] slice plan, [1] escapes per chunk, [2] their scan;
+    // the scan and the slices' bytes are kept for the encode call that follows a size call on the
+    // same slices (wire_key: a hash of the device pointers and the slice arrays)
+    DevBuf wire[3];
+    uint64_t wire_key = 0;
+    bool wire_valid = false;
+    std::vector<uint64_t> wire_sbytes;
     // the (goff, tbase) layout last copied to `meta` (upload_layout skips an identical copy)
     std::vector<uint64_t> meta_cache;
     // kmh_stage_host: bytes of the host sequence staged in `seq` (valid while staged_ok)
@@ -159,9 +166,9 @@ uint64_t sparse_windows(const uint64_t* offsets, int G, int k, uint64_t* out_off
 int sparse_count_dev(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                      int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nkmers,
                      hipStream_t s);
-// The same counts with every genome's rows in ascending code order: genome g's rows are
-// [out_off[g], out_off[g] + d_nrows[g]), and the rows whose count is 0 are padding (their code
-// repeats a neighbouring code, so the codes stay non-decreasing); d_ndist[g] = distinct k-mers.
+// The same counts with every genome's rows in ascending code order, compact and back to back from
+// entry 0: genome g's rows follow those of genomes 0 .. g - 1, codes strictly ascending, every count
+// nonzero; d_nrows[g] = d_ndist[g] = its distinct k-mers (no padding since round 5).
 int sparse_count_dev_sorted(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offsets, int G, int k,
                             int canonical, uint64_t* d_codes, uint32_t* d_counts, uint64_t* d_nrows,
                             uint64_t* d_ndist, hipStream_t s);
@@ -175,8 +182,25 @@ int sparse_count_dev_first(Ctx* ctx, const uint8_t* d_seq, const uint64_t* offse
 // R sorted organism rows of codes in [lo, hi_incl], rows back to back: row r is d_codes[row_off[r],
 // row_off[r + 1]) (host offsets).  d_columns (>= the entries) receives the sorted union of the
 // codes, d_indices[e] (for every entry e of the rows) its column; *ncols the union's size.
+// idx32: d_indices is uint32_t[] (the rows hold fewer than 2^32 entries), else int64_t[].
 int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
-                uint64_t hi_incl, uint64_t* d_columns, int64_t* d_indices, uint64_t* ncols, hipStream_t s);
+                uint64_t hi_incl, uint64_t* d_columns, void* d_indices, bool idx32, uint64_t* ncols, hipStream_t s);
+// out[0 .. n] = the exclusive u64 scan of in[0 .. n) and its total (ctx->scan_tmp).
+int scan_u32_u64(Ctx* ctx, const uint32_t* in, uint32_t n, unsigned long long* out, hipStream_t s);
+
+// ---- the config-5 exchange (kmh_wire.hip) ----
+// d_cuts[r * nb + b] = first entry of row r (relative) with code >= bounds[b] (host row_off, bounds).
+int rows_cuts(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, const uint64_t* bounds, int nb,
+              uint64_t* d_cuts, hipStream_t s);
+// Compact wire of S row slices (slice i = entries [sstart[i], + sn[i]) of d_codes / d_counts, host
+// arrays): wire_size -> bytes per slice (synchronises); wire_encode -> the slices back to back.
+int wire_size(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* sstart, const uint64_t* sn,
+              int S, uint64_t* slice_bytes, hipStream_t s);
+int wire_encode(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* sstart, const uint64_t* sn,
+                int S, uint8_t* d_out, uint64_t out_bytes, hipStream_t s);
+// Slices back to back in d_in (sn entries, sbytes bytes each) -> entries sdst[i] .. of the output.
+int wire_decode(Ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* sn, const uint64_t* sbytes,
+                const uint64_t* sdst, int S, uint64_t* d_codes, uint32_t* d_counts, hipStream_t s);
 
 
 // ---- feature columns of the feature CSV (kmh_features.hip) ----

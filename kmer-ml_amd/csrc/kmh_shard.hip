@@ -161,7 +161,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
 // pieces are scanned (into the other of two LDS tables) and its codes loaded right after this
 // unit's scatter, so they land during this unit's sort, heads and stores (one unit at a time per
 // workgroup waited for two global round trips per unit: latency-bound).
-template <bool WRITE, typename K>
+template <bool WRITE, typename K, typename IX>
 __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
                                                             const uint32_t* __restrict__ st, uint32_t S,
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                             uint32_t* __restrict__ big,
                                                             const unsigned long long* __restrict__ colbase,
                                                             uint64_t* __restrict__ columns,
-                                                            int64_t* __restrict__ indices) {
+                                                            IX* __restrict__ indices) {
     // the unit's codes as offsets from its first code: u32 whenever every unit spans < 2^32 codes
     __shared__ __attribute__((aligned(16))) K scode[kShCap];
     __shared__ __attribute__((aligned(16))) uint16_t sidx[kShCap];
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                    if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (int64_t)(cb + colrel[i]);
+                    if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (IX)(cb + colrel[i]);
                 }
             }
         }
@@ -665,6 +665,7 @@ __global__ __launch_bounds__(256) void k_shard_big_count(const uint64_t* __restr
 
 // Fallback, write: run r's column = colbase[its sub-range] + (r - the sub-range's first run);
 // every entry of the run gets it.
+template <typename IX>
 __global__ __launch_bounds__(256) void k_shard_big_write(const uint64_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, uint64_t m,
                                                          const uint32_t* __restrict__ starts,
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(256) void k_shard_big_write(const uint64_t* __restr
                                                          const uint64_t* __restrict__ ub, uint32_t U,
                                                          const unsigned long long* __restrict__ colbase,
                                                          const uint64_t* __restrict__ gpos,
-                                                         uint64_t* __restrict__ columns, int64_t* __restrict__ indices) {
+                                                         uint64_t* __restrict__ columns, IX* __restrict__ indices) {
     const uint32_t n = *nruns;
     for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < n; r += gridDim.x * 256u) {
         const uint64_t c = keys[starts[r]];
@@ -686,7 +687,7 @@ __global__ __launch_bounds__(256) void k_shard_big_write(const uint64_t* __restr
         const unsigned long long col = colbase[s] + (r - a);
         columns[col] = c;
         const uint64_t e = r + 1u < n ? starts[r + 1u] : m;
-        for (uint64_t t = starts[r]; t < e; ++t) indices[gpos[vals[t]]] = (int64_t)col;
+        for (uint64_t t = starts[r]; t < e; ++t) indices[gpos[vals[t]]] = (IX)col;
     }
 }
 
@@ -708,7 +709,7 @@ int scan_u32_u64(Ctx* ctx, const uint32_t* in, uint32_t n, unsigned long long* o
 }
 
 int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
-                uint64_t hi_incl, uint64_t* d_columns, int64_t* d_indices, uint64_t* ncols, hipStream_t s) {
+                uint64_t hi_incl, uint64_t* d_columns, void* d_indices, bool idx32, uint64_t* ncols, hipStream_t s) {
     static_assert(kShMaxRows <= kShCap, "a unit of one code fits the LDS");
     if (R < 1 || R > kShMaxRows) return fail(ctx, KMH_ERR_UNSUPPORTED, "a shard holds 1 to 4096 organism rows");
     if (!d_codes || !row_off || !ncols || hi_incl < lo) return fail(ctx, KMH_ERR_INVALID, "bad shard arguments");
@@ -718,6 +719,7 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
             return fail(ctx, KMH_ERR_INVALID, "row offsets must ascend, rows below 2^32 - 1 entries");
     *ncols = 0;
     if (T == 0) return KMH_OK;
+    if (idx32 && T >= 0xFFFFFFFFull) return fail(ctx, KMH_ERR_INVALID, "u32 column indices need fewer than 2^32 - 1 entries");
     if (!d_columns || !d_indices) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
     // coarse cells of 2^CSH codes: span <= 2^nbits, at most 2^kShCoarseBits cells
     const uint64_t span1 = hi_incl - lo;   // span - 1
@@ -786,11 +788,11 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     // every unit lies inside one coarse cell of 2^CSH codes: u32 offsets when CSH <= 32
     const bool narrow = CSH <= 32;
     if (narrow)
-        hipLaunchKernelGGL((k_shard_union<false, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
-                           d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL((k_shard_union<false, uint32_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
+                           d_st, S, d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_shard_union<false, uint64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
-                           d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL((k_shard_union<false, uint64_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
+                           d_st, S, d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     uint32_t nbig = 0;
@@ -852,17 +854,30 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
     time_begin(ctx, s, "k_shard_union");
-    if (narrow)
-        hipLaunchKernelGGL((k_shard_union<true, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
-                           d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
+    // (indices at the rows' own offsets: row_off[0] may be past the start of d_indices)
+    uint32_t* const ix32 = idx32 ? static_cast<uint32_t*>(d_indices) + row_off[0] : nullptr;
+    int64_t* const ix64 = idx32 ? nullptr : static_cast<int64_t*>(d_indices) + row_off[0];
+    if (narrow && idx32)
+        hipLaunchKernelGGL((k_shard_union<true, uint32_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
+                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix32);
+    else if (narrow)
+        hipLaunchKernelGGL((k_shard_union<true, uint32_t, int64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
+                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix64);
+    else if (idx32)
+        hipLaunchKernelGGL((k_shard_union<true, uint64_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
+                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix32);
     else
-        hipLaunchKernelGGL((k_shard_union<true, uint64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R, d_st, S,
-                           d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, d_indices + row_off[0]);
+        hipLaunchKernelGGL((k_shard_union<true, uint64_t, int64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
+                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix64);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (nbig) {
-        hipLaunchKernelGGL(k_shard_big_write, dim3(1024), dim3(256), 0, s, gcode, gval, m, starts, nruns, d_ub, S,
-                           d_colbase, gpos, d_columns, d_indices + row_off[0]);
+        if (idx32)
+            hipLaunchKernelGGL((k_shard_big_write<uint32_t>), dim3(1024), dim3(256), 0, s, gcode, gval, m, starts, nruns, d_ub,
+                               S, d_colbase, gpos, d_columns, ix32);
+        else
+            hipLaunchKernelGGL((k_shard_big_write<int64_t>), dim3(1024), dim3(256), 0, s, gcode, gval, m, starts, nruns, d_ub,
+                               S, d_colbase, gpos, d_columns, ix64);
         KMH_HIP(ctx, hipGetLastError());
     }
     KMH_HIP(ctx, hipStreamSynchronize(s));

@@ -1,0 +1,462 @@
+// kmh_wire.hip -- the exchange step of the column-sharded config-5 matrix
+// (/root/reference/kmerml/ml/features.py:96-111: the matrix's columns are the sorted union of every
+// organism's labels; here every rank owns a contiguous code range, so every organism row must reach
+// the rank of each of its codes).  Rows are sorted by code (kmh_count_sparse_sorted_dev), so what a
+// rank sends another is one contiguous slice per row: its start and end come from binary searches of
+// the range bounds (k_rows_cuts), which also give the global code histogram that places the bounds.
+//
+// The compact wire.  A sorted row slice is mostly small gaps between codes
+// (k = 21 canonical, 250 Mbp genomes: ~1.8e4 codes on average, ~15 bits) and counts of 1, so it
+// travels as chunk records of 1024 entries:
+//
+//   [u64 anchor = the chunk's first code][u32 first escape of the chunk, slice-relative][u32 escapes]
+//   [u16 gap x 1024: code - previous code (0 for the first entry, and past the slice's end);
+//    0xFFFF = the gap is in an escape]
+//   [128 bytes: bit i set = entry i's count is not 1 (the count is in an escape)]
+//
+// (2192 bytes, 2.14 B per entry) followed, per slice, by its escape table: 16-byte entries
+// {u32 entry index in the chunk | kind << 16, u32 0, u64 value}, kind 0 = the full gap, kind 1 = the
+// count.  Exact for any codes and counts (k = 32 codes use all 64 bits; the sums wrap like the codes).
+// A slice is sized first (k_wire_count: escapes per chunk, a scan, the slice's bytes), then packed
+// (k_wire_pack), and the receiver rebuilds codes and counts with one u64 scan per chunk
+// (k_wire_unpack) straight into its shard's row layout.  Every kernel is one streaming pass: the
+// reads and writes are the algorithmic bytes (12 B per entry raw, ~2.2 B packed).
+#include <algorithm>
+#include <vector>
+
+#include "kmh_device.h"
+
+namespace kmh {
+namespace {
+
+constexpr int kWThreads = 256;
+constexpr int kWPer = 4;                               // entries per thread: j * 256 + tid
+constexpr int kWChunk = kWThreads * kWPer;             // entries per chunk record
+constexpr int kWHead = 16;
+constexpr int kWBits = kWHead + 2 * kWChunk;           // offset of the count bitmap
+constexpr int kWRec = kWBits + kWChunk / 8;            // 2192 bytes
+constexpr uint64_t kWEsc = 16;                         // bytes per escape
+constexpr uint32_t kWGapEsc = 0xFFFFu;
+static_assert(kWRec % 16 == 0, "records keep 16-byte alignment");
+
+// cuts[r * nb + b] = the first entry of row r (relative to the row) whose code is >= bounds[b].
+__global__ __launch_bounds__(256) void k_rows_cuts(const uint64_t* __restrict__ codes, const uint64_t* __restrict__ roff,
+                                                   uint32_t R, const uint64_t* __restrict__ bounds, uint32_t nb,
+                                                   uint64_t* __restrict__ cuts) {
+    const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (x >= (uint64_t)R * nb) return;
+    const uint32_t r = (uint32_t)(x / nb), b = (uint32_t)(x % nb);
+    const uint64_t a = roff[r], e = roff[r + 1];
+    const uint64_t c = bounds[b];
+    uint64_t lo = a, hi = e;
+    while (lo < hi) {
+        const uint64_t m = lo + (hi - lo) / 2u;
+        if (codes[m] < c) lo = m + 1u;
+        else hi = m;
+    }
+    cuts[x] = lo - a;
+}
+
+// The slice of chunk c: the last s with cbase[s] <= c (cbase: S + 1 non-decreasing chunk starts;
+// empty slices own no chunk).
+__device__ __forceinline__ uint32_t slice_of(const uint64_t* __restrict__ cbase, uint32_t S, uint64_t c) {
+    uint32_t a = 0u, b = S - 1u;
+    while (a < b) {
+        const uint32_t m = (a + b + 1u) / 2u;
+        if (cbase[m] <= c) a = m;
+        else b = m - 1u;
+    }
+    return a;
+}
+
+// Sum over the workgroup (kWThreads); ws: kWThreads / 64 words.
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* ws) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    if ((threadIdx.x & 63u) == 0u) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t t = 0u;
+#pragma unroll
+    for (int w = 0; w < kWThreads / 64; ++w) t += ws[w];
+    __syncthreads();
+    return t;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_u64(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// A chunk's place: slice s, chunk index within it, first entry (input index), entries.
+struct Chunk {
+    uint32_t s;
+    uint64_t cl, base;
+    uint32_t n;
+};
+
+__device__ __forceinline__ Chunk chunk_at(const uint64_t* __restrict__ sstart, const uint64_t* __restrict__ sn,
+                                          const uint64_t* __restrict__ cbase, uint32_t S, uint64_t c) {
+    Chunk k;
+    k.s = slice_of(cbase, S, c);
+    k.cl = c - cbase[k.s];
+    k.base = sstart[k.s] + k.cl * kWChunk;
+    const uint64_t rem = sn[k.s] - k.cl * kWChunk;
+    k.n = (uint32_t)(rem < (uint64_t)kWChunk ? rem : (uint64_t)kWChunk);
+    return k;
+}
+
+// Escapes of every chunk: gaps >= 0xFFFF and counts != 1.
+__global__ __launch_bounds__(kWThreads) void k_wire_count(const uint64_t* __restrict__ codes,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint64_t* __restrict__ sstart,
+                                                          const uint64_t* __restrict__ sn,
+                                                          const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
+                                                          uint32_t* __restrict__ esc) {
+    __shared__ uint32_t ws[kWThreads / 64];
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
+        const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
+        uint32_t e = 0u;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            if (i < ch.n) {
+                const uint64_t code = codes[ch.base + i];
+                const uint64_t prev = i ? codes[ch.base + i - 1u] : code;
+                e += (code - prev >= (uint64_t)kWGapEsc) ? 1u : 0u;
+                e += counts[ch.base + i] != 1u ? 1u : 0u;
+            }
+        }
+        const uint32_t t = block_sum(e, ws);
+        if (tid == 0) esc[c] = t;
+    }
+}
+
+// Bytes of every slice: its records + its escapes (esc_off: exclusive scan of the chunks' escapes).
+__global__ __launch_bounds__(256) void k_wire_slice_bytes(const uint64_t* __restrict__ cbase,
+                                                          const unsigned long long* __restrict__ esc_off, uint32_t S,
+                                                          uint64_t* __restrict__ sbytes) {
+    const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+    if (s >= S) return;
+    const uint64_t c0 = cbase[s], c1 = cbase[s + 1];
+    sbytes[s] = (c1 - c0) * (uint64_t)kWRec + (uint64_t)(esc_off[c1] - esc_off[c0]) * kWEsc;
+}
+
+// Pack every chunk: record at sboff[s] + cl * kWRec, escapes in the slice's table.
+__global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restrict__ codes,
+                                                         const uint32_t* __restrict__ counts,
+                                                         const uint64_t* __restrict__ sstart,
+                                                         const uint64_t* __restrict__ sn,
+                                                         const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
+                                                         const unsigned long long* __restrict__ esc_off,
+                                                         const uint64_t* __restrict__ sboff, uint8_t* __restrict__ out) {
+    __shared__ uint32_t ws[kWThreads / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
+        const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
+        const uint64_t c0 = cbase[ch.s];
+        uint8_t* const rec = out + sboff[ch.s] + ch.cl * (uint64_t)kWRec;
+        uint8_t* const etab = out + sboff[ch.s] + (cbase[ch.s + 1] - c0) * (uint64_t)kWRec;
+        const unsigned long long e0 = esc_off[c] - esc_off[c0];   // the chunk's first escape in the slice
+        uint64_t code[kWPer], gap[kWPer];
+        uint32_t cnt[kWPer], ne = 0u;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            const bool v = i < ch.n;
+            code[j] = v ? codes[ch.base + i] : 0ull;
+            cnt[j] = v ? counts[ch.base + i] : 1u;
+            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code[j];
+            gap[j] = code[j] - prev;
+            ne += (gap[j] >= (uint64_t)kWGapEsc ? 1u : 0u) + (cnt[j] != 1u ? 1u : 0u);
+        }
+        // this thread's first escape: exclusive scan of ne over the workgroup
+        uint32_t incl = scan64(ne);
+        if (lane == 63u) ws[wave] = incl;
+        __syncthreads();
+        uint32_t pre = incl - ne, tot = 0u;
+#pragma unroll
+        for (int w = 0; w < kWThreads / 64; ++w) {
+            pre += (uint32_t)w < wave ? ws[w] : 0u;
+            tot += ws[w];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            *reinterpret_cast<uint64_t*>(rec) = code[0];
+            *reinterpret_cast<uint2*>(rec + 8) = make_uint2((uint32_t)e0, tot);
+        }
+        uint16_t* const g16 = reinterpret_cast<uint16_t*>(rec + kWHead);
+        uint4* const et = reinterpret_cast<uint4*>(etab) + e0 + pre;
+        uint32_t k = 0u;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            const bool ge = gap[j] >= (uint64_t)kWGapEsc, ce = cnt[j] != 1u;
+            g16[i] = ge ? (uint16_t)kWGapEsc : (uint16_t)gap[j];
+            const uint64_t bits = __ballot(ce);
+            if (lane == 0u) *reinterpret_cast<uint64_t*>(rec + kWBits + ((uint32_t)j * kWThreads + wave * 64u) / 8u) = bits;
+            if (ge) et[k++] = make_uint4(i, 0u, (uint32_t)gap[j], (uint32_t)(gap[j] >> 32));
+            if (ce) et[k++] = make_uint4(i | (1u << 16), 0u, cnt[j], 0u);
+        }
+    }
+}
+
+// Unpack every chunk of the received slices: slice s (entries sn[s]) at byte sboff[s] of `in`, its
+// entries to sdst[s] .. of the output.  Escape indices and counts are clamped to the slice's table, so
+// a damaged buffer cannot make a read or write leave the slice.
+__global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __restrict__ in,
+                                                           const uint64_t* __restrict__ sboff,
+                                                           const uint64_t* __restrict__ sn,
+                                                           const uint64_t* __restrict__ sesc,
+                                                           const uint64_t* __restrict__ sdst,
+                                                           const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
+                                                           uint64_t* __restrict__ out_codes,
+                                                           uint32_t* __restrict__ out_counts) {
+    __shared__ uint64_t ogap[kWChunk];
+    __shared__ uint32_t ocnt[kWChunk];
+    __shared__ uint64_t ws[kWThreads / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
+        const uint32_t s = slice_of(cbase, S, c);
+        const uint64_t c0 = cbase[s], cl = c - c0;
+        const uint64_t rem = sn[s] - cl * kWChunk;
+        const uint32_t n = (uint32_t)(rem < (uint64_t)kWChunk ? rem : (uint64_t)kWChunk);
+        const uint8_t* const rec = in + sboff[s] + cl * (uint64_t)kWRec;
+        const uint4* const etab = reinterpret_cast<const uint4*>(in + sboff[s] + (cbase[s + 1] - c0) * (uint64_t)kWRec);
+        const uint64_t anchor = *reinterpret_cast<const uint64_t*>(rec);
+        const uint2 eh = *reinterpret_cast<const uint2*>(rec + 8);
+        const uint64_t etot = sesc[s];
+        const uint64_t elo = eh.x < etot ? eh.x : etot;
+        const uint64_t en = (uint64_t)eh.y < etot - elo ? (uint64_t)eh.y : etot - elo;
+        for (uint64_t e = tid; e < en; e += kWThreads) {
+            const uint4 v = etab[elo + e];
+            const uint32_t i = v.x & (uint32_t)(kWChunk - 1);
+            if (v.x >> 16) ocnt[i] = v.z;
+            else ogap[i] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        }
+        __syncthreads();
+        const uint16_t* const g16 = reinterpret_cast<const uint16_t*>(rec + kWHead);
+        uint64_t carry = anchor;
+        uint64_t* const oc = out_codes + sdst[s] + cl * kWChunk;
+        uint32_t* const on = out_counts + sdst[s] + cl * kWChunk;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            const bool v = i < n;
+            const uint32_t g = v ? g16[i] : 0u;
+            const uint64_t gap = g == kWGapEsc ? ogap[i] : (uint64_t)g;
+            const uint64_t bits = *reinterpret_cast<const uint64_t*>(rec + kWBits + ((uint32_t)j * kWThreads + wave * 64u) / 8u);
+            const uint32_t cnt = (bits >> lane) & 1u ? ocnt[i] : 1u;
+            const uint64_t incl = wave_incl_u64(v ? gap : 0ull);
+            if (lane == 63u) ws[wave] = incl;
+            __syncthreads();
+            uint64_t pre = 0ull, tot = 0ull;
+#pragma unroll
+            for (int w = 0; w < kWThreads / 64; ++w) {
+                pre += (uint32_t)w < wave ? ws[w] : 0ull;
+                tot += ws[w];
+            }
+            __syncthreads();
+            if (v) {
+                oc[i] = carry + pre + incl;
+                on[i] = cnt;
+            }
+            carry += tot;
+        }
+    }
+}
+
+unsigned grid_for(Ctx* ctx, uint64_t NC) {
+    return (unsigned)std::min<uint64_t>(std::max<uint64_t>(NC, 1), (uint64_t)std::max(1, ctx->num_cu) * 16);
+}
+
+uint64_t fnv(uint64_t h, const uint64_t* p, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        h ^= p[i];
+        h *= 0x100000001B3ull;
+    }
+    return h;
+}
+
+}  // namespace
+
+int rows_cuts(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, const uint64_t* bounds, int nb,
+              uint64_t* d_cuts, hipStream_t s) {
+    if (R < 0 || nb < 0 || (R && !row_off) || (nb && !bounds)) return fail(ctx, KMH_ERR_INVALID, "bad cuts arguments");
+    if (!R || !nb) return KMH_OK;
+    if (!d_codes || !d_cuts) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    for (int r = 0; r < R; ++r)
+        if (row_off[r + 1] < row_off[r]) return fail(ctx, KMH_ERR_INVALID, "row offsets must ascend");
+    std::vector<uint64_t> h((size_t)R + 1 + nb);
+    std::copy(row_off, row_off + R + 1, h.begin());
+    std::copy(bounds, bounds + nb, h.begin() + R + 1);
+    int rc = ensure(ctx, ctx->wire[0], h.size() * 8 + 256);
+    if (rc) return rc;
+    uint64_t* d = static_cast<uint64_t*>(ctx->wire[0].ptr);
+    if ((rc = upload(ctx, d, h.data(), h.size() * 8, s))) return rc;
+    const uint64_t n = (uint64_t)R * (uint64_t)nb;
+    time_begin(ctx, s, "k_rows_cuts");
+    hipLaunchKernelGGL(k_rows_cuts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_codes, d, (uint32_t)R,
+                       d + R + 1, (uint32_t)nb, d_cuts);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+// The plan of S slices (host): chunk starts, chunks; uploads [sstart | sn | cbase] to wire[0].
+static int wire_layout(Ctx* ctx, const uint64_t* sstart, const uint64_t* sn, int S, std::vector<uint64_t>& cbase,
+                       uint64_t** d_plan, hipStream_t s) {
+    cbase.assign((size_t)S + 1, 0);
+    for (int i = 0; i < S; ++i) {
+        if (sn[i] >= (1ull << 40)) return fail(ctx, KMH_ERR_INVALID, "wire: slice too large");
+        cbase[i + 1] = cbase[i] + (sn[i] + kWChunk - 1) / kWChunk;
+    }
+    std::vector<uint64_t> h(3 * (size_t)S + 1 + S);
+    std::copy(sstart, sstart + S, h.begin());
+    std::copy(sn, sn + S, h.begin() + S);
+    std::copy(cbase.begin(), cbase.end(), h.begin() + 2 * S);
+    int rc = ensure(ctx, ctx->wire[0], h.size() * 8 + 256);
+    if (rc) return rc;
+    *d_plan = static_cast<uint64_t*>(ctx->wire[0].ptr);
+    return upload(ctx, *d_plan, h.data(), (3 * (size_t)S + 1) * 8, s);
+}
+
+// Count + scan + slice bytes of a plan (cached on the context by inputs and slices).
+static int wire_sizes(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* sstart,
+                      const uint64_t* sn, int S, std::vector<uint64_t>& cbase, uint64_t** d_plan,
+                      std::vector<uint64_t>& sbytes, hipStream_t s) {
+    int rc = wire_layout(ctx, sstart, sn, S, cbase, d_plan, s);
+    if (rc) return rc;
+    const uint64_t NC = cbase[S];
+    uint64_t key = fnv(0xCBF29CE484222325ull, sstart, S);
+    key = fnv(key, sn, S);
+    const uint64_t ptrs[3] = {(uint64_t)(uintptr_t)d_codes, (uint64_t)(uintptr_t)d_counts, (uint64_t)S};
+    key = fnv(key, ptrs, 3);
+    if (ctx->wire_valid && ctx->wire_key == key && ctx->wire_sbytes.size() == (size_t)S) {
+        sbytes = ctx->wire_sbytes;
+        return KMH_OK;
+    }
+    ctx->wire_valid = false;
+    if ((rc = ensure(ctx, ctx->wire[1], (NC + 1) * 4 + 256))) return rc;
+    if ((rc = ensure(ctx, ctx->wire[2], (NC + 2) * 8 + 256))) return rc;
+    uint32_t* d_esc = static_cast<uint32_t*>(ctx->wire[1].ptr);
+    unsigned long long* d_eoff = static_cast<unsigned long long*>(ctx->wire[2].ptr);
+    uint64_t* d_sb = *d_plan + 3 * (size_t)S + 1;
+    if (NC) {
+        time_begin(ctx, s, "k_wire_count");
+        hipLaunchKernelGGL(k_wire_count, dim3(grid_for(ctx, NC)), dim3(kWThreads), 0, s, d_codes, d_counts, *d_plan,
+                           *d_plan + S, *d_plan + 2 * S, (uint32_t)S, NC, d_esc);
+        time_end(ctx, s);
+        KMH_HIP(ctx, hipGetLastError());
+    }
+    if ((rc = scan_u32_u64(ctx, d_esc, (uint32_t)NC, d_eoff, s))) return rc;
+    hipLaunchKernelGGL(k_wire_slice_bytes, dim3((S + 255) / 256), dim3(256), 0, s, *d_plan + 2 * S, d_eoff, (uint32_t)S,
+                       d_sb);
+    KMH_HIP(ctx, hipGetLastError());
+    sbytes.assign(S, 0);
+    KMH_HIP(ctx, hipMemcpyAsync(sbytes.data(), d_sb, (size_t)S * 8, hipMemcpyDeviceToHost, s));
+    KMH_HIP(ctx, hipStreamSynchronize(s));
+    ctx->wire_key = key;
+    ctx->wire_sbytes = sbytes;
+    ctx->wire_valid = true;
+    return KMH_OK;
+}
+
+int wire_size(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* sstart, const uint64_t* sn,
+              int S, uint64_t* slice_bytes, hipStream_t s) {
+    if (S < 0 || (S && (!sstart || !sn || !slice_bytes))) return fail(ctx, KMH_ERR_INVALID, "bad wire arguments");
+    if (!S) return KMH_OK;
+    uint64_t NE = 0;
+    for (int i = 0; i < S; ++i) NE += sn[i];
+    if (NE && (!d_codes || !d_counts)) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    if ((uint64_t)S > (1ull << 24) || (NE + kWChunk) / kWChunk >= 0xFFFFFFFFull)
+        return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: too many slices or chunks");
+    std::vector<uint64_t> cbase, sb;
+    uint64_t* d_plan = nullptr;
+    int rc = wire_sizes(ctx, d_codes, d_counts, sstart, sn, S, cbase, &d_plan, sb, s);
+    if (rc) return rc;
+    for (int i = 0; i < S; ++i) {
+        const uint64_t nch = cbase[i + 1] - cbase[i];
+        if ((sb[i] - nch * kWRec) / kWEsc >= 0xFFFFFFFFull)
+            return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: 2^32 or more escapes in one slice");
+        slice_bytes[i] = sb[i];
+    }
+    return KMH_OK;
+}
+
+int wire_encode(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* sstart, const uint64_t* sn,
+                int S, uint8_t* d_out, uint64_t out_bytes, hipStream_t s) {
+    if (S < 0 || (S && (!sstart || !sn))) return fail(ctx, KMH_ERR_INVALID, "bad wire arguments");
+    if (!S) return KMH_OK;
+    std::vector<uint64_t> sb((size_t)S);
+    int rc = wire_size(ctx, d_codes, d_counts, sstart, sn, S, sb.data(), s);   // (cached if just sized)
+    if (rc) return rc;
+    std::vector<uint64_t> cbase, h((size_t)S);
+    uint64_t* d_plan = nullptr;
+    if ((rc = wire_sizes(ctx, d_codes, d_counts, sstart, sn, S, cbase, &d_plan, sb, s))) return rc;
+    uint64_t total = 0;
+    for (int i = 0; i < S; ++i) {
+        h[i] = total;
+        total += sb[i];
+    }
+    if (total > out_bytes) return fail(ctx, KMH_ERR_INVALID, "wire: output buffer too small");
+    if (total && !d_out) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    const uint64_t NC = cbase[S];
+    if (!NC) return KMH_OK;
+    uint64_t* d_sboff = d_plan + 3 * (size_t)S + 1;
+    if ((rc = upload(ctx, d_sboff, h.data(), (size_t)S * 8, s))) return rc;
+    time_begin(ctx, s, "k_wire_pack");
+    hipLaunchKernelGGL(k_wire_pack, dim3(grid_for(ctx, NC)), dim3(kWThreads), 0, s, d_codes, d_counts, d_plan, d_plan + S,
+                       d_plan + 2 * S, (uint32_t)S, NC, static_cast<const unsigned long long*>(ctx->wire[2].ptr),
+                       d_sboff, d_out);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+int wire_decode(Ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* sn, const uint64_t* sbytes,
+                const uint64_t* sdst, int S, uint64_t* d_codes, uint32_t* d_counts, hipStream_t s) {
+    if (S < 0 || (S && (!sn || !sbytes || !sdst))) return fail(ctx, KMH_ERR_INVALID, "bad wire arguments");
+    if (!S) return KMH_OK;
+    // plan: [sboff | sn | cbase | sesc | sdst]
+    std::vector<uint64_t> h(5 * (size_t)S + 1);
+    uint64_t* const sboff = h.data();
+    uint64_t* const hsn = sboff + S;
+    uint64_t* const cb = hsn + S;
+    uint64_t* const sesc = cb + S + 1;
+    uint64_t* const hdst = sesc + S;
+    uint64_t off = 0;
+    cb[0] = 0;
+    for (int i = 0; i < S; ++i) {
+        const uint64_t nch = (sn[i] + kWChunk - 1) / kWChunk;
+        if (sn[i] >= (1ull << 40) || sbytes[i] < nch * kWRec || (sbytes[i] - nch * kWRec) % kWEsc)
+            return fail(ctx, KMH_ERR_INVALID, "wire: slice bytes do not match its entries");
+        sboff[i] = off;
+        off += sbytes[i];
+        hsn[i] = sn[i];
+        cb[i + 1] = cb[i] + nch;
+        sesc[i] = (sbytes[i] - nch * kWRec) / kWEsc;
+        hdst[i] = sdst[i];
+    }
+    if (off > in_bytes) return fail(ctx, KMH_ERR_INVALID, "wire: input shorter than its slices");
+    const uint64_t NC = cb[S];
+    if (!NC) return KMH_OK;
+    if (!d_in || !d_codes || !d_counts) return fail(ctx, KMH_ERR_INVALID, "NULL device pointer");
+    int rc = ensure(ctx, ctx->wire[0], h.size() * 8 + 256);
+    if (rc) return rc;
+    uint64_t* d = static_cast<uint64_t*>(ctx->wire[0].ptr);
+    if ((rc = upload(ctx, d, h.data(), h.size() * 8, s))) return rc;
+    time_begin(ctx, s, "k_wire_unpack");
+    hipLaunchKernelGGL(k_wire_unpack, dim3(grid_for(ctx, NC)), dim3(kWThreads), 0, s, d_in, d, d + S, d + 3 * S + 1,
+                       d + 4 * S + 1, d + 2 * S, (uint32_t)S, NC, d_codes, d_counts);
+    time_end(ctx, s);
+    KMH_HIP(ctx, hipGetLastError());
+    return KMH_OK;
+}
+
+}  // namespace kmh

@@ -66,6 +66,11 @@ SIGNATURES = [
     ("kmh_count_sparse_sorted_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _c.c_int, _c.c_int, _vp, _vp, _vp, _vp,
                                                _vp]),
     ("kmh_shard_union_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _u64, _u64, _vp, _vp, _u64p, _vp]),
+    ("kmh_shard_union_u32_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _u64, _u64, _vp, _vp, _u64p, _vp]),
+    ("kmh_rows_cuts_dev", _c.c_int, [_vp, _vp, _vp, _c.c_int, _vp, _c.c_int, _vp, _vp]),
+    ("kmh_wire_size_dev", _c.c_int, [_vp, _vp, _vp, _vp, _vp, _c.c_int, _vp, _vp]),
+    ("kmh_wire_encode_dev", _c.c_int, [_vp, _vp, _vp, _vp, _vp, _c.c_int, _vp, _u64, _vp]),
+    ("kmh_wire_decode_dev", _c.c_int, [_vp, _vp, _u64, _vp, _vp, _vp, _c.c_int, _vp, _vp, _vp]),
     ("kmh_sparse_out_offsets", _u64, [_vp, _c.c_int, _c.c_int, _vp]),
     ("kmh_rows_encode_u8_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
     ("kmh_rows_encode_u4_dev", _c.c_int, [_vp, _vp, _u64, _u64, _vp, _vp, _c.c_uint32, _vp, _vp]),
@@ -300,16 +305,57 @@ class Context:
                                                  ctypes.c_void_p(stream) if stream else None), self._h)
 
     @_locked
-    def shard_union_dev(self, d_codes, row_off, lo_code, hi_code_incl, d_columns, d_indices, stream=None):
+    def shard_union_dev(self, d_codes, row_off, lo_code, hi_code_incl, d_columns, d_indices, stream=None,
+                        idx32=False):
         """kmh_shard_union_dev: the sorted union of R sorted rows (row r = d_codes[row_off[r],
-        row_off[r + 1]), host offsets) into d_columns and every entry's column into d_indices;
-        returns the union's size."""
+        row_off[r + 1]), host offsets) into d_columns and every entry's column into d_indices
+        (int64, or u32 with idx32=True: kmh_shard_union_u32_dev); returns the union's size."""
         ro = np.ascontiguousarray(row_off, dtype=np.uint64)
         n = ctypes.c_uint64(0)
-        _check(lib().kmh_shard_union_dev(self._h, ctypes.c_void_p(d_codes), _ptr(ro), ro.size - 1, int(lo_code),
-                                         int(hi_code_incl), ctypes.c_void_p(d_columns), ctypes.c_void_p(d_indices),
-                                         ctypes.byref(n), ctypes.c_void_p(stream) if stream else None), self._h)
+        fn = lib().kmh_shard_union_u32_dev if idx32 else lib().kmh_shard_union_dev
+        _check(fn(self._h, ctypes.c_void_p(d_codes), _ptr(ro), ro.size - 1, int(lo_code), int(hi_code_incl),
+                  ctypes.c_void_p(d_columns), ctypes.c_void_p(d_indices), ctypes.byref(n),
+                  ctypes.c_void_p(stream) if stream else None), self._h)
         return int(n.value)
+
+    # -- the config-5 exchange (kmh_wire.hip) --
+    @_locked
+    def rows_cuts_dev(self, d_codes, row_off, bounds, d_cuts, stream=None):
+        """kmh_rows_cuts_dev: d_cuts[r * nb + b] (device u64) = the first entry of sorted row r (host
+        row_off) whose code is >= bounds[b] (host uint64 array)."""
+        ro = np.ascontiguousarray(row_off, dtype=np.uint64)
+        b = np.ascontiguousarray(bounds, dtype=np.uint64)
+        _check(lib().kmh_rows_cuts_dev(self._h, ctypes.c_void_p(d_codes), _ptr(ro), ro.size - 1, _ptr(b), b.size,
+                                       ctypes.c_void_p(d_cuts), ctypes.c_void_p(stream) if stream else None), self._h)
+
+    @_locked
+    def wire_size_dev(self, d_codes, d_counts, slice_start, slice_n, stream=None):
+        """kmh_wire_size_dev: bytes of every slice in the compact wire format (uint64 array)."""
+        st = np.ascontiguousarray(slice_start, dtype=np.uint64)
+        sn = np.ascontiguousarray(slice_n, dtype=np.uint64)
+        out = np.zeros(st.size, np.uint64)
+        _check(lib().kmh_wire_size_dev(self._h, ctypes.c_void_p(d_codes), ctypes.c_void_p(d_counts), _ptr(st), _ptr(sn),
+                                       st.size, _ptr(out), ctypes.c_void_p(stream) if stream else None), self._h)
+        return out
+
+    @_locked
+    def wire_encode_dev(self, d_codes, d_counts, slice_start, slice_n, d_out, out_bytes, stream=None):
+        """kmh_wire_encode_dev: the slices back to back at d_out (device)."""
+        st = np.ascontiguousarray(slice_start, dtype=np.uint64)
+        sn = np.ascontiguousarray(slice_n, dtype=np.uint64)
+        _check(lib().kmh_wire_encode_dev(self._h, ctypes.c_void_p(d_codes), ctypes.c_void_p(d_counts), _ptr(st),
+                                         _ptr(sn), st.size, ctypes.c_void_p(d_out), int(out_bytes),
+                                         ctypes.c_void_p(stream) if stream else None), self._h)
+
+    @_locked
+    def wire_decode_dev(self, d_in, in_bytes, slice_n, slice_bytes, slice_dst, d_codes, d_counts, stream=None):
+        """kmh_wire_decode_dev: slices back to back at d_in -> entries slice_dst[i] .. of d_codes / d_counts."""
+        sn = np.ascontiguousarray(slice_n, dtype=np.uint64)
+        sb = np.ascontiguousarray(slice_bytes, dtype=np.uint64)
+        sd = np.ascontiguousarray(slice_dst, dtype=np.uint64)
+        _check(lib().kmh_wire_decode_dev(self._h, ctypes.c_void_p(d_in), int(in_bytes), _ptr(sn), _ptr(sb), _ptr(sd),
+                                         sn.size, ctypes.c_void_p(d_codes), ctypes.c_void_p(d_counts),
+                                         ctypes.c_void_p(stream) if stream else None), self._h)
 
     # -- matrix assembly encoding (device pointers) --
     @_locked

@@ -448,7 +448,9 @@ class ShardedSparseMatrix:
 
       columns  uint64 [ncols]   the sorted union of the organisms' codes in the range
       indptr   int64  [G + 1]   organism g's entries are indptr[g] .. indptr[g + 1]
-      indices  int64  [nnz]     column index of each entry (ascending within an organism)
+      indices  int64  [nnz]     column index of each entry (ascending within an organism); on the
+                                device u32 (int32 storage) when nnz < 2^32 - 1: read it through
+                                column_indices()
       values   uint32 [nnz]     its count
 
     Codes are 2-bit A0 C1 G2 T3, first base most significant, so code order is the string order
@@ -477,10 +479,36 @@ class ShardedSparseMatrix:
         """The same shard with numpy arrays (columns uint64, indices int64, values uint32)."""
         if not self.on_device:
             return self
+        ix = self.indices.cpu().numpy()
+        if ix.dtype == np.int32:   # u32 indices in int32 storage
+            ix = ix.view(np.uint32).astype(np.int64)
         return ShardedSparseMatrix(self.k, self.G, self.lo_code, self.hi_code,
                                    self.columns.cpu().numpy().view(np.uint64), np.asarray(self.indptr, np.int64),
-                                   self.indices.cpu().numpy(), self.values.cpu().numpy().view(np.uint32),
-                                   self.rank, self.world)
+                                   ix, self.values.cpu().numpy().view(np.uint32), self.rank, self.world)
+
+    def column_indices(self, a=0, b=None):
+        """Entries [a, b)'s column indices as int64 (a device tensor on the GPU path, whose u32
+        indices are widened here)."""
+        b = self.nnz if b is None else b
+        ix = self.indices[a:b]
+        if self.on_device:
+            import torch
+            if ix.dtype == torch.int32:
+                return ix.to(torch.int64) & 0xFFFFFFFF
+        return ix
+
+    def all_columns_used(self, chunk=1 << 28):
+        """True iff every column holds at least one entry (the union has no stray column); chunked
+        so that widening u32 indices never needs more than `chunk` int64 entries."""
+        if not self.on_device:
+            used = np.zeros(self.columns.size, bool)
+            used[self.indices] = True
+            return bool(used.all())
+        import torch
+        used = torch.zeros(self.columns.numel(), dtype=torch.uint8, device=self.columns.device)
+        for a in range(0, self.nnz, chunk):
+            used[self.column_indices(a, min(self.nnz, a + chunk))] = 1
+        return bool(torch.all(used == 1).item())
 
     def __getstate__(self):   # all_gather_object and pickling carry the host form
         return self.host().__dict__
@@ -555,7 +583,9 @@ def sparse_matrix(genome_files, k, canonical=True, device=None, group=None, rows
 
     files = list(genome_files)
     G = len(files)
-    if rows_fn is None and 13 <= k <= 32:   # device-resident: sorted rows, all-to-all, kmh_shard_union_dev
+    if rows_fn is None and 13 <= k <= 32 and G <= SHARD_MAX_ROWS:
+        # device-resident: sorted rows, all-to-all, kmh_shard_union_dev (at most SHARD_MAX_ROWS
+        # organism rows per shard; larger matrices take the host assembly below)
         return _sparse_matrix_dev(files, k, canonical, device, group)
     if rows_fn is None:
         lo, rows = sparse_rows(files, k, canonical=canonical, device=device, group=group)
@@ -670,46 +700,42 @@ def sorted_rows_from_device(d_seq, offsets, k, canonical=True, timings=None):
     return codes, counts, roff   # back to back from entry 0
 
 
+def _stream(dev):
+    import torch
+
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _rows_cuts(codes, roff, bounds):
+    """[n, nb] int64 device tensor: for every sorted row i = codes[roff[i], roff[i + 1]) (host roff)
+    the first entry (relative to the row) whose code is >= each bound (kmh_rows_cuts_dev; codes
+    compared as u64, so k = 32 needs no sign flip)."""
+    import torch
+
+    n, nb = roff.size - 1, len(bounds)
+    out = torch.zeros((max(n, 1), max(nb, 1)), dtype=torch.int64, device=codes.device)
+    if n and nb and int(roff[-1]) > int(roff[0]):
+        _native.context(codes.device.index).rows_cuts_dev(codes.data_ptr(), roff, np.asarray(bounds, np.uint64),
+                                                           out.data_ptr(), _stream(codes.device))
+    return out[:n, :nb]
+
+
 def _row_histogram(codes, roff, k, nbits=16):
-    """Counts of the rows' codes per top-`nbits`-bit prefix (a device searchsorted over the sorted
-    rows: no pass over the entries)."""
+    """Counts of the rows' codes per top-`nbits`-bit prefix, a device int64 tensor (the rows' cuts at
+    every prefix edge, kmh_rows_cuts_dev: binary searches, no pass over the entries)."""
     import torch
 
     bits = 2 * k
     sh = max(bits - nbits, 0)
     nb = 1 << min(bits, nbits)
+    n = roff.size - 1
     dev = codes.device
-    hist = np.zeros(nb, np.int64)
-    if codes.numel() == 0:
-        return hist
-    # signed view of u64 codes: order-preserving after flipping the top bit when k = 32
-    flip = k == 32
-    edges = torch.arange(1, nb, dtype=torch.int64, device=dev) << sh
-    if flip:
-        edges = edges ^ torch.iinfo(torch.int64).min
-    for r in range(roff.size - 1):
-        a, b = int(roff[r]), int(roff[r + 1])
-        if b == a:
-            continue
-        row = codes[a:b]
-        if flip:
-            row = row ^ torch.iinfo(torch.int64).min
-        cuts = torch.searchsorted(row, edges).cpu().numpy()
-        hist += np.diff(np.concatenate(([0], cuts, [b - a])))
-    return hist
-
-
-def _cuts(codes, a, b, bounds, k):
-    """Positions in the sorted row codes[a:b] of the code bounds (each the first entry >= bound)."""
-    import torch
-
-    row = codes[a:b]
-    e = torch.tensor([min(x, (1 << 64) - 1) for x in bounds], dtype=torch.uint64).view(torch.int64).to(codes.device)
-    if k == 32:
-        row = row ^ torch.iinfo(torch.int64).min
-        e = e ^ torch.iinfo(torch.int64).min
-    c = torch.searchsorted(row, e).cpu().numpy().astype(np.int64)
-    return c
+    if n == 0:
+        return torch.zeros(nb, dtype=torch.int64, device=dev)
+    cuts = _rows_cuts(codes, roff, [i << sh for i in range(1, nb)])
+    lens = torch.from_numpy(np.diff(roff).astype(np.int64)).to(dev)
+    full = torch.cat([torch.zeros((n, 1), dtype=torch.int64, device=dev), cuts, lens[:, None]], 1)
+    return (full[:, 1:] - full[:, :-1]).sum(0)
 
 
 def _sparse_matrix_dev(files, k, canonical, device, group):
@@ -718,89 +744,232 @@ def _sparse_matrix_dev(files, k, canonical, device, group):
     return shard_from_rows(codes, counts, roff, len(files), k, group=group)
 
 
-def shard_from_rows(codes, counts, roff, G, k, group=None):
-    """This rank's ShardedSparseMatrix from its sorted device rows (genomes shard_bounds(G, W,
-    rank), row i = codes / counts [roff[i], roff[i + 1])): with W > 1 ranks the code space is cut
-    into W ranges of ~equal entries (an all-reduced histogram of the codes' top 16 bits, from a
-    device searchsorted of the sorted rows) and one all_to_all_single per genome index of the
-    ranks' blocks sends every row's slice of each range to its rank (RCCL over xGMI, or gloo);
-    then kmh_shard_union_dev builds the columns (sorted union) and the CSR indices on the device.
-    Every array stays in device memory; `codes` / `counts` may be consumed."""
+# the exchange of the last shard_from_rows call with W > 1 ranks (bench / tests): wire format, bytes
+# this rank sent and received over the all-to-all, and their raw (12 B per entry) equivalent
+LAST_EXCHANGE = None
+WIRE_RECORD_ENTRIES = 1024        # entries per record of the compact wire (kmh_wire.hip)
+SHARD_MAX_ROWS = 4096             # kmh_shard_union_dev's limit on the organism rows of one shard
+
+
+def shard_plan(codes, roff, bounds, rank):
+    """The slices this rank's sorted rows send to every rank's code range [bounds[q], bounds[q + 1]):
+    returns (send_len [n, W] int64: entries of row j in range q, starts [n, W] int64: their first
+    entry in `codes`).  One device cuts call and one host copy."""
+    n, W = roff.size - 1, len(bounds) - 1
+    lens = np.diff(roff).astype(np.int64)
+    cuts = _rows_cuts(codes, roff, bounds[1:-1]).cpu().numpy() if n else np.zeros((0, W - 1), np.int64)
+    full = np.concatenate([np.zeros((n, 1), np.int64), cuts, lens[:, None]], 1)
+    return np.diff(full, axis=1), roff[:-1].astype(np.int64)[:, None] + full[:, :-1]
+
+
+def _a2a(out, inp, out_splits, in_splits, gloo, group):
     import torch
     import torch.distributed as dist
 
+    if gloo:   # gloo exchanges host tensors
+        ho = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(ho)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+    return out
+
+
+def shard_from_rows(codes, counts, roff, G, k, group=None, wire="auto", timings=None):
+    """This rank's ShardedSparseMatrix from its sorted device rows (genomes shard_bounds(G, W,
+    rank), row i = codes / counts [roff[i], roff[i + 1])).  With W > 1 ranks:
+
+      1. the code space is cut into W ranges of ~equal entries: an all-reduced histogram of the
+         codes' top 16 bits, from the rows' cuts at every prefix edge (kmh_rows_cuts_dev);
+      2. the rows' cuts at the W - 1 range bounds give every (row, rank) slice (one host copy) and
+         one all_gather tells every rank what it receives;
+      3. the slices for the other ranks are packed in the compact wire format (kmh_wire_encode_dev,
+         ~2.2 B per entry against 12; wire="raw" sends u64 codes + u32 counts, and "auto" falls back
+         to raw when the packed bytes would be larger, e.g. k = 32 codes with 40-bit gaps), sent by
+         ONE all_to_all_single (RCCL over xGMI, or gloo), and unpacked straight into the shard's row
+         layout (kmh_wire_decode_dev); the rank's own slices are device copies;
+      4. kmh_shard_union(_u32)_dev builds the columns (the sorted union: features.py:96-111) and
+         the CSR indices, u32 whenever the shard holds fewer than 2^32 - 1 entries.
+
+    Every array stays in device memory.  `timings` (a dict) receives per-phase wall ms (each phase
+    synchronised; bench)."""
+    import time
+    import torch
+    import torch.distributed as dist
+
+    global LAST_EXCHANGE
     dist_on = dist.is_available() and dist.is_initialized()
     world = dist.get_world_size(group) if dist_on else 1
     rank = dist.get_rank(group) if dist_on else 0
     dev = codes.device
     n = roff.size - 1
+    ctx = _native.context(dev.index)
+    s = _stream(dev)
+    tick = [time.perf_counter()]
+
+    def phase(name):
+        if timings is not None:
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            timings[name] = timings.get(name, 0.0) + (t - tick[0]) * 1e3
+            tick[0] = t
+
     if world == 1:   # one shard: every genome's row, the whole code space
         rc, rn, indptr, lo_code, hi_code = codes, counts, roff.astype(np.int64), 0, 1 << (2 * k)
     else:
-        hist = torch.from_numpy(_row_histogram(codes, roff, k))
         gloo = dist.get_backend(group) == "gloo"
-        t = hist if gloo else hist.to(dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        tot = t.cpu().numpy()
-        bounds = _splitters_from_hist(tot, k, world)
+        hist = _row_histogram(codes, roff, k)
+        if gloo:
+            hist = hist.cpu()
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        bounds = _splitters_from_hist(hist.cpu().numpy(), k, world)
+        send_len, starts = shard_plan(codes, roff, bounds, rank)
+        phase("plan_ms")
         B = block_rows(G, world)
-        # send_len[j, q]: entries of my genome j in rank q's range
-        send_len = np.zeros((B, world), np.int64)
-        for j in range(n):
-            a, b = int(roff[j]), int(roff[j + 1])
-            c = _cuts(codes, a, b, bounds[1:-1], k) if b > a else np.zeros(world - 1, np.int64)
-            send_len[j] = np.diff(np.concatenate(([0], c, [b - a])))
-        lt = torch.from_numpy(send_len) if gloo else torch.from_numpy(send_len).to(dev)
+        others = [q for q in range(world) if q != rank]
+        sl_start = np.array([starts[j, q] for q in others for j in range(n)], np.uint64)
+        sl_n = np.array([send_len[j, q] for q in others for j in range(n)], np.uint64)
+        raw_bytes = int(sl_n.sum()) * 12
+        mode = wire
+        sl_bytes = sl_n * np.uint64(12)
+        if wire in ("auto", "compact"):
+            sl_bytes = ctx.wire_size_dev(codes.data_ptr(), counts.data_ptr(), sl_start, sl_n, s) if sl_n.size else sl_n
+            if wire == "auto":   # every rank must choose the same format
+                t = torch.tensor([int(sl_bytes.sum()), raw_bytes], dtype=torch.int64)
+                if not gloo:
+                    t = t.to(dev)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+                t = t.cpu()
+                mode = "compact" if int(t[0]) < int(t[1]) else "raw"
+            if mode == "raw":
+                sl_bytes = sl_n * np.uint64(12)
+        # every rank learns (entries, bytes) of every (source, genome index, destination) slice
+        mine = np.zeros((B, world, 2), np.int64)
+        mine[:n, :, 0] = send_len
+        for i, q in enumerate(others):
+            mine[:n, q, 1] = sl_bytes[i * n:(i + 1) * n].astype(np.int64)
+        lt = torch.from_numpy(mine) if gloo else torch.from_numpy(mine).to(dev)
         parts = [torch.zeros_like(lt) for _ in range(world)]
         dist.all_gather(parts, lt, group=group)
-        lens = np.stack([t.cpu().numpy() for t in parts])   # lens[src, j, dst]
-        # receive layout: genome-major; genome g = block of source src, index j
+        lens = np.stack([t.cpu().numpy() for t in parts])   # lens[src, j, dst, (entries, bytes)]
+        # receive layout: genome-major (= source-major: rank src holds genomes shard_bounds(G, W, src))
         gl = np.zeros(G, np.int64)
+        gsrc = []
         for src in range(world):
             glo, ghi = shard_bounds(G, world, src)
-            for j in range(ghi - glo):
-                gl[glo + j] = lens[src, j, rank]
+            gl[glo:ghi] = lens[src, :ghi - glo, rank, 0]
+            gsrc.append((glo, ghi))
         indptr = np.zeros(G + 1, np.int64)
         np.cumsum(gl, out=indptr[1:])
         total = int(indptr[-1])
+        phase("sizes_ms")
         rc = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
         rn = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
-        for j in range(B):
-            in_splits = [int(x) for x in (send_len[j] if j < n else np.zeros(world, np.int64))]
-            out_splits = [int(lens[src, j, rank]) for src in range(world)]
+        lo_g = gsrc[rank][0]
+        if mode == "raw":   # u64 codes + u32 counts, the rank's own slices included
+            sel = [(int(starts[j, q]), int(send_len[j, q])) for q in range(world) for j in range(n)]
+            in_splits = [int(send_len[:, q].sum()) for q in range(world)]
+            out_splits = [int(lens[src, :, rank, 0].sum()) for src in range(world)]
             for src_t, dst_t in ((codes, rc), (counts, rn)):
-                if j < n:
-                    a = int(roff[j])
-                    inp = src_t[a:a + sum(in_splits)]
-                else:
-                    inp = src_t[:0]
-                out = torch.empty(sum(out_splits), dtype=src_t.dtype, device=dev)
-                if gloo:
-                    ho = torch.empty(sum(out_splits), dtype=src_t.dtype)
-                    dist.all_to_all_single(ho, inp.cpu(), out_splits, in_splits, group=group)
-                    out.copy_(ho)
-                else:
-                    dist.all_to_all_single(out, inp.contiguous(), out_splits, in_splits, group=group)
-                pos = 0
-                for src in range(world):
-                    glo, ghi = shard_bounds(G, world, src)
-                    m = out_splits[src]
-                    if j < ghi - glo and m:
-                        g = glo + j
-                        dst_t[int(indptr[g]):int(indptr[g]) + m].copy_(out[pos:pos + m])
-                    pos += m
+                inp = torch.cat([src_t[a:a + m] for a, m in sel] + [src_t[:0]])
+                _a2a(dst_t[:total], inp, out_splits, in_splits, gloo, group)
+                del inp
+            sent, received = raw_bytes, int(sum(out_splits[q] for q in others)) * 12
+            phase("exchange_ms")
+        else:
+            for j in range(n):   # the rank's own slices: device copies into place
+                a, m, d = int(starts[j, rank]), int(send_len[j, rank]), int(indptr[lo_g + j])
+                if m:
+                    rc[d:d + m].copy_(codes[a:a + m])
+                    rn[d:d + m].copy_(counts[a:a + m])
+            nbytes = int(sl_bytes.sum())
+            send = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
+            if sl_n.size:
+                ctx.wire_encode_dev(codes.data_ptr(), counts.data_ptr(), sl_start, sl_n, send.data_ptr(), nbytes, s)
+            phase("encode_ms")
+            in_splits = [0 if q == rank else int(sl_bytes[others.index(q) * n:(others.index(q) + 1) * n].sum())
+                         for q in range(world)]
+            out_splits = [0 if src == rank else int(lens[src, :, rank, 1].sum()) for src in range(world)]
+            recv = torch.empty(max(sum(out_splits), 16), dtype=torch.uint8, device=dev)
+            _a2a(recv[:sum(out_splits)], send[:nbytes], out_splits, in_splits, gloo, group)
+            del send
+            phase("exchange_ms")
+            rs_n, rs_b, rs_d = [], [], []
+            for src in others:
+                glo, ghi = gsrc[src]
+                for j in range(ghi - glo):
+                    rs_n.append(lens[src, j, rank, 0])
+                    rs_b.append(lens[src, j, rank, 1])
+                    rs_d.append(indptr[glo + j])
+            if rs_n:
+                ctx.wire_decode_dev(recv.data_ptr(), sum(out_splits), np.array(rs_n, np.uint64),
+                                    np.array(rs_b, np.uint64), np.array(rs_d, np.uint64), rc.data_ptr(),
+                                    rn.data_ptr(), s)
+            del recv
+            sent, received = nbytes, sum(out_splits)
+            phase("decode_ms")
+        LAST_EXCHANGE = {"wire": mode, "sent_bytes": int(sent), "received_bytes": int(received),
+                         "raw_sent_bytes": raw_bytes,
+                         "raw_received_bytes": int(sum(lens[src, :, rank, 0].sum() for src in others)) * 12,
+                         "entries_in": int(np.diff(roff).sum()) if n else 0, "entries_out": total}
         del codes, counts
         lo_code, hi_code = bounds[rank], bounds[rank + 1]
     total = int(indptr[-1])
+    if total and indptr.size - 1 > SHARD_MAX_ROWS:
+        raise NotImplementedError(f"kmh_shard_union_dev holds at most {SHARD_MAX_ROWS} organism rows per shard "
+                                  f"(got {indptr.size - 1}); sparse_matrix routes such matrices to the host path")
+    idx32 = total < 0xFFFFFFFF
     columns = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
-    indices = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    indices = torch.empty(max(total, 1), dtype=torch.int32 if idx32 else torch.int64, device=dev)
     ncols = 0
     if total and hi_code > lo_code:
-        ctx = _native.context(dev.index)
-        ncols = ctx.shard_union_dev(rc.data_ptr(), indptr.astype(np.uint64), lo_code, hi_code - 1,
-                                    columns.data_ptr(), indices.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        ncols = ctx.shard_union_dev(rc.data_ptr(), indptr.astype(np.uint64), lo_code, hi_code - 1, columns.data_ptr(),
+                                    indices.data_ptr(), s, idx32=idx32)
+    elif total:
+        raise RuntimeError(f"rank {rank} received {total} entries for the empty code range [{lo_code}, {hi_code})")
+    phase("union_ms")
     return ShardedSparseMatrix(k, G, lo_code, hi_code, columns[:ncols], indptr, indices[:total], rn[:total],
                                rank, world)
+
+
+def shard_check(m, windows_total, group=None):
+    """Global checks of a column-sharded matrix (every rank calls it; returns (ok, summary)): within
+    the rank, columns strictly ascending and every column used; across ranks, sum(values) over all
+    shards = windows_total (every window of every genome counted exactly once: a slice lost or sent
+    twice by the exchange changes it), sum(nnz) consistent with it, and rank q's last column below
+    rank q + 1's first.  Returns the all-reduced summary (nnz, values, columns)."""
+    import torch
+    import torch.distributed as dist
+
+    cols = m.columns
+    dev = cols.device
+    ok = bool(torch.all(cols[1:] > cols[:-1]).item()) if cols.numel() > 1 else True
+    ok = ok and m.all_columns_used()
+    vsum = int((m.values.to(torch.int64) & 0xFFFFFFFF).sum().item()) if m.nnz else 0
+    # (k = 32 codes use all 64 bits: as int64 they would not order; compare the unsigned values)
+    first = int(cols[0].item()) & 0xFFFFFFFFFFFFFFFF if cols.numel() else None
+    last = int(cols[-1].item()) & 0xFFFFFFFFFFFFFFFF if cols.numel() else None
+    ok = ok and all(m.lo_code <= c < m.hi_code for c in (first, last) if c is not None)
+    world = m.world
+    if world > 1:
+        gloo = dist.get_backend(group) == "gloo"
+        t = torch.tensor([m.nnz, vsum, int(cols.numel()), 0 if ok else 1], dtype=torch.int64)
+        t = t if gloo else t.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        nnz, vsum, ncols, bad = (int(x) for x in t.cpu().tolist())
+        ends = [None] * world
+        dist.all_gather_object(ends, (m.rank, first, last), group=group)
+        ok = bad == 0
+        prev = None
+        for _, f, l in sorted(ends):
+            if f is None:
+                continue
+            ok = ok and (prev is None or prev < f)
+            prev = l
+    else:
+        nnz, ncols = m.nnz, int(cols.numel())
+    ok = ok and vsum == windows_total and ncols <= nnz <= vsum
+    return ok, {"nnz": nnz, "values": vsum, "columns": ncols}
 
 
 def _splitters_from_hist(hist, k, world):
@@ -813,10 +982,13 @@ def _splitters_from_hist(hist, k, world):
     total = int(cum[-1]) if cum.size else 0
     # bucket indices stay unshifted (monotone, <= nb) until the end; the last bound is the
     # code space's end, 1 << 64 at k = 32 (a Python int: never converted to uint64)
+    # inner bounds at most (nb - 1) << sh, so every one stays below the code space's end (< 2^64 at
+    # k = 32: a bound of 1 << 64 would not survive the uint64 conversions of the exchange); ranks
+    # past a bound in the last bucket get an empty range
     idx = [0]
     for q in range(1, world):
         b = int(np.searchsorted(cum, total * q / world, side="left")) + 1 if total else (nb * q) // world
-        idx.append(max(idx[-1], min(b, nb)))
+        idx.append(max(idx[-1], min(b, nb - 1)))
     return [i << sh for i in idx] + [1 << bits]
 
 

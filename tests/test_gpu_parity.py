@@ -993,6 +993,41 @@ def test_bench_simulated_rank():
     assert d["config"]["workload"].startswith("projection")
 
 
+def test_bench_config5_object_two_ranks():
+    """at N > 1 the dense line carries a config5 object -- every rank counts its
+    genomes (k = 21 canonical) and the matrix leg's all-to-all runs in the compact wire -- and the
+    global check (values summing to every window of every genome, column ranges in rank order)
+    passes.  Two ranks sharing cuda:0 over gloo, at rehearsal sizes (labelled so)."""
+    r = _torchrun(["bench.py", "--gpus", "2", "--backend", "gloo", "--single-device", "--genomes", "4",
+                   "--genome-len", "3000000", "--k", "10", "--steps", "2", "--warmup", "1", "--cpu-sample", "0",
+                   "--config5-genomes-per-rank", "2", "--config5-genome-len", "3000000"], nproc=2, timeout=600)
+    assert r.returncode == 0, _failure(r)
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    c5 = d["config5"]
+    assert c5["rows_checked"] is True and c5["n_gpus"] == 2 and c5["config"]["workload"].startswith("rehearsal")
+    mx = c5["matrix"]
+    assert mx["shard_checked"] is True and mx["global"]["values"] == mx["global_windows"] == 4 * (3_000_000 - 20)
+    ex = mx["exchange"]
+    assert ex["wire"] == "compact" and 0 < ex["sent_bytes"] < ex["raw_sent_bytes"] / 4, ex
+    assert ex["received_bytes"] > 0 and ex["bytes_per_entry"] < 3
+
+
+def test_bench_sparse_simulated_rank():
+    """bench.py --workload sparse --simulate-ranks N, one rank of config 5's matrix
+    at N GPUs on one GPU: the other ranks' slices of its range really counted, packed and unpacked,
+    the union at R = N x genomes rows, the shard checked (every entry of the range arrived, columns
+    ascending and used); the line is labelled a projection and names the assumed link rate."""
+    r = _torchrun(["bench.py", "--workload", "sparse", "--simulate-ranks", "4", "--genomes", "2",
+                   "--genome-len", "3000000", "--steps", "1"], timeout=600)
+    assert r.returncode == 0, _failure(r)
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["simulated_ranks"] == 4 and d["config"]["workload"].startswith("projection")
+    assert d["shard"]["checked"] is True and d["shard"]["rows"] == 8
+    ex = d["exchange"]
+    assert ex["wire"] == "compact" and 0 < ex["received_bytes"] < ex["raw_received_bytes"] / 4
+    assert d["projected_ms_per_step"] > d["ms_per_step"] > 0
+
+
 @pytest.mark.parametrize("k", [6, 10])
 def test_from_count_matrix_gpu_equals_file_path(tmp_path, k):
     """Row f4 end to end: the GPU count matrix (kmerml.kmers.matrix.count_matrix, and its
@@ -1222,36 +1257,59 @@ def test_dropin_workspace_trim_and_staging(ctx, oracle_lib, monkeypatch):
         c.count_staged(21)
 
 
-@pytest.mark.parametrize("backend,nproc", [("nccl", 1), ("gloo", 2)])
-def test_sparse_matrix_sharded_on_gpu(tmp_path, oracle_lib, backend, nproc):
-    """kmerml.kmers.matrix.sparse_matrix on the GPU path: genomes counted by
-    the batched hash-table pipeline at k = 21 canonical, column shards assembled by all-to-all-v
-    (RCCL with one rank; gloo with two ranks sharing cuda:0).  The shards side by side must equal
-    the organisms x k-mers matrix of the oracle's counts (features.py:85-117's layout: sorted union
-    of k-mers, missing = 0)."""
-    files, rows = [], []
-    for i in range(3):
+@pytest.mark.parametrize("backend,nproc,k,canonical,wire,G", [
+    ("nccl", 1, 21, True, "auto", 3), ("gloo", 2, 21, True, "auto", 3), ("gloo", 2, 21, True, "raw", 3),
+    ("gloo", 3, 32, False, "auto", 2), ("gloo", 2, 32, False, "compact", 3), ("gloo", 4, 13, True, "compact", 5)])
+def test_sparse_matrix_sharded_on_gpu(tmp_path, oracle_lib, backend, nproc, k, canonical, wire, G):
+    """The column-sharded matrix on the GPU path:
+    each rank's genomes counted in code order on the GPU (kmh_count_sparse_sorted_dev), the code
+    space cut by the rows' device cuts, one all-to-all of the slices in the compact wire format
+    (kmh_wire_encode/decode_dev) or raw, and kmh_shard_union_u32_dev (RCCL with one rank; gloo with
+    2-4 ranks sharing cuda:0).  The shards side by side must equal the organisms x k-mers matrix of
+    the oracle's counts (features.py:85-117's layout: sorted union of k-mers, missing = 0), and every
+    rank's global check (shard_check: values summing to every window, ranks' column ranges in order)
+    must pass.  Cases: repeated k-mers and a poly-A run (counts > 1 in escapes); k = 32 forward with a
+    poly-T run (the code 2^64 - 1, the last top-16-bit bucket) at world 3 > G = 2, so that a rank
+    holds no genome; k = 32 forced through the compact wire (every gap escaped); k = 13 at world 4."""
+    files, rows, windows = [], [], 0
+    for i in range(G):
         p = tmp_path / f"g{i}.fa"
         seq = osynth.synth_bases(120_000 + 9_000 * i, osynth.genome_seed(60 + i)).tobytes()
         if i == 2:
             seq = seq + seq[:30_000]   # k-mers counted twice
+        if i == 1:
+            seq = seq + b"A" * 5_000 + b"T" * 3_000   # counts of thousands; top-bucket codes
         osynth.write_fasta(p, [(f"SYN_{i}", seq)])
         files.append(str(p))
-        c, n, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), 21, canonical=True)
+        windows += len(seq) - k + 1
+        c, n, _ = oracle_lib.count_sparse(np.frombuffer(seq, np.uint8), k, canonical=canonical)
         rows.append((c, n))
     here = os.path.dirname(os.path.abspath(__file__))
-    extra = ["--single-device"] if nproc > 1 else []
-    r = _torchrun([os.path.join(here, "sparse_matrix_probe.py"), str(tmp_path), "21", backend] + extra + files,
+    extra = (["--single-device"] if nproc > 1 else []) + ([] if canonical else ["--forward"])
+    extra += ["--wire", wire, "--windows", str(windows)]
+    r = _torchrun([os.path.join(here, "sparse_matrix_probe.py"), str(tmp_path), str(k), backend] + extra + files,
                   nproc=nproc, timeout=300)
     assert r.returncode == 0, _failure(r)
     cols = np.load(tmp_path / "columns.npy")
     vals = np.load(tmp_path / "values.npy")
     want_cols = np.unique(np.concatenate([c for c, _ in rows]))
     assert np.array_equal(cols, want_cols)
-    want = np.zeros((3, want_cols.size), np.int64)
+    want = np.zeros((G, want_cols.size), np.int64)
     for g, (c, n) in enumerate(rows):
         want[g, np.searchsorted(want_cols, c)] = n
     assert np.array_equal(vals, want) and vals.max() >= 2
+    checks = [json.load(open(tmp_path / f"check_{q}.json")) for q in range(nproc)]
+    assert all(c["ok"] for c in checks), checks
+    assert all(c["index_dtype"] == "torch.int32" for c in checks), checks
+    if nproc > 1:
+        ex = [c["exchange"] for c in checks]
+        assert len({e["wire"] for e in ex}) == 1, ex
+        assert ex[0]["wire"] == ("raw" if wire == "raw" or (wire == "auto" and k == 32) else "compact"), ex
+        assert sum(e["sent_bytes"] for e in ex) == sum(e["received_bytes"] for e in ex), ex
+        if ex[0]["wire"] == "compact" and k == 21:
+            assert sum(e["sent_bytes"] for e in ex) * 4 < sum(e["raw_sent_bytes"] for e in ex), ex
+    if k == 32 and not canonical:
+        assert want_cols[-1] == np.uint64(2**64 - 1)
 
 
 def test_sparse_skewed_bucket_fallback_grouped(ctx, oracle_lib, monkeypatch):
@@ -1435,14 +1493,144 @@ def test_sparse_matrix_two_config5_genomes(tmp_path, ctx, dev, oracle_lib):
     assert m.on_device and m.G == 2 and m.lo_code == 0 and m.hi_code == 1 << 42
     cols = m.columns
     assert bool(torch.all(cols[1:] > cols[:-1]).item())
-    used = torch.zeros(cols.numel(), dtype=torch.int32, device=cols.device)
-    used[m.indices] = 1
-    assert bool(torch.all(used == 1).item())
+    assert m.indices.dtype == torch.int32   # u32 indices (fewer than 2^32 - 1 entries)
+    assert m.all_columns_used()
     for g, seq in enumerate(seqs):
         wc, wn, _ = oracle_lib.count_sparse(seq, 21, canonical=True)
         a, b = int(m.indptr[g]), int(m.indptr[g + 1])
         assert b - a == wc.size
-        got_c = cols[m.indices[a:b]].cpu().numpy().view(np.uint64)
+        got_c = cols[m.column_indices(a, b)].cpu().numpy().view(np.uint64)
         assert np.array_equal(got_c, wc)
         assert np.array_equal(m.values[a:b].cpu().numpy().view(np.uint32), wn)
         del wc, wn
+
+
+# ---------------------------------------------------------------- the config-5 exchange wire (kmh_wire.hip)
+def _wire_encode_np(codes, counts):
+    """Restatement of the compact wire format of one slice (include/kmerhip.h, kmh_wire.hip header):
+    per 1024 entries a 2192-byte record [u64 first code][u32 first escape][u32 escapes][u16 gaps,
+    0xFFFF = escaped][128-byte bitmap of counts != 1], then the slice's 16-byte escapes, in the
+    encoder's order (thread t = entry i % 256 in thread order, its entries i = j * 256 + t in j order,
+    the gap escape before the count escape)."""
+    n = codes.size
+    recs, escs = [], []
+    for c0 in range(0, n, 1024):
+        c = codes[c0:c0 + 1024].astype(np.uint64)
+        m = counts[c0:c0 + 1024].astype(np.uint32)
+        gap = np.zeros(1024, np.uint64)
+        gap[1:c.size] = c[1:] - c[:-1]
+        ge = gap >= 0xFFFF
+        cn = np.ones(1024, np.uint32)
+        cn[:c.size] = m
+        ce = cn != 1
+        e0 = len(escs)
+        for t in range(256):
+            for j in range(4):
+                i = j * 256 + t
+                if ge[i]:
+                    escs.append(np.array([i, 0, int(gap[i]) & 0xFFFFFFFF, int(gap[i]) >> 32], np.uint32))
+                if ce[i]:
+                    escs.append(np.array([i | (1 << 16), 0, int(cn[i]), 0], np.uint32))
+        g16 = np.where(ge, 0xFFFF, gap & np.uint64(0xFFFF)).astype(np.uint16)
+        rec = (np.array([c[0]], np.uint64).tobytes() + np.array([e0, len(escs) - e0], np.uint32).tobytes()
+               + g16.tobytes() + np.packbits(ce, bitorder="little").tobytes())
+        recs.append(rec)
+    return b"".join(recs) + b"".join(e.tobytes() for e in escs)
+
+
+def _wire_round_trip(ctx, dev, codes, counts, cuts):
+    """Slices of (codes, counts) between consecutive cuts: sized, packed, unpacked in reverse slice
+    order into a fresh buffer; returns (packed bytes, unpacked codes, unpacked counts, slice bytes)."""
+    d_c = torch.from_numpy(codes.view(np.int64).copy()).to(dev)
+    d_n = torch.from_numpy(counts.view(np.int32).copy()).to(dev)
+    st = np.array(cuts[:-1], np.uint64)
+    sn = np.diff(np.array(cuts, np.uint64))
+    s = torch.cuda.current_stream().cuda_stream
+    sb = ctx.wire_size_dev(d_c.data_ptr(), d_n.data_ptr(), st, sn, s)
+    tot = int(sb.sum())
+    out = torch.full((max(tot, 16),), 0xA5, dtype=torch.uint8, device=dev)
+    ctx.wire_encode_dev(d_c.data_ptr(), d_n.data_ptr(), st, sn, out.data_ptr(), tot, s)
+    packed = out[:tot].cpu().numpy().tobytes()
+    # decode the slices in reverse order from a buffer that holds them reversed
+    boff = np.concatenate([[0], np.cumsum(sb)]).astype(np.int64)
+    rev = b"".join(packed[boff[i]:boff[i + 1]] for i in reversed(range(sn.size)))
+    d_in = torch.from_numpy(np.frombuffer(rev, np.uint8).copy()).to(dev) if rev else torch.zeros(16, dtype=torch.uint8,
+                                                                                                  device=dev)
+    rc = torch.full((max(codes.size, 1),), -1, dtype=torch.int64, device=dev)
+    rn = torch.full((max(codes.size, 1),), -1, dtype=torch.int32, device=dev)
+    ctx.wire_decode_dev(d_in.data_ptr(), len(rev), sn[::-1].copy(), sb[::-1].copy(), st[::-1].copy(), rc.data_ptr(),
+                        rn.data_ptr(), s)
+    torch.cuda.synchronize()
+    return (packed, rc[:codes.size].cpu().numpy().view(np.uint64), rn[:codes.size].cpu().numpy().view(np.uint32), sb)
+
+
+@pytest.mark.parametrize("case", ["k21_ragged", "repeats", "k32_wide", "tiny"])
+def test_wire_round_trip_small(ctx, dev, oracle_lib, case):
+    """The compact wire on small slices: the packed bytes equal the numpy
+    restatement of the format byte for byte, and decoding (slices in another order, other
+    destinations) gives the exact codes and counts back.  Cases: k = 21 canonical rows of ragged
+    genomes; a repeat-rich genome with poly-A (counts up to ~10^5, every count escaped); k = 32
+    forward codes (gaps of ~2^40: every gap escaped) with a poly-T run (code 2^64 - 1); slices of
+    0, 1, 1023, 1024 and 1025 entries."""
+    rng = np.random.default_rng({"k21_ragged": 1, "repeats": 2, "k32_wide": 3, "tiny": 4}[case])
+    if case == "k21_ragged":
+        seq, k, canon = _ragged_genomes(rng, [300_000])[0], 21, True
+    elif case == "repeats":
+        unit = osynth.synth_bases(3000, osynth.genome_seed(5))
+        seq, k, canon = np.concatenate([np.tile(unit, 30), np.full(100_000, ord("A"), np.uint8)]), 21, True
+    elif case == "k32_wide":
+        seq = np.concatenate([osynth.synth_bases(200_000, osynth.genome_seed(6)), np.full(500, ord("T"), np.uint8)])
+        k, canon = 32, False
+    else:
+        seq, k, canon = osynth.synth_bases(3_300, osynth.genome_seed(7)), 21, True
+    codes, counts, _ = oracle_lib.count_sparse(seq, k, canonical=canon)
+    n = codes.size
+    cuts = sorted({0, n, n // 3, n // 3, 2 * n // 3 + 5 if 2 * n // 3 + 5 < n else n})
+    if case == "tiny":
+        cuts = [0, 0, 1, 1024, 2048, 3072, 3073, n]
+    packed, rc, rn, sb = _wire_round_trip(ctx, dev, codes, counts, cuts)
+    want = b"".join(_wire_encode_np(codes[a:b], counts[a:b]) for a, b in zip(cuts[:-1], cuts[1:]))
+    assert packed == want
+    assert np.array_equal(rc, codes) and np.array_equal(rn, counts)
+    if case == "k32_wide":
+        assert codes[-1] == np.uint64(2**64 - 1) and sb.sum() > 12 * n   # every gap escaped: raw is smaller
+    if case == "k21_ragged":
+        assert sb.sum() < 3 * n
+
+
+def test_wire_round_trip_config5_genome(ctx, dev, oracle_lib):
+    """The compact wire on a full config-5 genome's sorted row (250 Mbp synthetic genome 0, k = 21
+    canonical, ~2.5e8 entries from kmh_count_sparse_sorted_dev) cut into the 8 slices an N = 8 run
+    sends: exact round trip against the uncompressed row, and the packed size (the VERDICT r05
+    target: ~2-2.5 B per entry against 12)."""
+    seq = oracle_lib.synth(250_000_000, osynth.genome_seed(0))
+    buf, offs = _layout([seq])
+    d_seq = torch.from_numpy(buf).to(dev)
+    cap = int(_native.sparse_out_offsets(offs, 21)[-1])
+    d_c = torch.empty(cap, dtype=torch.int64, device=dev)
+    d_n = torch.empty(cap, dtype=torch.int32, device=dev)
+    nr = torch.empty(1, dtype=torch.int64, device=dev)
+    nd = torch.empty(1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.count_sparse_sorted_dev(d_seq.data_ptr(), offs, 21, 1, d_c.data_ptr(), d_n.data_ptr(), nr.data_ptr(),
+                                nd.data_ptr(), s)
+    n = int(nr.item())
+    del d_seq
+    roff = np.array([0, n], np.uint64)
+    hist = kmatrix._row_histogram(d_c, roff, 21).cpu().numpy()
+    assert int(hist.sum()) == n
+    bounds = kmatrix._splitters_from_hist(hist, 21, 8)
+    send_len, starts = kmatrix.shard_plan(d_c, roff, bounds, 0)
+    assert int(send_len.sum()) == n and np.all(send_len > n // 10)
+    st, sn = starts[0].astype(np.uint64), send_len[0].astype(np.uint64)
+    sb = ctx.wire_size_dev(d_c.data_ptr(), d_n.data_ptr(), st, sn, s)
+    tot = int(sb.sum())
+    out = torch.empty(tot, dtype=torch.uint8, device=dev)
+    ctx.wire_encode_dev(d_c.data_ptr(), d_n.data_ptr(), st, sn, out.data_ptr(), tot, s)
+    rc = torch.empty(n, dtype=torch.int64, device=dev)
+    rn = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.wire_decode_dev(out.data_ptr(), tot, sn, sb, st, rc.data_ptr(), rn.data_ptr(), s)
+    assert torch.equal(rc, d_c[:n]) and torch.equal(rn, d_n[:n])
+    per = tot / n
+    print(f"config-5 genome 0: {n} entries, {tot} bytes packed = {per:.3f} B per entry")
+    assert per < 2.6, per
