@@ -85,6 +85,9 @@ def parse():
                         "device copies of the slot; no xGMI); sparse = config 5's matrix (--genomes per "
                         "rank, the other ranks' slices of its code range really counted and packed, "
                         "unpacked and unioned at R = N x genomes rows): a projection, labelled as such")
+    p.add_argument("--matrix-wire", choices=["auto", "compact", "raw"], default="auto",
+                   help="config-5 matrix at N > 1: the all-to-all's wire (auto = compact gaps unless raw u64 + "
+                        "u32 is smaller, e.g. small genomes or k = 32; kmerml.kmers.matrix.shard_from_rows)")
     p.add_argument("--config5-genomes-per-rank", type=int, default=16,
                    help="the config-5 object of the dense line: genomes per rank (config 5: 128 / 8 = 16)")
     p.add_argument("--config5-genome-len", type=int, default=250_000_000,
@@ -658,7 +661,7 @@ def main():
         sa = argparse.Namespace(k=21, genomes=a.config5_genomes_per_rank * world, genome_len=a.config5_genome_len,
                                 steps=3, warmup=1, cpu_sample=0, forward=False, backend=a.backend,
                                 pmc_summary=a.pmc_summary, cpu=None, no_matrix=a.no_matrix,
-                                single_device=a.single_device)
+                                single_device=a.single_device, matrix_wire=a.matrix_wire)
         c5_multi = run_sparse(sa, world, rank, dev, dev_index, emit=False)
 
     if rank == 0:
@@ -1024,7 +1027,7 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
         ph["fallback_passes"] = st1["fallback_passes"] - st0["fallback_passes"]
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        m = kmatrix.shard_from_rows(codes, counts, roff, G, k, timings=sph)
+        m = kmatrix.shard_from_rows(codes, counts, roff, G, k, timings=sph, wire=getattr(a, "matrix_wire", "auto"))
         del codes, counts
         torch.cuda.synchronize()
         if world > 1:
@@ -1190,9 +1193,8 @@ def run_sparse_sim(a, dev, dev_index):
             phs.append(ph)
         if i < a.steps:
             del m
-    ok = m.all_columns_used()
+    ok = m.all_columns_used() and m.columns_ascending()
     cols = m.columns
-    ok = ok and (bool(torch.all(cols[1:] > cols[:-1]).item()) if cols.numel() > 1 else True)
     # every entry of range 0 of all N x 16 genomes arrived: the rows' cuts of range 0 summed
     want_entries = int(hist.cpu().numpy()[:bounds[1] >> max(2 * k - 16, 0)].sum())
     ok = ok and total == want_entries

@@ -233,13 +233,14 @@ int kmh_rows_cuts_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint64_t* row
                       int nb, uint64_t* d_cuts, void* stream);
 /* Compact wire format of S row slices for the all-to-all: slice i = entries [slice_start[i],
  * slice_start[i] + slice_n[i]) of d_codes / d_counts (device; host slice arrays), codes ascending
- * within a slice.  Per 1024 entries one 2192-byte record (the first code, u16 gaps, a bit per count
- * that is not 1) and, per slice, 16-byte escapes for gaps >= 65535 and counts != 1: exact for any
- * codes and counts, ~2.2 bytes per entry for config 5's rows against 12 raw.  kmh_wire_size_dev
+ * within a slice.  Per 1024 entries one 2320-byte record (the first code, the low 16 bits of every
+ * gap, a bit per gap with higher bits and per count that is not 1) and, per slice, the escape words
+ * (u32, in entry order: gap >> 16, then the count) at positions implied by the bits: exact for any
+ * codes and counts, ~2.4 bytes per entry for config 5's rows against 12 raw.  kmh_wire_size_dev
  * writes every slice's byte size to slice_bytes (host; synchronises the stream); kmh_wire_encode_dev
  * writes the slices back to back to d_out (out_bytes >= the sum), reusing the sizing of a
  * kmh_wire_size_dev call with the same arguments just before it (the data must not change in
- * between).  KMH_ERR_UNSUPPORTED past 2^24 slices, 2^32 chunks or 2^32 escapes in one slice. */
+ * between).  KMH_ERR_UNSUPPORTED past 2^24 slices, 2^32 chunks or 2^32 escape words in one slice. */
 int kmh_wire_size_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* slice_start,
                       const uint64_t* slice_n, int S, uint64_t* slice_bytes, void* stream);
 int kmh_wire_encode_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* slice_start,
@@ -247,8 +248,8 @@ int kmh_wire_encode_dev(kmh_ctx* ctx, const uint64_t* d_codes, const uint32_t* d
 /* Decode S slices back to back in d_in (slice i: slice_n[i] entries in slice_bytes[i] bytes, as the
  * sender's kmh_wire_size_dev reported; host arrays) into d_codes / d_counts at entry slice_dst[i]
  * (the caller's output must hold them).  A slice whose bytes do not match its entries is
- * KMH_ERR_INVALID; escape fields are clamped to their slice, so damaged bytes cannot move a read or
- * write outside it. */
+ * KMH_ERR_INVALID; escape positions are clamped to their chunk and slice, so damaged bytes cannot
+ * move a read or write outside it. */
 int kmh_wire_decode_dev(kmh_ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t* slice_n,
                         const uint64_t* slice_bytes, const uint64_t* slice_dst, int S, uint64_t* d_codes,
                         uint32_t* d_counts, void* stream);

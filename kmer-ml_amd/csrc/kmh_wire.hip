@@ -6,21 +6,26 @@
 // the range bounds (k_rows_cuts), which also give the global code histogram that places the bounds.
 //
 // The compact wire.  A sorted row slice is mostly small gaps between codes
-// (k = 21 canonical, 250 Mbp genomes: ~1.8e4 codes on average, ~15 bits) and counts of 1, so it
-// travels as chunk records of 1024 entries:
+// (k = 21 canonical, 250 Mbp genomes: ~9e3 codes in the dense low end of the canonical code space,
+// more towards its top) and counts of 1, so it travels as chunk records of 1024 entries:
 //
-//   [u64 anchor = the chunk's first code][u32 first escape of the chunk, slice-relative][u32 escapes]
-//   [u16 gap x 1024: code - previous code (0 for the first entry, and past the slice's end);
-//    0xFFFF = the gap is in an escape]
-//   [128 bytes: bit i set = entry i's count is not 1 (the count is in an escape)]
+//   [u64 anchor = the chunk's first code][u32 first escape word of the chunk, slice-relative]
+//   [u32 escape words of the chunk | wide << 31]
+//   [u16 x 1024: the low 16 bits of each gap, code - previous code (0 for the first entry, and past
+//    the slice's end)]
+//   [u64 x 16: bit i set = entry i's gap has high bits (gap >> 16 != 0)]
+//   [u64 x 16: bit i set = entry i's count is not 1]
 //
-// (2192 bytes, 2.14 B per entry) followed, per slice, by its escape table: 16-byte entries
-// {u32 entry index in the chunk | kind << 16, u32 0, u64 value}, kind 0 = the full gap, kind 1 = the
-// count.  Exact for any codes and counts (k = 32 codes use all 64 bits; the sums wrap like the codes).
-// A slice is sized first (k_wire_count: escapes per chunk, a scan, the slice's bytes), then packed
-// (k_wire_pack), and the receiver rebuilds codes and counts with one u64 scan per chunk
-// (k_wire_unpack) straight into its shard's row layout.  Every kernel is one streaming pass: the
-// reads and writes are the algorithmic bytes (12 B per entry raw, ~2.2 B packed).
+// (2320 bytes, 2.27 B per entry), and after a slice's records its escape words (u32), in entry
+// order: for an entry with high bits, gap >> 16 in one word (two, low word first, in a "wide" chunk,
+// one with a gap of 2^48 or more: k >= 25 codes), then for a count that is not 1, the count.  The
+// position of an entry's words is the prefix sum of the words of the entries before it, so the
+// flags carry no index: an escape costs 4 bytes (8 in a wide chunk).  Exact for any codes and
+// counts (k = 32 codes use all 64 bits; the sums wrap like the codes).  A slice is sized first
+// (k_wire_count: words per chunk, a scan, the slice's bytes), then packed (k_wire_pack), and the
+// receiver rebuilds codes and counts with two scans per chunk (escape positions, then codes;
+// k_wire_unpack) straight into its shard's row layout.  Every kernel is one streaming pass: the
+// reads and writes are the algorithmic bytes (12 B per entry raw, ~2.4 B packed for config 5).
 #include <algorithm>
 #include <vector>
 
@@ -33,10 +38,10 @@ constexpr int kWThreads = 256;
 constexpr int kWPer = 4;                               // entries per thread: j * 256 + tid
 constexpr int kWChunk = kWThreads * kWPer;             // entries per chunk record
 constexpr int kWHead = 16;
-constexpr int kWBits = kWHead + 2 * kWChunk;           // offset of the count bitmap
-constexpr int kWRec = kWBits + kWChunk / 8;            // 2192 bytes
-constexpr uint64_t kWEsc = 16;                         // bytes per escape
-constexpr uint32_t kWGapEsc = 0xFFFFu;
+constexpr int kWHi = kWHead + 2 * kWChunk;             // offset of the high-bits bitmap
+constexpr int kWCnt = kWHi + kWChunk / 8;              // offset of the count bitmap
+constexpr int kWRec = kWCnt + kWChunk / 8;             // 2320 bytes
+constexpr int kWMaxWords = 3 * kWChunk;                // escape words of one chunk, at most
 static_assert(kWRec % 16 == 0, "records keep 16-byte alignment");
 
 // cuts[r * nb + b] = the first entry of row r (relative to the row) whose code is >= bounds[b].
@@ -69,13 +74,13 @@ __device__ __forceinline__ uint32_t slice_of(const uint64_t* __restrict__ cbase,
     return a;
 }
 
-// Sum over the workgroup (kWThreads); ws: kWThreads / 64 words.
-__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* ws) {
+// Sum over the workgroup (kWThreads) of a u64; ws: kWThreads / 64 words.
+__device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* ws) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     if ((threadIdx.x & 63u) == 0u) ws[threadIdx.x >> 6] = v;
     __syncthreads();
-    uint32_t t = 0u;
+    uint64_t t = 0u;
 #pragma unroll
     for (int w = 0; w < kWThreads / 64; ++w) t += ws[w];
     __syncthreads();
@@ -90,6 +95,21 @@ __device__ __forceinline__ uint64_t wave_incl_u64(uint64_t v) {
         if (lane >= d) v += t;
     }
     return v;
+}
+
+// Per-entry flags packed for one block reduction: high bits (1 << 0), a high part of 32 bits or
+// more (1 << 21), a count that is not 1 (1 << 42).
+__device__ __forceinline__ uint64_t flag_bits(uint64_t gap, uint32_t cnt, bool v) {
+    if (!v) return 0ull;
+    const uint64_t hi = gap >> 16;
+    return (hi ? 1ull : 0ull) | ((hi >> 32) ? (1ull << 21) : 0ull) | (cnt != 1u ? (1ull << 42) : 0ull);
+}
+
+// Escape words of a chunk from its summed flags.
+__device__ __forceinline__ uint32_t chunk_words(uint64_t f, bool* wide) {
+    const uint32_t nh = (uint32_t)(f & 0x1FFFFFu), nw = (uint32_t)((f >> 21) & 0x1FFFFFu), nc = (uint32_t)(f >> 42);
+    *wide = nw != 0u;
+    return nh * (nw ? 2u : 1u) + nc;
 }
 
 // A chunk's place: slice s, chunk index within it, first entry (input index), entries.
@@ -110,44 +130,61 @@ __device__ __forceinline__ Chunk chunk_at(const uint64_t* __restrict__ sstart, c
     return k;
 }
 
-// Escapes of every chunk: gaps >= 0xFFFF and counts != 1.
+// Escape words of every chunk.
 __global__ __launch_bounds__(kWThreads) void k_wire_count(const uint64_t* __restrict__ codes,
                                                           const uint32_t* __restrict__ counts,
                                                           const uint64_t* __restrict__ sstart,
                                                           const uint64_t* __restrict__ sn,
                                                           const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
                                                           uint32_t* __restrict__ esc) {
-    __shared__ uint32_t ws[kWThreads / 64];
+    __shared__ uint64_t ws[kWThreads / 64];
     const uint32_t tid = threadIdx.x;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
-        uint32_t e = 0u;
+        uint64_t f = 0ull;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
             const uint32_t i = (uint32_t)j * kWThreads + tid;
-            if (i < ch.n) {
-                const uint64_t code = codes[ch.base + i];
-                const uint64_t prev = i ? codes[ch.base + i - 1u] : code;
-                e += (code - prev >= (uint64_t)kWGapEsc) ? 1u : 0u;
-                e += counts[ch.base + i] != 1u ? 1u : 0u;
-            }
+            const bool v = i < ch.n;
+            const uint64_t code = v ? codes[ch.base + i] : 0ull;
+            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code;
+            f += flag_bits(code - prev, v ? counts[ch.base + i] : 1u, v);
         }
-        const uint32_t t = block_sum(e, ws);
+        bool wide;
+        const uint32_t t = chunk_words(block_sum64(f, ws), &wide);
         if (tid == 0) esc[c] = t;
     }
 }
 
-// Bytes of every slice: its records + its escapes (esc_off: exclusive scan of the chunks' escapes).
+// Bytes of every slice: its records + its escape words, padded to 16 bytes (esc_off: exclusive scan
+// of the chunks' words).
 __global__ __launch_bounds__(256) void k_wire_slice_bytes(const uint64_t* __restrict__ cbase,
                                                           const unsigned long long* __restrict__ esc_off, uint32_t S,
                                                           uint64_t* __restrict__ sbytes) {
     const uint32_t s = blockIdx.x * 256u + threadIdx.x;
     if (s >= S) return;
     const uint64_t c0 = cbase[s], c1 = cbase[s + 1];
-    sbytes[s] = (c1 - c0) * (uint64_t)kWRec + (uint64_t)(esc_off[c1] - esc_off[c0]) * kWEsc;
+    sbytes[s] = (c1 - c0) * (uint64_t)kWRec + ((uint64_t)(esc_off[c1] - esc_off[c0]) * 4u + 15u) / 16u * 16u;
 }
 
-// Pack every chunk: record at sboff[s] + cl * kWRec, escapes in the slice's table.
+// Workgroup exclusive scan of a u32 (kWThreads); returns the prefix, *total the sum.
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* ws, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t incl = scan64(v);
+    if (lane == 63u) ws[wave] = incl;
+    __syncthreads();
+    uint32_t pre = incl - v, tot = 0u;
+#pragma unroll
+    for (int w = 0; w < kWThreads / 64; ++w) {
+        pre += (uint32_t)w < wave ? ws[w] : 0u;
+        tot += ws[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return pre;
+}
+
+// Pack every chunk: record at sboff[s] + cl * kWRec, escape words in the slice's table.
 __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restrict__ codes,
                                                          const uint32_t* __restrict__ counts,
                                                          const uint64_t* __restrict__ sstart,
@@ -155,60 +192,69 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
                                                          const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
                                                          const unsigned long long* __restrict__ esc_off,
                                                          const uint64_t* __restrict__ sboff, uint8_t* __restrict__ out) {
+    __shared__ uint64_t ws64[kWThreads / 64];
     __shared__ uint32_t ws[kWThreads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
         const uint64_t c0 = cbase[ch.s];
         uint8_t* const rec = out + sboff[ch.s] + ch.cl * (uint64_t)kWRec;
-        uint8_t* const etab = out + sboff[ch.s] + (cbase[ch.s + 1] - c0) * (uint64_t)kWRec;
-        const unsigned long long e0 = esc_off[c] - esc_off[c0];   // the chunk's first escape in the slice
-        uint64_t code[kWPer], gap[kWPer];
-        uint32_t cnt[kWPer], ne = 0u;
+        const unsigned long long w0 = esc_off[c] - esc_off[c0];   // the chunk's first escape word in the slice
+        uint32_t* const etab = reinterpret_cast<uint32_t*>(out + sboff[ch.s] + (cbase[ch.s + 1] - c0) * (uint64_t)kWRec) + w0;
+        uint64_t gap[kWPer];
+        uint32_t cnt[kWPer];
+        uint64_t f = 0ull, first = 0ull;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
             const uint32_t i = (uint32_t)j * kWThreads + tid;
             const bool v = i < ch.n;
-            code[j] = v ? codes[ch.base + i] : 0ull;
+            const uint64_t code = v ? codes[ch.base + i] : 0ull;
+            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code;
+            if (j == 0) first = code;
+            gap[j] = code - prev;
             cnt[j] = v ? counts[ch.base + i] : 1u;
-            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code[j];
-            gap[j] = code[j] - prev;
-            ne += (gap[j] >= (uint64_t)kWGapEsc ? 1u : 0u) + (cnt[j] != 1u ? 1u : 0u);
+            f += flag_bits(gap[j], cnt[j], v);
         }
-        // this thread's first escape: exclusive scan of ne over the workgroup
-        uint32_t incl = scan64(ne);
-        if (lane == 63u) ws[wave] = incl;
-        __syncthreads();
-        uint32_t pre = incl - ne, tot = 0u;
-#pragma unroll
-        for (int w = 0; w < kWThreads / 64; ++w) {
-            pre += (uint32_t)w < wave ? ws[w] : 0u;
-            tot += ws[w];
-        }
-        __syncthreads();
+        bool wide;
+        const uint32_t words = chunk_words(block_sum64(f, ws64), &wide);
         if (tid == 0) {
-            *reinterpret_cast<uint64_t*>(rec) = code[0];
-            *reinterpret_cast<uint2*>(rec + 8) = make_uint2((uint32_t)e0, tot);
+            *reinterpret_cast<uint64_t*>(rec) = first;   // (entry 0 is thread 0's first)
+            *reinterpret_cast<uint2*>(rec + 8) = make_uint2((uint32_t)w0, words | (wide ? 0x80000000u : 0u));
         }
-        uint16_t* const g16 = reinterpret_cast<uint16_t*>(rec + kWHead);
-        uint4* const et = reinterpret_cast<uint4*>(etab) + e0 + pre;
-        uint32_t k = 0u;
+        if (c + 1u == cbase[ch.s + 1] && tid < 4u) {   // the slice's last chunk zeroes the table's padding
+            const unsigned long long sw = esc_off[c + 1u] - esc_off[c0];
+            if (tid < ((4u - (uint32_t)(sw & 3u)) & 3u)) etab[sw - w0 + tid] = 0u;
+        }
+        uint16_t* const low = reinterpret_cast<uint16_t*>(rec + kWHead);
+        uint32_t carry = 0u;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
             const uint32_t i = (uint32_t)j * kWThreads + tid;
-            const bool ge = gap[j] >= (uint64_t)kWGapEsc, ce = cnt[j] != 1u;
-            g16[i] = ge ? (uint16_t)kWGapEsc : (uint16_t)gap[j];
-            const uint64_t bits = __ballot(ce);
-            if (lane == 0u) *reinterpret_cast<uint64_t*>(rec + kWBits + ((uint32_t)j * kWThreads + wave * 64u) / 8u) = bits;
-            if (ge) et[k++] = make_uint4(i, 0u, (uint32_t)gap[j], (uint32_t)(gap[j] >> 32));
-            if (ce) et[k++] = make_uint4(i | (1u << 16), 0u, cnt[j], 0u);
+            const uint64_t hi = gap[j] >> 16;
+            const bool hf = hi != 0ull, cf = cnt[j] != 1u;
+            const uint32_t gw = hf ? (wide ? 2u : 1u) : 0u;
+            uint32_t tot;
+            const uint32_t pos = carry + block_excl(gw + (cf ? 1u : 0u), ws, &tot);
+            carry += tot;
+            low[i] = (uint16_t)gap[j];
+            const uint64_t hb = __ballot(hf), cb = __ballot(cf);
+            if (lane == 0u) {
+                const uint32_t o = ((uint32_t)j * kWThreads + wave * 64u) / 8u;
+                *reinterpret_cast<uint64_t*>(rec + kWHi + o) = hb;
+                *reinterpret_cast<uint64_t*>(rec + kWCnt + o) = cb;
+            }
+            if (hf) {
+                etab[pos] = (uint32_t)hi;
+                if (wide) etab[pos + 1u] = (uint32_t)(hi >> 32);
+            }
+            if (cf) etab[pos + gw] = cnt[j];
         }
     }
 }
 
 // Unpack every chunk of the received slices: slice s (entries sn[s]) at byte sboff[s] of `in`, its
-// entries to sdst[s] .. of the output.  Escape indices and counts are clamped to the slice's table, so
-// a damaged buffer cannot make a read or write leave the slice.
+// entries to sdst[s] .. of the output.  Escape positions are clamped to the chunk's words and those
+// to the slice's table, so a damaged buffer cannot make a read or write leave the slice.
 __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ sboff,
                                                            const uint64_t* __restrict__ sn,
@@ -217,9 +263,9 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
                                                            const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
                                                            uint64_t* __restrict__ out_codes,
                                                            uint32_t* __restrict__ out_counts) {
-    __shared__ uint64_t ogap[kWChunk];
-    __shared__ uint32_t ocnt[kWChunk];
-    __shared__ uint64_t ws[kWThreads / 64];
+    __shared__ uint32_t wbuf[kWMaxWords + 2];
+    __shared__ uint64_t ws64[kWThreads / 64];
+    __shared__ uint32_t ws[kWThreads / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const uint32_t s = slice_of(cbase, S, c);
@@ -227,46 +273,61 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
         const uint64_t rem = sn[s] - cl * kWChunk;
         const uint32_t n = (uint32_t)(rem < (uint64_t)kWChunk ? rem : (uint64_t)kWChunk);
         const uint8_t* const rec = in + sboff[s] + cl * (uint64_t)kWRec;
-        const uint4* const etab = reinterpret_cast<const uint4*>(in + sboff[s] + (cbase[s + 1] - c0) * (uint64_t)kWRec);
+        const uint32_t* const etab = reinterpret_cast<const uint32_t*>(in + sboff[s] + (cbase[s + 1] - c0) * (uint64_t)kWRec);
         const uint64_t anchor = *reinterpret_cast<const uint64_t*>(rec);
         const uint2 eh = *reinterpret_cast<const uint2*>(rec + 8);
+        const bool wide = (eh.y >> 31) != 0u;
         const uint64_t etot = sesc[s];
-        const uint64_t elo = eh.x < etot ? eh.x : etot;
-        const uint64_t en = (uint64_t)eh.y < etot - elo ? (uint64_t)eh.y : etot - elo;
-        for (uint64_t e = tid; e < en; e += kWThreads) {
-            const uint4 v = etab[elo + e];
-            const uint32_t i = v.x & (uint32_t)(kWChunk - 1);
-            if (v.x >> 16) ocnt[i] = v.z;
-            else ogap[i] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        }
+        const uint64_t wlo = eh.x < etot ? eh.x : etot;
+        uint32_t wn = eh.y & 0x7FFFFFFFu;
+        wn = (uint32_t)((uint64_t)wn < etot - wlo ? (uint64_t)wn : etot - wlo);
+        wn = wn < (uint32_t)kWMaxWords ? wn : (uint32_t)kWMaxWords;
+        for (uint32_t w = tid; w < wn; w += kWThreads) wbuf[w] = etab[wlo + w];
         __syncthreads();
-        const uint16_t* const g16 = reinterpret_cast<const uint16_t*>(rec + kWHead);
-        uint64_t carry = anchor;
+        auto word = [&](uint32_t p) { return p < wn ? wbuf[p] : 0u; };
+        const uint16_t* const low = reinterpret_cast<const uint16_t*>(rec + kWHead);
         uint64_t* const oc = out_codes + sdst[s] + cl * kWChunk;
         uint32_t* const on = out_counts + sdst[s] + cl * kWChunk;
+        uint64_t carry = anchor;
+        uint32_t wcarry = 0u;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
             const uint32_t i = (uint32_t)j * kWThreads + tid;
             const bool v = i < n;
-            const uint32_t g = v ? g16[i] : 0u;
-            const uint64_t gap = g == kWGapEsc ? ogap[i] : (uint64_t)g;
-            const uint64_t bits = *reinterpret_cast<const uint64_t*>(rec + kWBits + ((uint32_t)j * kWThreads + wave * 64u) / 8u);
-            const uint32_t cnt = (bits >> lane) & 1u ? ocnt[i] : 1u;
-            const uint64_t incl = wave_incl_u64(v ? gap : 0ull);
-            if (lane == 63u) ws[wave] = incl;
+            const uint32_t o = ((uint32_t)j * kWThreads + wave * 64u) / 8u;
+            const bool hf = v && ((*reinterpret_cast<const uint64_t*>(rec + kWHi + o) >> lane) & 1ull);
+            const bool cf = v && ((*reinterpret_cast<const uint64_t*>(rec + kWCnt + o) >> lane) & 1ull);
+            const uint32_t gw = hf ? (wide ? 2u : 1u) : 0u, nw = gw + (cf ? 1u : 0u);
+            // both scans at once: escape words (u32) and, once the words are read, gaps (u64)
+            const uint32_t wincl = scan64(nw);
+            if (lane == 63u) ws[wave] = wincl;
+            __syncthreads();
+            uint32_t pos = wcarry + wincl - nw, wtot = 0u;
+#pragma unroll
+            for (int w = 0; w < kWThreads / 64; ++w) {
+                pos += (uint32_t)w < wave ? ws[w] : 0u;
+                wtot += ws[w];
+            }
+            wcarry += wtot;
+            uint64_t hi = 0ull;
+            if (hf) hi = (uint64_t)word(pos) | (wide ? (uint64_t)word(pos + 1u) << 32 : 0ull);
+            const uint32_t cnt = cf ? word(pos + gw) : 1u;
+            const uint64_t gap = v ? ((uint64_t)low[i] | (hi << 16)) : 0ull;
+            const uint64_t incl = wave_incl_u64(gap);
+            if (lane == 63u) ws64[wave] = incl;
             __syncthreads();
             uint64_t pre = 0ull, tot = 0ull;
 #pragma unroll
             for (int w = 0; w < kWThreads / 64; ++w) {
-                pre += (uint32_t)w < wave ? ws[w] : 0ull;
-                tot += ws[w];
+                pre += (uint32_t)w < wave ? ws64[w] : 0ull;
+                tot += ws64[w];
             }
-            __syncthreads();
             if (v) {
                 oc[i] = carry + pre + incl;
                 on[i] = cnt;
             }
             carry += tot;
+            __syncthreads();   // ws / ws64 reused by the next round; wbuf by the next chunk
         }
     }
 }
@@ -382,8 +443,8 @@ int wire_size(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const
     if (rc) return rc;
     for (int i = 0; i < S; ++i) {
         const uint64_t nch = cbase[i + 1] - cbase[i];
-        if ((sb[i] - nch * kWRec) / kWEsc >= 0xFFFFFFFFull)
-            return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: 2^32 or more escapes in one slice");
+        if ((sb[i] - nch * kWRec) / 4u >= 0xFFFFFFFFull)
+            return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: 2^32 or more escape words in one slice");
         slice_bytes[i] = sb[i];
     }
     return KMH_OK;
@@ -434,13 +495,13 @@ int wire_decode(Ctx* ctx, const uint8_t* d_in, uint64_t in_bytes, const uint64_t
     cb[0] = 0;
     for (int i = 0; i < S; ++i) {
         const uint64_t nch = (sn[i] + kWChunk - 1) / kWChunk;
-        if (sn[i] >= (1ull << 40) || sbytes[i] < nch * kWRec || (sbytes[i] - nch * kWRec) % kWEsc)
+        if (sn[i] >= (1ull << 40) || sbytes[i] < nch * kWRec || (sbytes[i] - nch * kWRec) % 16u)
             return fail(ctx, KMH_ERR_INVALID, "wire: slice bytes do not match its entries");
         sboff[i] = off;
         off += sbytes[i];
         hsn[i] = sn[i];
         cb[i + 1] = cb[i] + nch;
-        sesc[i] = (sbytes[i] - nch * kWRec) / kWEsc;
+        sesc[i] = (sbytes[i] - nch * kWRec) / 4u;   // escape words (with the padding)
         hdst[i] = sdst[i];
     }
     if (off > in_bytes) return fail(ctx, KMH_ERR_INVALID, "wire: input shorter than its slices");

@@ -497,6 +497,17 @@ class ShardedSparseMatrix:
                 return ix.to(torch.int64) & 0xFFFFFFFF
         return ix
 
+    def columns_ascending(self):
+        """True iff the columns strictly ascend as unsigned 64-bit codes (on the device the int64
+        storage is compared with its sign bit flipped: k = 32 codes use all 64 bits)."""
+        if not self.on_device:
+            return bool(np.all(self.columns[1:] > self.columns[:-1]))
+        import torch
+        if self.columns.numel() < 2:
+            return True
+        c = self.columns ^ torch.iinfo(torch.int64).min
+        return bool(torch.all(c[1:] > c[:-1]).item())
+
     def all_columns_used(self, chunk=1 << 28):
         """True iff every column holds at least one entry (the union has no stray column); chunked
         so that widening u32 indices never needs more than `chunk` int64 entries."""
@@ -943,8 +954,7 @@ def shard_check(m, windows_total, group=None):
 
     cols = m.columns
     dev = cols.device
-    ok = bool(torch.all(cols[1:] > cols[:-1]).item()) if cols.numel() > 1 else True
-    ok = ok and m.all_columns_used()
+    ok = m.columns_ascending() and m.all_columns_used()
     vsum = int((m.values.to(torch.int64) & 0xFFFFFFFF).sum().item()) if m.nnz else 0
     # (k = 32 codes use all 64 bits: as int64 they would not order; compare the unsigned values)
     first = int(cols[0].item()) & 0xFFFFFFFFFFFFFFFF if cols.numel() else None
