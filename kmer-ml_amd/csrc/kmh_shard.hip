@@ -39,6 +39,10 @@ constexpr int kShMaxRows = 4096;    // organisms of one shard (LDS piece table)
 constexpr int kShRoffCache = 1024;  // row offsets kept in LDS
 constexpr int kShTarget = 3072;     // entries per unit (units of one coarse cell share its entries)
 constexpr int kShCoarseBits = 16;   // coarse cells: at most 2^16
+constexpr int kShSlotRows = 256;    // up to this many rows, an entry's row comes from the 64-entry slot
+                                    // table (a u8 row per slot, then a few steps over row starts); beyond,
+                                    // by binary search (R = 128, config 5's shard at N = 8: 3 vs 7 LDS
+                                    // round trips per entry)
 
 // First entry of row[a, b) that is >= c (row ascending).
 __device__ __forceinline__ uint32_t lower_in(const uint64_t* __restrict__ row, uint32_t a, uint32_t b, uint64_t c) {
@@ -102,8 +106,10 @@ __global__ __launch_bounds__(256) void k_shard_units(const uint32_t* __restrict_
     }
 }
 
-// st[r * (U + 1) + u] = the first entry of row r whose code is >= unit u's first code, found
-// inside the unit's coarse cell; st[.. U] = the row's length.  One thread per (u, r).
+// st[u * R + r] = the first entry of row r whose code is >= unit u's first code, found inside the
+// unit's coarse cell; st[U * R + r] = the row's length.  Unit-major, so that a union workgroup reads
+// one unit's R row starts as one contiguous run (row-major, each unit read R cache lines: at R = 128
+// rows that was most of the union's memory traffic).  One thread per (u, r), r fastest.
 __global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restrict__ codes,
                                                        const uint64_t* __restrict__ roff, int R,
                                                        const uint32_t* __restrict__ cs, uint32_t Q,
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restric
                                                        uint32_t* __restrict__ st) {
     const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (x >= (uint64_t)(U + 1u) * (uint64_t)R) return;
-    const uint32_t r = (uint32_t)(x / (U + 1u)), u = (uint32_t)(x % (U + 1u));
+    const uint32_t u = (uint32_t)(x / (uint64_t)R), r = (uint32_t)(x % (uint64_t)R);
     const uint64_t a = roff[r];
     if (u == U) {
         st[x] = (uint32_t)(roff[r + 1] - a);
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     auto pa_of = [&](int k) { return ptab + (uint32_t)k * (2u * (uint32_t)R + 1u) + (uint32_t)R + 1u; };
     __shared__ uint32_t ws[kShThreads / 64];
     __shared__ uint32_t flag;
-    // up to 64 rows: the row holding gathered entry 64 m of piece table k (rtab[k][m])
+    // up to kShSlotRows rows: the row holding gathered entry 64 m of piece table k (rtab[k][m])
     __shared__ uint8_t rtab[2][kShCap / 64];
     constexpr int PER = kShCap / kShThreads;   // entries per thread
     constexpr int BPT = kShBins / kShThreads;  // bins per thread
@@ -195,12 +201,12 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     // (made visible by the first barriers)
     auto row_base = [&](int r) { return r < kShRoffCache ? sroff[r] : roff[r]; };
 
-    // the rows of PER gathered entries at once (table k): up to 64 rows, the row of the entry's
+    // the rows of PER gathered entries at once (table k): up to kShSlotRows rows, the row of the entry's
     // 64-entry slot (rtab, written by build) and then over the row starts up to the entry (a
-    // 64-entry window crosses about T / R / 64 of them; counting all R row starts per entry cost
-    // 2 (R - 1) VALU operations); beyond 64 rows by binary search
+    // 64-entry window crosses about 64 R / T of them; counting all R row starts per entry cost
+    // 2 (R - 1) VALU operations); beyond kShSlotRows rows by binary search
     auto rows_of = [&](const uint32_t* pfx, const uint8_t* rt, const uint32_t (&iv)[PER], int (&rv)[PER]) {
-        if (R <= 64) {   // (uniform)
+        if (R <= kShSlotRows) {   // (uniform)
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 int r = rt[iv[u] >> 6];
@@ -225,9 +231,9 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     uint32_t sta = 0u, stb = 0u;
     auto issue_st = [&](uint32_t u) {
         if (pipe_st && tid < R) {
-            const uint64_t o = (uint64_t)tid * (S + 1u) + u;
+            const uint64_t o = (uint64_t)u * (uint64_t)R + tid;
             sta = st[o];
-            stb = st[o + 1];
+            stb = st[o + (uint64_t)R];
         }
     };
     // the pieces of unit u into table k (block scan: every thread calls it); returns the entries
@@ -245,9 +251,9 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         } else {
             for (int r = r0; r < r1; ++r) {
-                const uint64_t o = (uint64_t)r * (S + 1u) + u;
+                const uint64_t o = (uint64_t)u * (uint64_t)R + r;
                 pa[r] = st[o];
-                mine += st[o + 1] - st[o];
+                mine += st[o + (uint64_t)R] - st[o];
             }
         }
         uint32_t T;
@@ -256,13 +262,13 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             if (tid < R) pfx[tid] = pre;
         } else {
             for (int r = r0; r < r1; ++r) {
-                const uint64_t o = (uint64_t)r * (S + 1u) + u;
+                const uint64_t o = (uint64_t)u * (uint64_t)R + r;
                 pfx[r] = pre;
-                pre += st[o + 1] - st[o];
+                pre += st[o + (uint64_t)R] - st[o];
             }
         }
         if (tid == 0) pfx[R] = T;
-        if (R <= 64 && tid < R && mine) {   // (one row per thread) the 64-entry slots starting in this row
+        if (R <= kShSlotRows && tid < R && mine) {   // (one row per thread) the 64-entry slots starting in this row
             // (a unit over kShCap entries is not gathered: its slots past the table are skipped)
             for (uint32_t m = (pre + 63u) >> 6; (m << 6) < pre + mine && m < (uint32_t)(kShCap / 64); ++m)
                 rtab[k][m] = (uint8_t)tid;
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         return T;
     };
     // the codes of a unit of T (1 .. kShCap) entries, table k (visible), all loads in flight;
-    // WRITE with up to 64 rows: the entries' rows packed a byte each into rk, for the index stores
+    // WRITE with up to kShSlotRows rows: the entries' rows packed a byte each into rk, for the index stores
     auto gather = [&](uint32_t T, int k, uint64_t (&cv)[PER], uint32_t (&rk)[2]) {
         const uint32_t* const pfx = pfx_of(k);
         const uint32_t* const pa = pa_of(k);
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             iv[u] = i < T ? i : T - 1u;
         }
         rows_of(pfx, rtab[k], iv, rv);
-        if (WRITE && R <= 64) {
+        if (WRITE && R <= kShSlotRows) {
             rk[0] = (uint32_t)rv[0] | (uint32_t)rv[1] << 8 | (uint32_t)rv[2] << 16 | (uint32_t)rv[3] << 24;
             rk[1] = (uint32_t)rv[4] | (uint32_t)rv[5] << 8 | (uint32_t)rv[6] << 16 | (uint32_t)rv[7] << 24;
         }
@@ -508,7 +514,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 }
                 __syncthreads();
                 int rv[PER];
-                if (R <= 64) {   // (uniform) the rows found by the gather
+                if (R <= kShSlotRows) {   // (uniform) the rows found by the gather
 #pragma unroll
                     for (int u = 0; u < PER; ++u) rv[u] = (int)((rk[u >> 2] >> (8 * (u & 3))) & 0xFFu);
                 } else {
@@ -625,7 +631,7 @@ __global__ __launch_bounds__(256) void k_shard_big_sizes(const uint32_t* __restr
     if (j >= nbig) return;
     const uint32_t s = bigs[j];
     uint32_t t = 0u;
-    for (int r = 0; r < R; ++r) t += st[(uint64_t)r * (S + 1u) + s + 1u] - st[(uint64_t)r * (S + 1u) + s];
+    for (int r = 0; r < R; ++r) t += st[(uint64_t)(s + 1u) * R + r] - st[(uint64_t)s * R + r];
     sizes[j] = t;
 }
 
@@ -641,7 +647,7 @@ __global__ __launch_bounds__(256) void k_shard_big_gather(const uint64_t* __rest
     const uint32_t j = blockIdx.x, s = bigs[j];
     unsigned long long o = goff[j];
     for (int r = 0; r < R; ++r) {
-        const uint32_t a = st[(uint64_t)r * (S + 1u) + s], b = st[(uint64_t)r * (S + 1u) + s + 1u];
+        const uint32_t a = st[(uint64_t)s * R + r], b = st[(uint64_t)(s + 1u) * R + r];
         for (uint32_t i = a + threadIdx.x; i < b; i += 256u) {
             const unsigned long long t = o + (i - a);
             gcode[t] = codes[roff[r] + i];

@@ -130,6 +130,26 @@ __device__ __forceinline__ Chunk chunk_at(const uint64_t* __restrict__ sstart, c
     return k;
 }
 
+// A thread's 4 consecutive entries i = 4 tid + j of a chunk: codes, gaps (code - previous code; 0 for
+// the chunk's first entry and past its end) and counts (1 past the end).
+__device__ __forceinline__ void load4(const uint64_t* __restrict__ codes, const uint32_t* __restrict__ counts,
+                                      const Chunk& ch, uint32_t tid, uint64_t (&code)[kWPer], uint64_t (&gap)[kWPer],
+                                      uint32_t (&cnt)[kWPer]) {
+    const uint32_t i0 = kWPer * tid;
+#pragma unroll
+    for (int j = 0; j < kWPer; ++j) {
+        const bool v = i0 + j < ch.n;
+        code[j] = v ? codes[ch.base + i0 + j] : 0ull;
+        cnt[j] = v ? counts[ch.base + i0 + j] : 1u;
+    }
+    const uint64_t p0 = (i0 && i0 < ch.n) ? codes[ch.base + i0 - 1u] : code[0];
+#pragma unroll
+    for (int j = 0; j < kWPer; ++j) {
+        const bool v = i0 + j < ch.n;
+        gap[j] = v ? code[j] - (j ? code[j - 1] : p0) : 0ull;
+    }
+}
+
 // Escape words of every chunk.
 __global__ __launch_bounds__(kWThreads) void k_wire_count(const uint64_t* __restrict__ codes,
                                                           const uint32_t* __restrict__ counts,
@@ -141,15 +161,12 @@ __global__ __launch_bounds__(kWThreads) void k_wire_count(const uint64_t* __rest
     const uint32_t tid = threadIdx.x;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
+        uint64_t code[kWPer], gap[kWPer];
+        uint32_t cnt[kWPer];
+        load4(codes, counts, ch, tid, code, gap, cnt);
         uint64_t f = 0ull;
 #pragma unroll
-        for (int j = 0; j < kWPer; ++j) {
-            const uint32_t i = (uint32_t)j * kWThreads + tid;
-            const bool v = i < ch.n;
-            const uint64_t code = v ? codes[ch.base + i] : 0ull;
-            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code;
-            f += flag_bits(code - prev, v ? counts[ch.base + i] : 1u, v);
-        }
+        for (int j = 0; j < kWPer; ++j) f += flag_bits(gap[j], cnt[j], kWPer * tid + j < ch.n);
         bool wide;
         const uint32_t t = chunk_words(block_sum64(f, ws), &wide);
         if (tid == 0) esc[c] = t;
@@ -184,7 +201,9 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* ws, uint32_
     return pre;
 }
 
-// Pack every chunk: record at sboff[s] + cl * kWRec, escape words in the slice's table.
+// Pack every chunk: record at sboff[s] + cl * kWRec, escape words in the slice's table.  Thread t
+// packs entries 4t .. 4t + 3: one 8-byte store of their low gap bits, a nibble of each bitmap
+// (paired into bytes with the next thread's), and their escape words from one workgroup scan.
 __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restrict__ codes,
                                                          const uint32_t* __restrict__ counts,
                                                          const uint64_t* __restrict__ sstart,
@@ -194,67 +213,63 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
                                                          const uint64_t* __restrict__ sboff, uint8_t* __restrict__ out) {
     __shared__ uint64_t ws64[kWThreads / 64];
     __shared__ uint32_t ws[kWThreads / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
         const uint64_t c0 = cbase[ch.s];
         uint8_t* const rec = out + sboff[ch.s] + ch.cl * (uint64_t)kWRec;
         const unsigned long long w0 = esc_off[c] - esc_off[c0];   // the chunk's first escape word in the slice
         uint32_t* const etab = reinterpret_cast<uint32_t*>(out + sboff[ch.s] + (cbase[ch.s + 1] - c0) * (uint64_t)kWRec) + w0;
-        uint64_t gap[kWPer];
+        uint64_t code[kWPer], gap[kWPer];
         uint32_t cnt[kWPer];
-        uint64_t f = 0ull, first = 0ull;
+        load4(codes, counts, ch, tid, code, gap, cnt);
+        uint64_t f = 0ull;
 #pragma unroll
-        for (int j = 0; j < kWPer; ++j) {
-            const uint32_t i = (uint32_t)j * kWThreads + tid;
-            const bool v = i < ch.n;
-            const uint64_t code = v ? codes[ch.base + i] : 0ull;
-            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code;
-            if (j == 0) first = code;
-            gap[j] = code - prev;
-            cnt[j] = v ? counts[ch.base + i] : 1u;
-            f += flag_bits(gap[j], cnt[j], v);
-        }
+        for (int j = 0; j < kWPer; ++j) f += flag_bits(gap[j], cnt[j], kWPer * tid + j < ch.n);
         bool wide;
         const uint32_t words = chunk_words(block_sum64(f, ws64), &wide);
+        uint32_t nh = 0u, nc = 0u, tw = 0u;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const bool hf = (gap[j] >> 16) != 0ull, cf = cnt[j] != 1u;
+            nh |= (hf ? 1u : 0u) << j;
+            nc |= (cf ? 1u : 0u) << j;
+            tw += (hf ? (wide ? 2u : 1u) : 0u) + (cf ? 1u : 0u);
+        }
+        uint32_t tot;
+        uint32_t pos = block_excl(tw, ws, &tot);
         if (tid == 0) {
-            *reinterpret_cast<uint64_t*>(rec) = first;   // (entry 0 is thread 0's first)
+            *reinterpret_cast<uint64_t*>(rec) = code[0];
             *reinterpret_cast<uint2*>(rec + 8) = make_uint2((uint32_t)w0, words | (wide ? 0x80000000u : 0u));
+        }
+        *reinterpret_cast<uint64_t*>(rec + kWHead + 8u * tid) =
+            (gap[0] & 0xFFFFull) | (gap[1] & 0xFFFFull) << 16 | (gap[2] & 0xFFFFull) << 32 | (gap[3] & 0xFFFFull) << 48;
+        const uint32_t nh1 = __shfl_down(nh, 1), nc1 = __shfl_down(nc, 1);
+        if ((tid & 1u) == 0u) {
+            rec[kWHi + tid / 2u] = (uint8_t)(nh | nh1 << 4);
+            rec[kWCnt + tid / 2u] = (uint8_t)(nc | nc1 << 4);
+        }
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint64_t hi = gap[j] >> 16;
+            if (hi) {
+                etab[pos++] = (uint32_t)hi;
+                if (wide) etab[pos++] = (uint32_t)(hi >> 32);
+            }
+            if (cnt[j] != 1u) etab[pos++] = cnt[j];
         }
         if (c + 1u == cbase[ch.s + 1] && tid < 4u) {   // the slice's last chunk zeroes the table's padding
             const unsigned long long sw = esc_off[c + 1u] - esc_off[c0];
             if (tid < ((4u - (uint32_t)(sw & 3u)) & 3u)) etab[sw - w0 + tid] = 0u;
         }
-        uint16_t* const low = reinterpret_cast<uint16_t*>(rec + kWHead);
-        uint32_t carry = 0u;
-#pragma unroll
-        for (int j = 0; j < kWPer; ++j) {
-            const uint32_t i = (uint32_t)j * kWThreads + tid;
-            const uint64_t hi = gap[j] >> 16;
-            const bool hf = hi != 0ull, cf = cnt[j] != 1u;
-            const uint32_t gw = hf ? (wide ? 2u : 1u) : 0u;
-            uint32_t tot;
-            const uint32_t pos = carry + block_excl(gw + (cf ? 1u : 0u), ws, &tot);
-            carry += tot;
-            low[i] = (uint16_t)gap[j];
-            const uint64_t hb = __ballot(hf), cb = __ballot(cf);
-            if (lane == 0u) {
-                const uint32_t o = ((uint32_t)j * kWThreads + wave * 64u) / 8u;
-                *reinterpret_cast<uint64_t*>(rec + kWHi + o) = hb;
-                *reinterpret_cast<uint64_t*>(rec + kWCnt + o) = cb;
-            }
-            if (hf) {
-                etab[pos] = (uint32_t)hi;
-                if (wide) etab[pos + 1u] = (uint32_t)(hi >> 32);
-            }
-            if (cf) etab[pos + gw] = cnt[j];
-        }
     }
 }
 
 // Unpack every chunk of the received slices: slice s (entries sn[s]) at byte sboff[s] of `in`, its
-// entries to sdst[s] .. of the output.  Escape positions are clamped to the chunk's words and those
-// to the slice's table, so a damaged buffer cannot make a read or write leave the slice.
+// entries to sdst[s] .. of the output.  Thread t rebuilds entries 4t .. 4t + 3: two workgroup scans
+// per chunk (its escape words' position, then its codes' prefix).  Escape positions are clamped to
+// the chunk's words and those to the slice's table, so a damaged buffer cannot make a read or write
+// leave the slice.
 __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __restrict__ in,
                                                            const uint64_t* __restrict__ sboff,
                                                            const uint64_t* __restrict__ sn,
@@ -263,10 +278,10 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
                                                            const uint64_t* __restrict__ cbase, uint32_t S, uint64_t NC,
                                                            uint64_t* __restrict__ out_codes,
                                                            uint32_t* __restrict__ out_counts) {
-    __shared__ uint32_t wbuf[kWMaxWords + 2];
+    __shared__ uint32_t wbuf[kWMaxWords];
     __shared__ uint64_t ws64[kWThreads / 64];
     __shared__ uint32_t ws[kWThreads / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, i0 = kWPer * tid;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const uint32_t s = slice_of(cbase, S, c);
         const uint64_t c0 = cbase[s], cl = c - c0;
@@ -276,6 +291,9 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
         const uint32_t* const etab = reinterpret_cast<const uint32_t*>(in + sboff[s] + (cbase[s + 1] - c0) * (uint64_t)kWRec);
         const uint64_t anchor = *reinterpret_cast<const uint64_t*>(rec);
         const uint2 eh = *reinterpret_cast<const uint2*>(rec + 8);
+        const uint64_t lowv = *reinterpret_cast<const uint64_t*>(rec + kWHead + 8u * tid);
+        const uint32_t sh = 4u * (tid & 1u);
+        const uint32_t hb = (rec[kWHi + tid / 2u] >> sh) & 0xFu, cb = (rec[kWCnt + tid / 2u] >> sh) & 0xFu;
         const bool wide = (eh.y >> 31) != 0u;
         const uint64_t etot = sesc[s];
         const uint64_t wlo = eh.x < etot ? eh.x : etot;
@@ -283,52 +301,54 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
         wn = (uint32_t)((uint64_t)wn < etot - wlo ? (uint64_t)wn : etot - wlo);
         wn = wn < (uint32_t)kWMaxWords ? wn : (uint32_t)kWMaxWords;
         for (uint32_t w = tid; w < wn; w += kWThreads) wbuf[w] = etab[wlo + w];
-        __syncthreads();
-        auto word = [&](uint32_t p) { return p < wn ? wbuf[p] : 0u; };
-        const uint16_t* const low = reinterpret_cast<const uint16_t*>(rec + kWHead);
-        uint64_t* const oc = out_codes + sdst[s] + cl * kWChunk;
-        uint32_t* const on = out_counts + sdst[s] + cl * kWChunk;
-        uint64_t carry = anchor;
-        uint32_t wcarry = 0u;
+        uint32_t tw = 0u;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
-            const uint32_t i = (uint32_t)j * kWThreads + tid;
-            const bool v = i < n;
-            const uint32_t o = ((uint32_t)j * kWThreads + wave * 64u) / 8u;
-            const bool hf = v && ((*reinterpret_cast<const uint64_t*>(rec + kWHi + o) >> lane) & 1ull);
-            const bool cf = v && ((*reinterpret_cast<const uint64_t*>(rec + kWCnt + o) >> lane) & 1ull);
-            const uint32_t gw = hf ? (wide ? 2u : 1u) : 0u, nw = gw + (cf ? 1u : 0u);
-            // both scans at once: escape words (u32) and, once the words are read, gaps (u64)
-            const uint32_t wincl = scan64(nw);
-            if (lane == 63u) ws[wave] = wincl;
-            __syncthreads();
-            uint32_t pos = wcarry + wincl - nw, wtot = 0u;
-#pragma unroll
-            for (int w = 0; w < kWThreads / 64; ++w) {
-                pos += (uint32_t)w < wave ? ws[w] : 0u;
-                wtot += ws[w];
-            }
-            wcarry += wtot;
-            uint64_t hi = 0ull;
-            if (hf) hi = (uint64_t)word(pos) | (wide ? (uint64_t)word(pos + 1u) << 32 : 0ull);
-            const uint32_t cnt = cf ? word(pos + gw) : 1u;
-            const uint64_t gap = v ? ((uint64_t)low[i] | (hi << 16)) : 0ull;
-            const uint64_t incl = wave_incl_u64(gap);
-            if (lane == 63u) ws64[wave] = incl;
-            __syncthreads();
-            uint64_t pre = 0ull, tot = 0ull;
-#pragma unroll
-            for (int w = 0; w < kWThreads / 64; ++w) {
-                pre += (uint32_t)w < wave ? ws64[w] : 0ull;
-                tot += ws64[w];
-            }
-            if (v) {
-                oc[i] = carry + pre + incl;
-                on[i] = cnt;
-            }
-            carry += tot;
-            __syncthreads();   // ws / ws64 reused by the next round; wbuf by the next chunk
+            const bool v = i0 + j < n;
+            tw += (v && ((hb >> j) & 1u) ? (wide ? 2u : 1u) : 0u) + (v && ((cb >> j) & 1u) ? 1u : 0u);
         }
+        uint32_t tot;
+        uint32_t p = block_excl(tw, ws, &tot);   // (its barriers also publish wbuf)
+        uint64_t gap[kWPer];
+        uint32_t cnt[kWPer];
+        uint64_t sum = 0ull;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const bool v = i0 + j < n;
+            uint64_t hi = 0ull;
+            if (v && ((hb >> j) & 1u)) {
+                hi = p < wn ? wbuf[p] : 0u;
+                ++p;
+                if (wide) {
+                    hi |= (uint64_t)(p < wn ? wbuf[p] : 0u) << 32;
+                    ++p;
+                }
+            }
+            cnt[j] = 1u;
+            if (v && ((cb >> j) & 1u)) {
+                cnt[j] = p < wn ? wbuf[p] : 0u;
+                ++p;
+            }
+            gap[j] = v ? (((lowv >> (16 * j)) & 0xFFFFull) | (hi << 16)) : 0ull;
+            sum += gap[j];
+        }
+        const uint64_t incl = wave_incl_u64(sum);
+        if (lane == 63u) ws64[wave] = incl;
+        __syncthreads();
+        uint64_t code = anchor + incl - sum;
+#pragma unroll
+        for (int w = 0; w < kWThreads / 64; ++w) code += (uint32_t)w < wave ? ws64[w] : 0ull;
+        uint64_t* const oc = out_codes + sdst[s] + cl * kWChunk + i0;
+        uint32_t* const on = out_counts + sdst[s] + cl * kWChunk + i0;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            code += gap[j];
+            if (i0 + j < n) {
+                oc[j] = code;
+                on[j] = cnt[j];
+            }
+        }
+        __syncthreads();   // wbuf and ws64 are rewritten by the next chunk
     }
 }
 

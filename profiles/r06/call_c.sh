@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 6: union changes (unit-major row starts, slot-table rows up to 256): shard tests, then the
+# simulated N = 8 rank and the N = 1 matrix under a kernel trace.
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r06c}
+mkdir -p $OUT
+python3 -c "import sys; sys.path.insert(0, 'kmer-ml_amd'); from kmerml import _native; print(_native.build_id())" > $OUT/build_id.txt
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  -k "shard_union or sharded_on_gpu or two_config5_genomes or wire_round_trip" > $OUT/tests.log 2>&1
+rc=$?
+tail -3 $OUT/tests.log
+[ $rc -eq 0 ] || exit 10
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 -u bench.py --workload sparse --simulate-ranks 8 --steps 2 > $OUT/sim8.log 2>&1 || exit 12
+f=$(find $OUT/trace -name "*kernel_stats.csv" | head -1)
+cp "$f" $OUT/kernel_stats.csv
+python3 - $OUT/kernel_stats.csv <<'P'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+for r in rows[:14]:
+    print(f'{r["Name"][:70]:70s} {int(r["Calls"]):5d} avg {float(r["AverageNs"])/1e6:9.3f} ms tot {float(r["TotalDurationNs"])/1e6:9.2f}')
+P
+grep -o '"phases_ms[^}]*}' $OUT/sim8.log
+timeout -k 10 300 python3 -u bench.py --workload sparse --steps 3 --cpu-sample 0 > $OUT/sparse.log 2>&1 || exit 11
+grep -o '"matrix": {"matrix_ms[^,]*,[^,]*,[^,]*' $OUT/sparse.log

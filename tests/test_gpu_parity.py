@@ -1429,7 +1429,7 @@ def _shard_union(ctx, dev, rows, lo, hi_incl):
 
 
 @pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow", "wide", "many_rows", "dense_cell",
-                                  "max_rows", "slot_rows64"])
+                                  "max_rows", "slot_rows64", "rows200"])
 def test_shard_union_vs_numpy(ctx, dev, case):
     """kmh_shard_union_dev (the column union and CSR indices of a shard) against numpy's
     union1d / searchsorted: rows of distinct codes (the LDS path), rows sharing half their codes,
@@ -1442,9 +1442,10 @@ def test_shard_union_vs_numpy(ctx, dev, case):
     (VERDICT r05 item 4): R = 64, the largest row count whose gathered entries find their rows
     through the 64-entry slot table, with one dense window cut into ~120 units whose row pieces
     range from ~20 entries (inside one slot) to ~500 (spanning 7-8 slots, starting at every offset
-    of a slot) -- the shape of the only case (dense_cell) that failed the first slot-table build."""
+    of a slot) -- the shape of the only case (dense_cell) that failed the first slot-table build;
+    rows200: 200 rows sharing a pool of codes (the slot table beyond 64 rows, up to its 256)."""
     rng = np.random.default_rng({"distinct": 1, "shared": 2, "identical": 3, "mixed": 4, "narrow": 5, "wide": 6,
-                                 "many_rows": 7, "dense_cell": 8, "max_rows": 9, "slot_rows64": 10}[case])
+                                 "many_rows": 7, "dense_cell": 8, "max_rows": 9, "slot_rows64": 10, "rows200": 11}[case])
     lo, hi = 1 << 40, (1 << 41) - 1
     if case == "distinct":
         rows = [np.unique(rng.integers(lo, hi, 200_000, dtype=np.uint64)) for _ in range(7)]
@@ -1474,6 +1475,9 @@ def test_shard_union_vs_numpy(ctx, dev, case):
         pool = rng.integers(lo, hi, 100_000, dtype=np.uint64)
         rows = [np.unique(rng.choice(pool, 40)) for _ in range(4096)]
         rows[4000] = np.zeros(0, np.uint64)
+    elif case == "rows200":   # R = 200: the slot table's rows past 64 (config 5's N = 8 shard has 128)
+        pool = rng.integers(lo, hi, 3_000_000, dtype=np.uint64)
+        rows = [np.unique(rng.choice(pool, 1_000 + 37 * r)) for r in range(200)]
     elif case == "slot_rows64":
         win = lo + (1 << 39) + np.arange(1 << 22, dtype=np.uint64)
         sizes = [40_000 if r % 10 == 0 else 2_000 + 500 * (r % 9) for r in range(64)]
