@@ -72,3 +72,10 @@ $(FABBENCH): tests/native/fabric_bench.hip
 	@mkdir -p $(OUTDIR)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
 .PHONY: fabbench
+
+RINGBENCH := $(OUTDIR)/ring_bench
+ringbench: $(RINGBENCH)
+$(RINGBENCH): tests/native/ring_bench.hip
+	@mkdir -p $(OUTDIR)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+.PHONY: ringbench

@@ -23,3 +23,8 @@ P
 grep -o '"phases_ms[^}]*}' $OUT/sim8.log
 timeout -k 10 300 python3 -u bench.py --workload sparse --steps 3 --cpu-sample 0 > $OUT/sparse.log 2>&1 || exit 11
 grep -o '"matrix": {"matrix_ms[^,]*,[^,]*,[^,]*' $OUT/sparse.log
+# the consumer-resident exchange floor: memory + LDS only
+for args in "8 64 1" "8 64 0" "8 32 1" "8 128 1" "16 64 1"; do
+  timeout -k 10 120 kmer-ml_amd/kmerml/_lib/ring_bench $args 3 >> $OUT/ring_bench.log 2>&1 || { echo "ring_bench $args rc=$?" >> $OUT/ring_bench.log; break; }
+done
+cat $OUT/ring_bench.log
