@@ -142,11 +142,16 @@ __device__ __forceinline__ uint32_t unit_of(const uint64_t* __restrict__ ub, uin
 
 // Block-wide exclusive scan of one u32 per thread (kShThreads); returns the thread's prefix,
 // *total = the sum.  ws: kShThreads / 64 words of LDS.
+//
+// Every barrier of the union is lds_barrier() (kmh_device.h): the kernel never reads back what it
+// stores, and __syncthreads() -- a workgroup release, s_waitcnt vmcnt(0) -- made each of a unit's
+// ~10 barriers wait for the stores of the previous unit and for the loads prefetched for the next
+// one (round 6: the software pipelining over units only works with LDS-only barriers).
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t incl = scan64(v);
     if (lane == 63) ws[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     uint32_t pre = 0u, tot = 0u;
 #pragma unroll
     for (int w = 0; w < kShThreads / 64; ++w) {
@@ -154,7 +159,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
         pre += w < wave ? x : 0u;
         tot += x;
     }
-    __syncthreads();   // ws reusable
+    lds_barrier();   // ws reusable
     *total = tot;
     return pre + incl - v;
 }
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     if (s >= S) return;   // (whole workgroup)
     issue_st(s);
     uint32_t Tc = build(s, 0);
-    __syncthreads();
+    lds_barrier();
     uint64_t cv[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) cv[u] = 0ull;
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         const unsigned long long cb2 = WRITE && has2 ? colbase[s2] : 0ull;
         for (int q = 0; q < BPT; ++q) hist[q * kShThreads + tid] = 0u;
         if (tid == 0) flag = 0u;
-        __syncthreads();
+        lds_barrier();
         const uint32_t T = Tc;
         const bool ok = T >= 1u && T <= (uint32_t)kShCap;   // (uniform)
         if (!ok && !WRITE && tid == 0) {   // empty (a part of a coarse cell with no entries) or too big
@@ -341,7 +346,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 bv[u] = (uint32_t)min((K)(cv[u] - base) >> bsh, (K)(kShBins - 1));
                 if (i < T) atomicAdd(&hist[bv[u]], 1u);
             }
-            __syncthreads();
+            lds_barrier();
             // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
             {
                 uint32_t v[BPT], sum = 0u;
@@ -359,7 +364,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     o += v[q];
                 }
             }
-            __syncthreads();
+            lds_barrier();
             sorted_ok = flag == 0u;   // (uniform)
             if (!sorted_ok && !WRITE && tid == 0) {
                 ucount[s] = 0u;
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         // this unit's sort, heads and stores)
         uint32_t T2 = 0u;
         if (has2) T2 = build(s2, k ^ 1);   // (its barriers also order the scatter before the sort)
-        __syncthreads();
+        lds_barrier();
         if (has2 && T2 >= 1u && T2 <= (uint32_t)kShCap) gather(T2, k ^ 1, cv, rk2);
         if (!WRITE && sorted_ok) {
             // the union's size needs no order: position p counts iff no earlier position of its
@@ -452,7 +457,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     }
                     dst[u] = p < T && be - bs > 1u ? bs + rk : 0xFFFFFFFFu;   // (single entries stay)
                 }
-                __syncthreads();
+                lds_barrier();
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     if (dst[u] != 0xFFFFFFFFu) {
@@ -461,7 +466,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     }
                 }
             }
-            __syncthreads();
+            lds_barrier();
             // 6. run heads = the distinct codes; thread t owns positions PER t .. PER t + PER - 1,
             //    read as 16-byte vectors (PER single reads at a stride of PER words were 8-way bank
             //    conflicts); positions past T hold stale codes and are masked
@@ -512,7 +517,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                         colrel[(ixw[u >> 1] >> (16 * (u & 1))) & 0xFFFFu] = run - 1u;
                     }
                 }
-                __syncthreads();
+                lds_barrier();
                 int rv[PER];
                 if (R <= kShSlotRows) {   // (uniform) the rows found by the gather
 #pragma unroll
@@ -534,7 +539,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
         if (!has2) break;
-        __syncthreads();   // the LDS tables are rewritten by the next unit
+        lds_barrier();   // the LDS tables are rewritten by the next unit
         s = s2;
         Tc = T2;
         k ^= 1;

@@ -79,11 +79,11 @@ __device__ __forceinline__ uint64_t block_sum64(uint64_t v, uint64_t* ws) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
     if ((threadIdx.x & 63u) == 0u) ws[threadIdx.x >> 6] = v;
-    __syncthreads();
+    lds_barrier();
     uint64_t t = 0u;
 #pragma unroll
     for (int w = 0; w < kWThreads / 64; ++w) t += ws[w];
-    __syncthreads();
+    lds_barrier();
     return t;
 }
 
@@ -189,14 +189,14 @@ __device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* ws, uint32_
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t incl = scan64(v);
     if (lane == 63u) ws[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     uint32_t pre = incl - v, tot = 0u;
 #pragma unroll
     for (int w = 0; w < kWThreads / 64; ++w) {
         pre += (uint32_t)w < wave ? ws[w] : 0u;
         tot += ws[w];
     }
-    __syncthreads();
+    lds_barrier();
     *total = tot;
     return pre;
 }
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
         }
         const uint64_t incl = wave_incl_u64(sum);
         if (lane == 63u) ws64[wave] = incl;
-        __syncthreads();
+        lds_barrier();
         uint64_t code = anchor + incl - sum;
 #pragma unroll
         for (int w = 0; w < kWThreads / 64; ++w) code += (uint32_t)w < wave ? ws64[w] : 0ull;
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
                 on[j] = cnt[j];
             }
         }
-        __syncthreads();   // wbuf and ws64 are rewritten by the next chunk
+        lds_barrier();   // wbuf and ws64 are rewritten by the next chunk
     }
 }
 
