@@ -167,7 +167,7 @@ def _sparse_worker(rank, world, port, files, orgs, k, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k,G", [(2, 13, 3), (2, 21, 3), (3, 21, 5), (4, 32, 5)])
+@pytest.mark.parametrize("world,k,G", [(2, 13, 3), (2, 21, 3), (3, 21, 5), (4, 32, 5), (3, 32, 2)])
 def test_sparse_matrix_column_sharded_gloo(tmp_path, oracle_lib, world, k, G):
     """Config 5's matrix: each of `world` ranks counts its block of genomes, the code
     space is cut into `world` ranges of ~equal entries and one all-to-all-v (gloo here, RCCL on the
@@ -175,7 +175,8 @@ def test_sparse_matrix_column_sharded_gloo(tmp_path, oracle_lib, world, k, G):
     equal the reference's matrix built from the per-organism files: k{k}.txt (the restated
     generate.py writer) -> KmerFeatureExtractor CSVs -> KmerFeatureBuilder.build_from_statistics_
     files (features.py:28-117: sorted union of labels, missing = 0; k = 13 has the integer-parsed,
-    A-stripped labels, k = 21 the exact k-mer text)."""
+    A-stripped labels, k = 21 the exact k-mer text).  k = 32 with a poly-T run puts the code
+    2^64 - 1 in the top histogram bucket, and world 3 > G = 2 leaves a rank without genomes."""
     import contextlib
     import io
     from oracle import kmers as okmers
@@ -192,6 +193,8 @@ def test_sparse_matrix_column_sharded_gloo(tmp_path, oracle_lib, world, k, G):
             seq = seq[:600] + seq[:600].lower() + "NNNNN" + seq[600:]
         if i == 2:
             seq = seq + "ACGTTGCA" * 40
+        if i == 1 and k == 32:   # TTT...T: the code 2^64 - 1, in the histogram's last bucket
+            seq = seq + "T" * 50
         fa = tmp_path / f"{org}.fa"
         osynth.write_fasta(fa, [(org, seq.encode()), ("short", b"ACGTA")])
         files.append(str(fa))
@@ -210,3 +213,30 @@ def test_sparse_matrix_column_sharded_gloo(tmp_path, oracle_lib, world, k, G):
     nnz = [int(x) for x in (tmp_path / f"nnz_k{k}.txt").read_text().split()]
     assert len(nnz) == world
     assert min(nnz) > 0.5 * sum(nnz) / world   # the code ranges balance the entries
+
+
+def test_sparse_matrix_many_rows_takes_host_path(tmp_path, monkeypatch, oracle_lib):
+    """kmh_shard_union_dev holds at most SHARD_MAX_ROWS organism rows, so a
+    matrix with more organisms than that is routed to the host assembly (sparse_rows + the sorted
+    union on the host), not to the device shard that would fail at its last step.  The limit is
+    lowered to 2 here, with 3 genomes and the GPU counter replaced by the C oracle's rows."""
+    from oracle import synth as osynth
+    files = []
+    for i in range(3):
+        fa = tmp_path / f"g{i}.fa"
+        osynth.write_fasta(fa, [(f"g{i}", osynth.synth_bases(3000, osynth.genome_seed(90 + i)).tobytes())])
+        files.append(str(fa))
+    monkeypatch.setattr(kmatrix, "SHARD_MAX_ROWS", 2)
+
+    def no_device(*a, **k):
+        raise AssertionError("the device shard was chosen for more rows than it holds")
+    monkeypatch.setattr(kmatrix, "_sparse_matrix_dev", no_device)
+    monkeypatch.setattr(kmatrix, "sparse_rows", lambda fs, k, canonical=True, device=None, group=None:
+                        (0, _sparse_rows_oracle(fs, k)))
+    m = kmatrix.sparse_matrix(files, 21, canonical=False)
+    rows = _sparse_rows_oracle(files, 21)
+    want = np.unique(np.concatenate([c for c, _ in rows]))
+    assert m.G == 3 and np.array_equal(m.columns, want)
+    for g, (c, n) in enumerate(rows):
+        a, b = int(m.indptr[g]), int(m.indptr[g + 1])
+        assert np.array_equal(m.columns[m.indices[a:b]], c) and np.array_equal(m.values[a:b], n)
