@@ -109,24 +109,49 @@ __global__ __launch_bounds__(256) void k_shard_units(const uint32_t* __restrict_
 // st[u * R + r] = the first entry of row r whose code is >= unit u's first code, found inside the
 // unit's coarse cell; st[U * R + r] = the row's length.  Unit-major, so that a union workgroup reads
 // one unit's R row starts as one contiguous run (row-major, each unit read R cache lines: at R = 128
-// rows that was most of the union's memory traffic).  One thread per (u, r), r fastest.
+// rows that was most of the union's memory traffic).  One workgroup per 64 units, rows in chunks of
+// 64: the searches run units-fastest (a wave searches 64 neighbouring units of ONE row, so its
+// loads share lines), then an LDS transpose writes every unit's row starts as one run (searching
+// rows-fastest was 2.4x slower at R = 128).
+constexpr int kUsU = 64, kUsR = 64;
+
 __global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restrict__ codes,
                                                        const uint64_t* __restrict__ roff, int R,
                                                        const uint32_t* __restrict__ cs, uint32_t Q,
                                                        const uint64_t* __restrict__ ub,
                                                        const uint32_t* __restrict__ ucell, uint32_t U,
                                                        uint32_t* __restrict__ st) {
-    const uint64_t x = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (x >= (uint64_t)(U + 1u) * (uint64_t)R) return;
-    const uint32_t u = (uint32_t)(x / (uint64_t)R), r = (uint32_t)(x % (uint64_t)R);
-    const uint64_t a = roff[r];
-    if (u == U) {
-        st[x] = (uint32_t)(roff[r + 1] - a);
-        return;
+    __shared__ uint32_t tile[kUsU][kUsR + 1];
+    const uint32_t u0 = blockIdx.x * (uint32_t)kUsU;
+    const uint32_t nu = min((uint32_t)kUsU, U + 1u - u0);
+    for (int r0 = 0; r0 < R; r0 += kUsR) {
+        const int nr = min(kUsR, R - r0);
+        for (int idx = threadIdx.x; idx < kUsU * kUsR; idx += 256) {
+            const uint32_t uu = (uint32_t)(idx % kUsU);
+            const int rr = idx / kUsU;
+            if (uu < nu && rr < nr) {
+                const uint32_t u = u0 + uu;
+                const int r = r0 + rr;
+                const uint64_t a = roff[r];
+                uint32_t v;
+                if (u == U) {
+                    v = (uint32_t)(roff[r + 1] - a);
+                } else {
+                    const uint32_t q = ucell[u];
+                    const uint32_t* c = cs + (uint64_t)r * (Q + 1u);
+                    v = lower_in(codes + a, c[q], c[q + 1u], ub[u]);
+                }
+                tile[uu][rr] = v;
+            }
+        }
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < kUsU * kUsR; idx += 256) {
+            const int rr = idx % kUsR;
+            const uint32_t uu = (uint32_t)(idx / kUsR);
+            if (uu < nu && rr < nr) st[(uint64_t)(u0 + uu) * (uint64_t)R + (uint64_t)(r0 + rr)] = tile[uu][rr];
+        }
+        __syncthreads();
     }
-    const uint32_t q = ucell[u];
-    const uint32_t* c = cs + (uint64_t)r * (Q + 1u);
-    st[x] = lower_in(codes + a, c[q], c[q + 1u], ub[u]);
 }
 
 // Unit of code c (fallback only): the last unit whose first code is <= c.
@@ -787,8 +812,7 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     hipLaunchKernelGGL(k_shard_units, dim3((Q + 255) / 256), dim3(256), 0, s, d_nu, d_ubase, Q, lo, hi_incl, CSH, d_ub,
                        d_ue, d_ucell);
     KMH_HIP(ctx, hipGetLastError());
-    const uint64_t nus = (uint64_t)(S + 1) * (uint64_t)R;
-    hipLaunchKernelGGL(k_shard_ustarts, dim3((unsigned)((nus + 255) / 256)), dim3(256), 0, s, codes, d_roff, R, d_cs, Q,
+    hipLaunchKernelGGL(k_shard_ustarts, dim3((unsigned)(((uint64_t)S + 1 + kUsU - 1) / kUsU)), dim3(256), 0, s, codes, d_roff, R, d_cs, Q,
                        d_ub, d_ucell, S, d_st);
     KMH_HIP(ctx, hipGetLastError());
     KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));

@@ -20,10 +20,11 @@
 // Per genome: 100.7 MB of bases read, 201 MB through the ring each way, 67 MB of rows written (the
 // same bytes as the real pattern, synthetic segment sizes: 64 entries per (tile, bucket)).  Every
 // spin is bounded (a timeout word is set and the kernel exits; the host reports it).
-//   ring_bench [genomes=8] [ring_MiB=64] [lds_adds=1] [reps=3]
+//   ring_bench [genomes=8] [ring_MiB=64] [lds_adds=1] [reps=3] [shape=4x1|4x2|8x1|8x2|12x2]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <vector>
@@ -33,7 +34,7 @@ constexpr int kTileWin = 16384;              // windows per tile
 constexpr int kSegBytes = kTileWin * 2 / kB;  // 128 B per (tile, bucket)
 constexpr int kSlotBytes = kTileWin * 2;     // 32 KiB per ring slot
 constexpr int kTilesPerGenome = 6144;        // 100.66 Mbp per genome (a multiple of 64 x 4 x ... tiles)
-constexpr int kWaves = 16, kCons = 4, kProd = kWaves - kCons;
+constexpr int kWaves = 16;
 constexpr int kGroup = 64;                   // tiles per consumer group (one per lane)
 constexpr unsigned kSpinMax = 1u << 22;      // bounded spins (s_sleep 2 each: a few seconds at most)
 
@@ -47,6 +48,9 @@ __device__ __forceinline__ void st_agent(unsigned* p, unsigned v) {
     __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// NC consumer waves (bucket blockIdx.x) and 16 - NC producer waves per workgroup; a consumer wave
+// takes GPI of its groups per round (GPI x 8 loads of 16 B per lane in flight).
+template <int NC, int GPI>
 __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases, uint8_t* ring, unsigned RT,
                                                unsigned ntiles, unsigned* ready, unsigned* progress,
                                                unsigned* timeout, uint32_t* rows, int lds_adds) {
@@ -57,6 +61,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
     for (int i = tid; i < 32768; i += 1024) table[i] = 0u;
     if (tid == 0) meet = 0u;
     __syncthreads();
+    constexpr int kCons = NC, kProd = kWaves - NC;
     const auto ring_rsrc = __builtin_amdgcn_make_buffer_rsrc(ring, (short)0, 0x7FFFFFFF, 0x00020000);
     if (wave >= kCons) {
         // ---------------------------------------------------------------- producer wave
@@ -103,8 +108,8 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
     // -------------------------------------------------------------------- consumer wave
     const unsigned ngroups = ntiles / kGroup, gpg = kTilesPerGenome / kGroup;   // groups per genome
     unsigned genome = 0;
-    for (unsigned gi = (unsigned)wave;; gi += kCons) {
-        // genome boundary for this wave: the 4 waves meet, write the row slice, clear the table
+    for (unsigned gi = (unsigned)wave;; gi += kCons * GPI) {
+        // genome boundary for this wave: the waves meet, write the row slice, clear the table
         const unsigned gnext = gi < ngroups ? gi / gpg : ntiles / kTilesPerGenome;
         while (genome < gnext) {
             unsigned spins = 0;
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
-            // row slice: bins of bucket b of this genome, 256 KB; this wave's quarter
+            // row slice: bins of bucket b of this genome, 256 KB; this wave's share
             uint4* row = reinterpret_cast<uint4*>(rows + ((size_t)genome * kB + b) * 65536u);
             for (int i = wave * 64 + lane; i < 16384; i += kCons * 64) {
                 const uint32_t w0 = table[2 * i], w1 = table[2 * i + 1];
@@ -136,38 +141,53 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
             ++genome;
         }
         if (gi >= ngroups) break;
-        const unsigned T0 = gi * kGroup, tl = T0 + (unsigned)lane;
-        const unsigned slot = tl % RT;
+        // GPI groups gi, gi + NC, ...: lane i polls tile i of each, then loads their segments
+        unsigned slot[GPI], tl[GPI];
+#pragma unroll
+        for (int q = 0; q < GPI; ++q) {
+            tl[q] = (gi + (unsigned)(q * kCons)) * kGroup + (unsigned)lane;
+            slot[q] = tl[q] % RT;
+        }
         unsigned spins = 0;
-        while (!__all(ld_agent(ready + slot) == tl + 1u)) {
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < GPI; ++q) ok = ok && ld_agent(ready + slot[q]) == tl[q] + 1u;
+            if (__all(ok)) break;
             if (++spins > kSpinMax || ld_agent(timeout)) {
                 if (lane == 0) st_agent(timeout, 4u);
                 return;
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        const int off = (int)(slot * (unsigned)kSlotBytes + b * (unsigned)kSegBytes);
-        u32x4 s[8];
+        u32x4 sv[GPI][8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s[k] = __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, off + 16 * k, 0, 16);
-        if (lds_adds) {
+        for (int q = 0; q < GPI; ++q) {
+            const int off = (int)(slot[q] * (unsigned)kSlotBytes + b * (unsigned)kSegBytes);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t w[4] = {s[k].x, s[k].y, s[k].z, s[k].w};
-#pragma unroll
-                for (int h = 0; h < 8; ++h) {
-                    const uint32_t x = (w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
-                    atomicAdd(&table[x >> 1], 1u << (16 * (x & 1u)));
-                }
-            }
-        } else {
-            uint32_t acc = 0u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc ^= s[k].x ^ s[k].w;
-            if (acc == 0x9E3779B9u) table[lane] = acc;
+            for (int k = 0; k < 8; ++k) sv[q][k] = __builtin_amdgcn_raw_buffer_load_b128(ring_rsrc, off + 16 * k, 0, 16);
         }
-        // progress: this wave is done with every tile before its next group
-        if (lane == 0) st_agent(progress + b * kCons + wave, T0 + kCons * kGroup);
+#pragma unroll
+        for (int q = 0; q < GPI; ++q) {
+            if (lds_adds) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t w[4] = {sv[q][k].x, sv[q][k].y, sv[q][k].z, sv[q][k].w};
+#pragma unroll
+                    for (int h = 0; h < 8; ++h) {
+                        const uint32_t x = (w[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+                        atomicAdd(&table[x >> 1], 1u << (16 * (x & 1u)));
+                    }
+                }
+            } else {
+                uint32_t acc = 0u;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc ^= sv[q][k].x ^ sv[q][k].w;
+                if (acc == 0x9E3779B9u) table[lane] = acc;
+            }
+        }
+        // progress: this wave is done with every tile before its next round
+        if (lane == 0) st_agent(progress + b * kCons + wave, (gi + kCons * GPI) * kGroup);
     }
     if (lane == 0) st_agent(progress + b * kCons + wave, 0xFFFFFFFFu);
 }
@@ -177,6 +197,7 @@ int main(int argc, char** argv) {
     const int ring_mib = argc > 2 ? atoi(argv[2]) : 64;
     const int lds_adds = argc > 3 ? atoi(argv[3]) : 1;
     const int reps = argc > 4 ? atoi(argv[4]) : 3;
+    const char* shape = argc > 5 ? argv[5] : "4x1";   // consumer waves x groups per round
     const unsigned RT = (unsigned)((size_t)ring_mib * 1024 * 1024 / kSlotBytes);
     const unsigned ntiles = (unsigned)G * kTilesPerGenome;
     int ncu = 0;
@@ -189,7 +210,7 @@ int main(int argc, char** argv) {
     unsigned *ready, *progress, *timeout;
     uint32_t* rows;
     if (hipMalloc(&bases, (size_t)ntiles * kTileWin) || hipMalloc(&ring, (size_t)RT * kSlotBytes) ||
-        hipMalloc(&ready, (size_t)RT * 4) || hipMalloc(&progress, kB * kCons * 4) || hipMalloc(&timeout, 256) ||
+        hipMalloc(&ready, (size_t)RT * 4) || hipMalloc(&progress, kB * 16 * 4) || hipMalloc(&timeout, 256) ||
         hipMalloc(&rows, (size_t)G * kB * 65536 * 4)) {
         printf("{\"error\": \"alloc failed\"}\n");
         return 1;
@@ -202,11 +223,16 @@ int main(int argc, char** argv) {
     unsigned tmo = 0;
     for (int r = 0; r < reps + 1 && !tmo; ++r) {
         (void)hipMemset(ready, 0, (size_t)RT * 4);
-        (void)hipMemset(progress, 0, kB * kCons * 4);
+        (void)hipMemset(progress, 0, kB * 16 * 4);
         (void)hipMemset(timeout, 0, 256);
         (void)hipDeviceSynchronize();
         (void)hipEventRecord(e0, 0);
-        hipLaunchKernelGGL(k_ring, dim3(kB), dim3(1024), 0, 0, bases, ring, RT, ntiles, ready, progress, timeout, rows,
+        auto k = &k_ring<4, 1>;
+        if (!strcmp(shape, "4x2")) k = &k_ring<4, 2>;
+        if (!strcmp(shape, "8x1")) k = &k_ring<8, 1>;
+        if (!strcmp(shape, "8x2")) k = &k_ring<8, 2>;
+        if (!strcmp(shape, "12x2")) k = &k_ring<12, 2>;
+        hipLaunchKernelGGL(k, dim3(kB), dim3(1024), 0, 0, bases, ring, RT, ntiles, ready, progress, timeout, rows,
                            lds_adds);
         (void)hipEventRecord(e1, 0);
         if (hipDeviceSynchronize() != hipSuccess) {
@@ -220,10 +246,10 @@ int main(int argc, char** argv) {
     }
     std::sort(ms.begin(), ms.end());
     const double med = ms.empty() ? 0.0 : ms[ms.size() / 2];
-    printf("{\"genomes\": %d, \"ring_MiB\": %d, \"ring_tiles\": %u, \"lds_adds\": %d, \"timeout\": %u, "
+    printf("{\"shape\": \"%s\", \"genomes\": %d, \"ring_MiB\": %d, \"ring_tiles\": %u, \"lds_adds\": %d, \"timeout\": %u, "
            "\"ms\": %.4f, \"us_per_genome\": %.2f, \"bases_per_genome\": %d, "
            "\"hbm_algorithmic_MB_per_genome\": %.1f, \"ring_MB_each_way_per_genome\": %.1f}\n",
-           G, ring_mib, RT, lds_adds, tmo, med, med * 1000.0 / G, kTilesPerGenome * kTileWin,
+           shape, G, ring_mib, RT, lds_adds, tmo, med, med * 1000.0 / G, kTilesPerGenome * kTileWin,
            (kTilesPerGenome * (double)kTileWin + kB * 65536.0 * 4) / 1e6, kTilesPerGenome * (double)kSlotBytes / 1e6);
     return tmo ? 4 : 0;
 }
