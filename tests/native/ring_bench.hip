@@ -36,7 +36,8 @@ constexpr int kSlotBytes = kTileWin * 2;     // 32 KiB per ring slot
 constexpr int kTilesPerGenome = 6144;        // 100.66 Mbp per genome (a multiple of 64 x 4 x ... tiles)
 constexpr int kWaves = 16;
 constexpr int kGroup = 64;                   // tiles per consumer group (one per lane)
-constexpr unsigned kSpinMax = 1u << 22;      // bounded spins (s_sleep 2 each: a few seconds at most)
+constexpr unsigned kSpinMax = 1u << 22;      // bounded spins (s_sleep 2-16 each: seconds at most)
+constexpr int kRep = 8;                      // flag replicas (one per XCD)
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
                     if (lane == 0) st_agent(timeout, 1u);
                     return;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(16);   // (back-pressure polls: 1024 words, not too often)
             }
             // the tile's bases: 16 KB, 256 B per lane, in two halves; 32 KB of suffixes written
             // through (sc1): 512 B per lane
@@ -101,7 +102,9 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) st_agent(ready + slot, t + 1u);
+            // one flag replica per XCD (each on lines of its own): the 256 consumers poll every tile's
+            // flag, and one replica polled by all of them serialised at its memory channel
+            if (lane < kRep) st_agent(ready + (unsigned)lane * RT + slot, t + 1u);
         }
         return;
     }
@@ -152,7 +155,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
         for (;;) {
             bool ok = true;
 #pragma unroll
-            for (int q = 0; q < GPI; ++q) ok = ok && ld_agent(ready + slot[q]) == tl[q] + 1u;
+            for (int q = 0; q < GPI; ++q) ok = ok && ld_agent(ready + (b % kRep) * RT + slot[q]) == tl[q] + 1u;
             if (__all(ok)) break;
             if (++spins > kSpinMax || ld_agent(timeout)) {
                 if (lane == 0) st_agent(timeout, 4u);
@@ -210,7 +213,7 @@ int main(int argc, char** argv) {
     unsigned *ready, *progress, *timeout;
     uint32_t* rows;
     if (hipMalloc(&bases, (size_t)ntiles * kTileWin) || hipMalloc(&ring, (size_t)RT * kSlotBytes) ||
-        hipMalloc(&ready, (size_t)RT * 4) || hipMalloc(&progress, kB * 16 * 4) || hipMalloc(&timeout, 256) ||
+        hipMalloc(&ready, (size_t)RT * 4 * kRep) || hipMalloc(&progress, kB * 16 * 4) || hipMalloc(&timeout, 256) ||
         hipMalloc(&rows, (size_t)G * kB * 65536 * 4)) {
         printf("{\"error\": \"alloc failed\"}\n");
         return 1;
@@ -222,7 +225,7 @@ int main(int argc, char** argv) {
     std::vector<float> ms;
     unsigned tmo = 0;
     for (int r = 0; r < reps + 1 && !tmo; ++r) {
-        (void)hipMemset(ready, 0, (size_t)RT * 4);
+        (void)hipMemset(ready, 0, (size_t)RT * 4 * kRep);
         (void)hipMemset(progress, 0, kB * 16 * 4);
         (void)hipMemset(timeout, 0, 256);
         (void)hipDeviceSynchronize();
