@@ -20,7 +20,9 @@
 // Per genome: 100.7 MB of bases read, 201 MB through the ring each way, 67 MB of rows written (the
 // same bytes as the real pattern, synthetic segment sizes: 64 entries per (tile, bucket)).  Every
 // spin is bounded (a timeout word is set and the kernel exits; the host reports it).
-//   ring_bench [genomes=8] [ring_MiB=64] [lds_adds=1] [reps=3] [shape=4x1|4x2|8x1|8x2|12x2]
+//   ring_bench [genomes=8] [ring_MiB=64] [mode=1] [reps=3] [shape=4x1|4x2|8x1|8x2|12x2]
+// mode bit 0: the consumers' LDS adds; bit 1: no hand-off protocol (producers never wait, consumers
+// never poll: the data movement alone, results meaningless -- the floor of the bytes).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
         unsigned minprog = 0u;   // all consumers are past tiles < minprog
         for (unsigned t = pid; t < ntiles; t += np) {
             unsigned spins = 0;
-            while (t >= minprog + RT) {   // slot t % RT still holds tile t - RT for some consumer
+            while (!(lds_adds & 2) && t >= minprog + RT) {   // slot t % RT still holds tile t - RT for some consumer
                 unsigned m = 0xFFFFFFFFu;
                 for (int q = lane; q < kB * kCons; q += 64) m = min(m, ld_agent(progress + q));
                 for (int d = 32; d >= 1; d >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, d));
@@ -153,6 +155,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
         }
         unsigned spins = 0;
         for (;;) {
+            if (lds_adds & 2) break;   // mode 2: no hand-off protocol at all (the data movement alone)
             bool ok = true;
 #pragma unroll
             for (int q = 0; q < GPI; ++q) ok = ok && ld_agent(ready + (b % kRep) * RT + slot[q]) == tl[q] + 1u;
@@ -172,7 +175,7 @@ __global__ __launch_bounds__(1024) void k_ring(const uint8_t* __restrict__ bases
         }
 #pragma unroll
         for (int q = 0; q < GPI; ++q) {
-            if (lds_adds) {
+            if (lds_adds & 1) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const uint32_t w[4] = {sv[q][k].x, sv[q][k].y, sv[q][k].z, sv[q][k].w};
