@@ -1027,8 +1027,11 @@ def matrix_leg(a, world, rank, d_seq, offsets, G, k, canonical, dev, steps=2):
         ph["fallback_passes"] = st1["fallback_passes"] - st0["fallback_passes"]
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        m = kmatrix.shard_from_rows(codes, counts, roff, G, k, timings=sph, wire=getattr(a, "matrix_wire", "auto"))
+        held = [codes, counts]   # (shard_from_rows frees the rows once they are sent)
         del codes, counts
+        m = kmatrix.shard_from_rows(held[0], held[1], roff, G, k, timings=sph, wire=getattr(a, "matrix_wire", "auto"),
+                                    owned=held)
+        del held
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -752,7 +752,9 @@ def _row_histogram(codes, roff, k, nbits=16):
 def _sparse_matrix_dev(files, k, canonical, device, group):
     """sparse_matrix on the GPU: sorted device rows (sorted_rows_dev), then shard_from_rows."""
     lo, codes, counts, roff = sorted_rows_dev(files, k, canonical=canonical, device=device, group=group)
-    return shard_from_rows(codes, counts, roff, len(files), k, group=group)
+    held = [codes, counts]
+    del codes, counts
+    return shard_from_rows(held[0], held[1], roff, len(files), k, group=group, owned=held)
 
 
 # the exchange of the last shard_from_rows call with W > 1 ranks (bench / tests): wire format, bytes
@@ -786,7 +788,7 @@ def _a2a(out, inp, out_splits, in_splits, gloo, group):
     return out
 
 
-def shard_from_rows(codes, counts, roff, G, k, group=None, wire="auto", timings=None):
+def shard_from_rows(codes, counts, roff, G, k, group=None, wire="auto", timings=None, owned=None):
     """This rank's ShardedSparseMatrix from its sorted device rows (genomes shard_bounds(G, W,
     rank), row i = codes / counts [roff[i], roff[i + 1])).  With W > 1 ranks:
 
@@ -803,7 +805,9 @@ def shard_from_rows(codes, counts, roff, G, k, group=None, wire="auto", timings=
          the CSR indices, u32 whenever the shard holds fewer than 2^32 - 1 entries.
 
     Every array stays in device memory.  `timings` (a dict) receives per-phase wall ms (each phase
-    synchronised; bench)."""
+    synchronised; bench).  `owned`: a list holding the caller's only references to codes and counts;
+    it is cleared once the rows have been sent, so their memory (12 B per entry) is free before the
+    receive side and the union allocate theirs (at N = 8, 48 GB per rank)."""
     import time
     import torch
     import torch.distributed as dist
@@ -886,6 +890,8 @@ def shard_from_rows(codes, counts, roff, G, k, group=None, wire="auto", timings=
                 _a2a(dst_t[:total], inp, out_splits, in_splits, gloo, group)
                 del inp
             sent, received = raw_bytes, int(sum(out_splits[q] for q in others)) * 12
+            if owned is not None:
+                owned.clear()
             phase("exchange_ms")
         else:
             for j in range(n):   # the rank's own slices: device copies into place
@@ -897,6 +903,10 @@ def shard_from_rows(codes, counts, roff, G, k, group=None, wire="auto", timings=
             send = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
             if sl_n.size:
                 ctx.wire_encode_dev(codes.data_ptr(), counts.data_ptr(), sl_start, sl_n, send.data_ptr(), nbytes, s)
+            if owned is not None:   # the rows are sent: free them before the receive buffers
+                owned.clear()
+                del codes, counts
+                codes = counts = None
             phase("encode_ms")
             in_splits = [0 if q == rank else int(sl_bytes[others.index(q) * n:(others.index(q) + 1) * n].sum())
                          for q in range(world)]
