@@ -220,6 +220,12 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     uint32_t* const ptab = reinterpret_cast<uint32_t*>(sdyn + (R < kShRoffCache ? R : kShRoffCache));
     auto pfx_of = [&](int k) { return ptab + (uint32_t)k * (2u * (uint32_t)R + 1u); };
     auto pa_of = [&](int k) { return ptab + (uint32_t)k * (2u * (uint32_t)R + 1u) + (uint32_t)R + 1u; };
+    // up to kShSlotRows rows, two more tables: row r's piece as one offset, dl[r] = the row's base +
+    // its piece's first entry - the entries gathered before it, so gathered entry i of row r is at
+    // dl[r] + i in the rows' arrays (codes and indices alike): one LDS read per address, not three
+    uint64_t* const dtab = reinterpret_cast<uint64_t*>(
+        reinterpret_cast<char*>(ptab) + ((2u * (2u * (uint32_t)R + 1u)) * 4u + 15u) / 16u * 16u);
+    auto dl_of = [&](int k) { return dtab + (uint32_t)k * (uint32_t)R; };
     __shared__ uint32_t ws[kShThreads / 64];
     __shared__ uint32_t flag;
     // up to kShSlotRows rows: the row holding gathered entry 64 m of piece table k (rtab[k][m])
@@ -298,6 +304,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
         if (tid == 0) pfx[R] = T;
+        if (R <= kShSlotRows && tid < R) dl_of(k)[tid] = row_base(tid) + pa[tid] - pre;   // (pipe_st: one row per thread)
         if (R <= kShSlotRows && tid < R && mine) {   // (one row per thread) the 64-entry slots starting in this row
             // (a unit over kShCap entries is not gathered: its slots past the table are skipped)
             for (uint32_t m = (pre + 63u) >> 6; (m << 6) < pre + mine && m < (uint32_t)(kShCap / 64); ++m)
@@ -323,8 +330,14 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             rk[1] = (uint32_t)rv[4] | (uint32_t)rv[5] << 8 | (uint32_t)rv[6] << 16 | (uint32_t)rv[7] << 24;
         }
         uint64_t at[PER];
+        if (R <= kShSlotRows) {   // (uniform)
+            const uint64_t* const dl = dl_of(k);
 #pragma unroll
-        for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
+            for (int u = 0; u < PER; ++u) at[u] = dl[rv[u]] + iv[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
+        }
 #pragma unroll
         for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
     };
@@ -559,7 +572,11 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                    if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (IX)(cb + colrel[i]);
+                    if (i < T) {
+                        const uint64_t at = R <= kShSlotRows ? dl_of(k)[rv[u]] + i
+                                                             : row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]]);
+                        indices[at] = (IX)(cb + colrel[i]);
+                    }
                 }
             }
         }
@@ -818,7 +835,8 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));
     time_end(ctx, s);
     const unsigned ug = (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * 2);
-    const size_t dyn = (size_t)std::min(R, kShRoffCache) * 8 + ((2 * ((size_t)2 * R + 1)) * 4 + 15) / 16 * 16;
+    const size_t dyn = (size_t)std::min(R, kShRoffCache) * 8 + ((2 * ((size_t)2 * R + 1)) * 4 + 15) / 16 * 16 +
+                       (R <= kShSlotRows ? (size_t)2 * R * 8 : 0);
     time_begin(ctx, s, "k_shard_union");
     // every unit lies inside one coarse cell of 2^CSH codes: u32 offsets when CSH <= 32
     const bool narrow = CSH <= 32;

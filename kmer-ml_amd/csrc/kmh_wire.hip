@@ -407,10 +407,12 @@ static int wire_layout(Ctx* ctx, const uint64_t* sstart, const uint64_t* sn, int
     return upload(ctx, *d_plan, h.data(), (3 * (size_t)S + 1) * 8, s);
 }
 
-// Count + scan + slice bytes of a plan (cached on the context by inputs and slices).
+// Count + scan + slice bytes of a plan.  use_cache: take the result of the last sizing if it was
+// made on the same inputs and slices and not used yet (the encode right after a size call); every
+// use consumes it, and a size call always recomputes, so a stale sizing is never reused.
 static int wire_sizes(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const uint64_t* sstart,
                       const uint64_t* sn, int S, std::vector<uint64_t>& cbase, uint64_t** d_plan,
-                      std::vector<uint64_t>& sbytes, hipStream_t s) {
+                      std::vector<uint64_t>& sbytes, bool use_cache, hipStream_t s) {
     int rc = wire_layout(ctx, sstart, sn, S, cbase, d_plan, s);
     if (rc) return rc;
     const uint64_t NC = cbase[S];
@@ -418,8 +420,9 @@ static int wire_sizes(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_count
     key = fnv(key, sn, S);
     const uint64_t ptrs[3] = {(uint64_t)(uintptr_t)d_codes, (uint64_t)(uintptr_t)d_counts, (uint64_t)S};
     key = fnv(key, ptrs, 3);
-    if (ctx->wire_valid && ctx->wire_key == key && ctx->wire_sbytes.size() == (size_t)S) {
+    if (use_cache && ctx->wire_valid && ctx->wire_key == key && ctx->wire_sbytes.size() == (size_t)S) {
         sbytes = ctx->wire_sbytes;
+        ctx->wire_valid = false;   // (one use)
         return KMH_OK;
     }
     ctx->wire_valid = false;
@@ -459,12 +462,14 @@ int wire_size(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, const
         return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: too many slices or chunks");
     std::vector<uint64_t> cbase, sb;
     uint64_t* d_plan = nullptr;
-    int rc = wire_sizes(ctx, d_codes, d_counts, sstart, sn, S, cbase, &d_plan, sb, s);
+    int rc = wire_sizes(ctx, d_codes, d_counts, sstart, sn, S, cbase, &d_plan, sb, false, s);
     if (rc) return rc;
     for (int i = 0; i < S; ++i) {
         const uint64_t nch = cbase[i + 1] - cbase[i];
-        if ((sb[i] - nch * kWRec) / 4u >= 0xFFFFFFFFull)
+        if ((sb[i] - nch * kWRec) / 4u >= 0xFFFFFFFFull) {
+            ctx->wire_valid = false;
             return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: 2^32 or more escape words in one slice");
+        }
         slice_bytes[i] = sb[i];
     }
     return KMH_OK;
@@ -474,12 +479,13 @@ int wire_encode(Ctx* ctx, const uint64_t* d_codes, const uint32_t* d_counts, con
                 int S, uint8_t* d_out, uint64_t out_bytes, hipStream_t s) {
     if (S < 0 || (S && (!sstart || !sn))) return fail(ctx, KMH_ERR_INVALID, "bad wire arguments");
     if (!S) return KMH_OK;
-    std::vector<uint64_t> sb((size_t)S);
-    int rc = wire_size(ctx, d_codes, d_counts, sstart, sn, S, sb.data(), s);   // (cached if just sized)
-    if (rc) return rc;
-    std::vector<uint64_t> cbase, h((size_t)S);
+    std::vector<uint64_t> sb((size_t)S), cbase, h((size_t)S);
     uint64_t* d_plan = nullptr;
-    if ((rc = wire_sizes(ctx, d_codes, d_counts, sstart, sn, S, cbase, &d_plan, sb, s))) return rc;
+    int rc = wire_sizes(ctx, d_codes, d_counts, sstart, sn, S, cbase, &d_plan, sb, true, s);   // (the size call's)
+    if (rc) return rc;
+    for (int i = 0; i < S; ++i)
+        if ((sb[i] - (cbase[i + 1] - cbase[i]) * kWRec) / 4u >= 0xFFFFFFFFull)
+            return fail(ctx, KMH_ERR_UNSUPPORTED, "wire: 2^32 or more escape words in one slice");
     uint64_t total = 0;
     for (int i = 0; i < S; ++i) {
         h[i] = total;
