@@ -161,12 +161,18 @@ __global__ __launch_bounds__(kWThreads) void k_wire_count(const uint64_t* __rest
     const uint32_t tid = threadIdx.x;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
-        uint64_t code[kWPer], gap[kWPer];
-        uint32_t cnt[kWPer];
-        load4(codes, counts, ch, tid, code, gap, cnt);
+        // (entries j * 256 + tid: every load instruction reads 512 contiguous bytes; the flags do
+        // not depend on which thread holds an entry -- 7.9 vs 11.5 ms at N = 8 with 4 consecutive
+        // entries per thread, whose loads stride 32 bytes)
         uint64_t f = 0ull;
 #pragma unroll
-        for (int j = 0; j < kWPer; ++j) f += flag_bits(gap[j], cnt[j], kWPer * tid + j < ch.n);
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            const bool v = i < ch.n;
+            const uint64_t code = v ? codes[ch.base + i] : 0ull;
+            const uint64_t prev = v && i ? codes[ch.base + i - 1u] : code;
+            f += flag_bits(code - prev, v ? counts[ch.base + i] : 1u, v);
+        }
         bool wide;
         const uint32_t t = chunk_words(block_sum64(f, ws), &wide);
         if (tid == 0) esc[c] = t;
