@@ -130,26 +130,6 @@ __device__ __forceinline__ Chunk chunk_at(const uint64_t* __restrict__ sstart, c
     return k;
 }
 
-// A thread's 4 consecutive entries i = 4 tid + j of a chunk: codes, gaps (code - previous code; 0 for
-// the chunk's first entry and past its end) and counts (1 past the end).
-__device__ __forceinline__ void load4(const uint64_t* __restrict__ codes, const uint32_t* __restrict__ counts,
-                                      const Chunk& ch, uint32_t tid, uint64_t (&code)[kWPer], uint64_t (&gap)[kWPer],
-                                      uint32_t (&cnt)[kWPer]) {
-    const uint32_t i0 = kWPer * tid;
-#pragma unroll
-    for (int j = 0; j < kWPer; ++j) {
-        const bool v = i0 + j < ch.n;
-        code[j] = v ? codes[ch.base + i0 + j] : 0ull;
-        cnt[j] = v ? counts[ch.base + i0 + j] : 1u;
-    }
-    const uint64_t p0 = (i0 && i0 < ch.n) ? codes[ch.base + i0 - 1u] : code[0];
-#pragma unroll
-    for (int j = 0; j < kWPer; ++j) {
-        const bool v = i0 + j < ch.n;
-        gap[j] = v ? code[j] - (j ? code[j - 1] : p0) : 0ull;
-    }
-}
-
 // Escape words of every chunk.
 __global__ __launch_bounds__(kWThreads) void k_wire_count(const uint64_t* __restrict__ codes,
                                                           const uint32_t* __restrict__ counts,
@@ -219,6 +199,8 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
                                                          const uint64_t* __restrict__ sboff, uint8_t* __restrict__ out) {
     __shared__ uint64_t ws64[kWThreads / 64];
     __shared__ uint32_t ws[kWThreads / 64];
+    __shared__ uint64_t scode[kWChunk];
+    __shared__ uint32_t scnt[kWChunk];
     const uint32_t tid = threadIdx.x;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
@@ -226,14 +208,34 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
         uint8_t* const rec = out + sboff[ch.s] + ch.cl * (uint64_t)kWRec;
         const unsigned long long w0 = esc_off[c] - esc_off[c0];   // the chunk's first escape word in the slice
         uint32_t* const etab = reinterpret_cast<uint32_t*>(out + sboff[ch.s] + (cbase[ch.s + 1] - c0) * (uint64_t)kWRec) + w0;
+        // the chunk into LDS by coalesced loads (entry j * 256 + tid), then 4 consecutive entries per
+        // thread from there (their previous entry too: no second global load)
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            const bool v = i < ch.n;
+            scode[i] = v ? codes[ch.base + i] : 0ull;
+            scnt[i] = v ? counts[ch.base + i] : 1u;
+        }
+        lds_barrier();
         uint64_t code[kWPer], gap[kWPer];
         uint32_t cnt[kWPer];
-        load4(codes, counts, ch, tid, code, gap, cnt);
+        {
+            const uint32_t i0 = kWPer * tid;
+            const uint64_t p0 = (i0 && i0 < ch.n) ? scode[i0 - 1u] : scode[i0];
+#pragma unroll
+            for (int j = 0; j < kWPer; ++j) {
+                const bool v = i0 + j < ch.n;
+                code[j] = scode[i0 + j];
+                cnt[j] = v ? scnt[i0 + j] : 1u;
+                gap[j] = v ? code[j] - (j ? code[j - 1] : p0) : 0ull;
+            }
+        }
         uint64_t f = 0ull;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) f += flag_bits(gap[j], cnt[j], kWPer * tid + j < ch.n);
         bool wide;
-        const uint32_t words = chunk_words(block_sum64(f, ws64), &wide);
+        const uint32_t words = chunk_words(block_sum64(f, ws64), &wide);   // (its barriers also free scode)
         uint32_t nh = 0u, nc = 0u, tw = 0u;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
@@ -287,6 +289,8 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
     __shared__ uint32_t wbuf[kWMaxWords];
     __shared__ uint64_t ws64[kWThreads / 64];
     __shared__ uint32_t ws[kWThreads / 64];
+    __shared__ uint64_t ocode[kWChunk];
+    __shared__ uint32_t ocnt[kWChunk];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, i0 = kWPer * tid;
     for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
         const uint32_t s = slice_of(cbase, S, c);
@@ -344,17 +348,25 @@ __global__ __launch_bounds__(kWThreads) void k_wire_unpack(const uint8_t* __rest
         uint64_t code = anchor + incl - sum;
 #pragma unroll
         for (int w = 0; w < kWThreads / 64; ++w) code += (uint32_t)w < wave ? ws64[w] : 0ull;
-        uint64_t* const oc = out_codes + sdst[s] + cl * kWChunk + i0;
-        uint32_t* const on = out_counts + sdst[s] + cl * kWChunk + i0;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
             code += gap[j];
-            if (i0 + j < n) {
-                oc[j] = code;
-                on[j] = cnt[j];
+            ocode[i0 + j] = code;
+            ocnt[i0 + j] = cnt[j];
+        }
+        lds_barrier();
+        // stored from LDS by entry j * 256 + tid: every store instruction writes contiguous bytes
+        uint64_t* const oc = out_codes + sdst[s] + cl * kWChunk;
+        uint32_t* const on = out_counts + sdst[s] + cl * kWChunk;
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            if (i < n) {
+                oc[i] = ocode[i];
+                on[i] = ocnt[i];
             }
         }
-        lds_barrier();   // wbuf and ws64 are rewritten by the next chunk
+        lds_barrier();   // wbuf, ws64 and the staging are rewritten by the next chunk
     }
 }
 
