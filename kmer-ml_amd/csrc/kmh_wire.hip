@@ -105,6 +105,16 @@ __device__ __forceinline__ uint64_t flag_bits(uint64_t gap, uint32_t cnt, bool v
     return (hi ? 1ull : 0ull) | ((hi >> 32) ? (1ull << 21) : 0ull) | (cnt != 1u ? (1ull << 42) : 0ull);
 }
 
+// Bits 0..15 of x to bits 0, 4, 8, .., 60 (the bitmap words of 16 threads' 4 entries each).
+__device__ __forceinline__ uint64_t spread16(uint64_t x) {
+    x &= 0xFFFFull;
+    x = (x | (x << 24)) & 0x000000FF000000FFull;
+    x = (x | (x << 12)) & 0x000F000F000F000Full;
+    x = (x | (x << 6)) & 0x0303030303030303ull;
+    x = (x | (x << 3)) & 0x1111111111111111ull;
+    return x;
+}
+
 // Escape words of a chunk from its summed flags.
 __device__ __forceinline__ uint32_t chunk_words(uint64_t f, bool* wide) {
     const uint32_t nh = (uint32_t)(f & 0x1FFFFFu), nw = (uint32_t)((f >> 21) & 0x1FFFFFu), nc = (uint32_t)(f >> 42);
@@ -198,7 +208,6 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
                                                          const unsigned long long* __restrict__ esc_off,
                                                          const uint64_t* __restrict__ sboff, uint8_t* __restrict__ out) {
     __shared__ uint64_t ws64[kWThreads / 64];
-    __shared__ uint32_t ws[kWThreads / 64];
     __shared__ uint64_t scode[kWChunk];
     __shared__ uint32_t scnt[kWChunk];
     const uint32_t tid = threadIdx.x;
@@ -231,31 +240,47 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
                 gap[j] = v ? code[j] - (j ? code[j - 1] : p0) : 0ull;
             }
         }
-        uint64_t f = 0ull;
-#pragma unroll
-        for (int j = 0; j < kWPer; ++j) f += flag_bits(gap[j], cnt[j], kWPer * tid + j < ch.n);
-        bool wide;
-        const uint32_t words = chunk_words(block_sum64(f, ws64), &wide);   // (its barriers also free scode)
-        uint32_t nh = 0u, nc = 0u, tw = 0u;
+        // one workgroup scan gives both layouts' word positions and whether the chunk is wide:
+        // (words if narrow | words if wide << 21 | wide gaps << 42) per thread
+        uint32_t nh = 0u, nc = 0u, nw = 0u;
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
-            const bool hf = (gap[j] >> 16) != 0ull, cf = cnt[j] != 1u;
-            nh |= (hf ? 1u : 0u) << j;
-            nc |= (cf ? 1u : 0u) << j;
-            tw += (hf ? (wide ? 2u : 1u) : 0u) + (cf ? 1u : 0u);
+            const uint64_t hi = gap[j] >> 16;
+            nh |= (hi ? 1u : 0u) << j;
+            nc |= (cnt[j] != 1u ? 1u : 0u) << j;
+            nw += (hi >> 32) ? 1u : 0u;
         }
-        uint32_t tot;
-        uint32_t pos = block_excl(tw, ws, &tot);
+        const uint32_t ph = (uint32_t)__builtin_popcount(nh), pc = (uint32_t)__builtin_popcount(nc);
+        const uint64_t mine = (uint64_t)(ph + pc) | (uint64_t)(2u * ph + pc) << 21 | (uint64_t)nw << 42;
+        const uint32_t lane = tid & 63u, wave = tid >> 6;
+        const uint64_t incl = wave_incl_u64(mine);
+        if (lane == 63u) ws64[wave] = incl;
+        const uint64_t hb[4] = {__ballot(nh & 1u), __ballot(nh & 2u), __ballot(nh & 4u), __ballot(nh & 8u)};
+        const uint64_t cb[4] = {__ballot(nc & 1u), __ballot(nc & 2u), __ballot(nc & 4u), __ballot(nc & 8u)};
+        lds_barrier();   // (also frees scode for the next chunk)
+        uint64_t pre = incl - mine, tot = 0ull;
+#pragma unroll
+        for (int w = 0; w < kWThreads / 64; ++w) {
+            pre += (uint32_t)w < wave ? ws64[w] : 0ull;
+            tot += ws64[w];
+        }
+        const bool wide = (tot >> 42) != 0ull;
+        const uint32_t words = wide ? (uint32_t)((tot >> 21) & 0x1FFFFFu) : (uint32_t)(tot & 0x1FFFFFu);
+        uint32_t pos = wide ? (uint32_t)((pre >> 21) & 0x1FFFFFu) : (uint32_t)(pre & 0x1FFFFFu);
         if (tid == 0) {
             *reinterpret_cast<uint64_t*>(rec) = code[0];
             *reinterpret_cast<uint2*>(rec + 8) = make_uint2((uint32_t)w0, words | (wide ? 0x80000000u : 0u));
         }
         *reinterpret_cast<uint64_t*>(rec + kWHead + 8u * tid) =
             (gap[0] & 0xFFFFull) | (gap[1] & 0xFFFFull) << 16 | (gap[2] & 0xFFFFull) << 32 | (gap[3] & 0xFFFFull) << 48;
-        const uint32_t nh1 = __shfl_down(nh, 1), nc1 = __shfl_down(nc, 1);
-        if ((tid & 1u) == 0u) {
-            rec[kWHi + tid / 2u] = (uint8_t)(nh | nh1 << 4);
-            rec[kWCnt + tid / 2u] = (uint8_t)(nc | nc1 << 4);
+        if (lane < 4u) {   // the wave's 256 bits of each bitmap: entry 4 t + j is ballot j's bit t
+            const uint32_t sh = 16u * lane;
+            const uint64_t h = spread16(hb[0] >> sh) | spread16(hb[1] >> sh) << 1 | spread16(hb[2] >> sh) << 2 |
+                               spread16(hb[3] >> sh) << 3;
+            const uint64_t q = spread16(cb[0] >> sh) | spread16(cb[1] >> sh) << 1 | spread16(cb[2] >> sh) << 2 |
+                               spread16(cb[3] >> sh) << 3;
+            *reinterpret_cast<uint64_t*>(rec + kWHi + wave * 32u + 8u * lane) = h;
+            *reinterpret_cast<uint64_t*>(rec + kWCnt + wave * 32u + 8u * lane) = q;
         }
 #pragma unroll
         for (int j = 0; j < kWPer; ++j) {
