@@ -211,21 +211,40 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
     __shared__ uint64_t scode[kWChunk];
     __shared__ uint32_t scnt[kWChunk];
     const uint32_t tid = threadIdx.x;
-    for (uint64_t c = blockIdx.x; c < NC; c += gridDim.x) {
-        const Chunk ch = chunk_at(sstart, sn, cbase, S, c);
+    // the chunk's entries by coalesced loads (entry j * 256 + tid), software-pipelined: the next
+    // chunk's loads are issued before this chunk's work, then staged in LDS for 4 consecutive
+    // entries per thread (their previous entry too: no second global load)
+    uint64_t lc[kWPer];
+    uint32_t ln[kWPer];
+    auto load_chunk = [&](const Chunk& k) {
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            const uint32_t i = (uint32_t)j * kWThreads + tid;
+            const bool v = i < k.n;
+            lc[j] = v ? codes[k.base + i] : 0ull;
+            ln[j] = v ? counts[k.base + i] : 1u;
+        }
+    };
+    uint64_t c = blockIdx.x;
+    if (c >= NC) return;
+    Chunk ch = chunk_at(sstart, sn, cbase, S, c);
+    load_chunk(ch);
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j < kWPer; ++j) {
+            scode[(uint32_t)j * kWThreads + tid] = lc[j];
+            scnt[(uint32_t)j * kWThreads + tid] = ln[j];
+        }
+        const uint64_t c2 = c + gridDim.x;
+        Chunk ch2 = ch;
+        if (c2 < NC) {
+            ch2 = chunk_at(sstart, sn, cbase, S, c2);
+            load_chunk(ch2);
+        }
         const uint64_t c0 = cbase[ch.s];
         uint8_t* const rec = out + sboff[ch.s] + ch.cl * (uint64_t)kWRec;
         const unsigned long long w0 = esc_off[c] - esc_off[c0];   // the chunk's first escape word in the slice
         uint32_t* const etab = reinterpret_cast<uint32_t*>(out + sboff[ch.s] + (cbase[ch.s + 1] - c0) * (uint64_t)kWRec) + w0;
-        // the chunk into LDS by coalesced loads (entry j * 256 + tid), then 4 consecutive entries per
-        // thread from there (their previous entry too: no second global load)
-#pragma unroll
-        for (int j = 0; j < kWPer; ++j) {
-            const uint32_t i = (uint32_t)j * kWThreads + tid;
-            const bool v = i < ch.n;
-            scode[i] = v ? codes[ch.base + i] : 0ull;
-            scnt[i] = v ? counts[ch.base + i] : 1u;
-        }
         lds_barrier();
         uint64_t code[kWPer], gap[kWPer];
         uint32_t cnt[kWPer];
@@ -295,6 +314,9 @@ __global__ __launch_bounds__(kWThreads) void k_wire_pack(const uint64_t* __restr
             const unsigned long long sw = esc_off[c + 1u] - esc_off[c0];
             if (tid < ((4u - (uint32_t)(sw & 3u)) & 3u)) etab[sw - w0 + tid] = 0u;
         }
+        if (c2 >= NC) break;
+        c = c2;
+        ch = ch2;
     }
 }
 
