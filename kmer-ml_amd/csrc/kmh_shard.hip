@@ -6,18 +6,20 @@
 // the sorted union of their codes (`columns`) and, for every row entry, its column index
 // (`indices`): with the rows' offsets as indptr and their counts as values, the shard's CSR.
 //
-// The code range is cut into units of ~kShTarget entries (all rows together), sized by the
+// The code range is cut into units of ~3/4 CAP entries (all rows together), sized by the
 // entries' density: a coarse grid of 2^16 power-of-two cells (k_shard_coarse: every row's start
-// in every cell, by binary search), each cell cut into ceil(entries / kShTarget) equal code spans
+// in every cell, by binary search), each cell cut into ceil(entries / target) equal code spans
 // (k_shard_cells, k_shard_units: the units' first and end codes), and every row's start in every
-// unit by a binary search inside its cell (k_shard_ustarts).  Then a persistent grid (two
-// workgroups per CU) takes the units in turn: a workgroup gathers a unit's row pieces into
-// registers, sorts them in LDS by a counting sort on 12 bits of the code (~0.75 entries per bin),
-// puts each bin in order by rank, and equal codes are then adjacent: run heads are the union.
-// k_shard_union runs twice -- the union's size per unit, then (after a scan) the columns and the
-// indices -- so no entry moves through memory other than its code being read.  A unit that overflows the LDS (more than kShCap entries, or a bin of more
-// than kShBin: codes shared by many organisms, low-complexity data) is left to an exact
-// fallback: its entries are gathered, radix-sorted (kmh_sort.hip) and written the same way.
+// unit by a search inside its cell (k_shard_ustarts: an interpolated guess, then galloping).  Then
+// a persistent grid (two or four workgroups per CU, by shape) takes the units in turn: a workgroup
+// gathers a unit's row pieces into registers, sorts them in LDS by a counting sort on 11-12 bits
+// of the code (~0.75 entries per bin), puts each bin in order by rank, and equal codes are then
+// adjacent: run heads are the union.  k_shard_union runs twice -- the union's size per unit (with
+// u32 code offsets: inserts into an LDS hash set, no sort), then (after a scan) the columns and
+// the indices -- so no entry moves through memory other than its code being read.  A unit that
+// overflows the LDS (more than CAP entries, or a bin of more than kShBin: codes shared by many
+// organisms, low-complexity data) is left to an exact fallback: its entries are gathered,
+// radix-sorted (kmh_sort.hip) and written the same way.
 // (Round 5: until then the units were uniform code spans of ~2048 entries on average and their
 // starts came from a pass over every code; the workgroups were latency-bound per unit, and a
 // uniform span must stay small enough for the densest part of the range.)
@@ -29,16 +31,17 @@
 namespace kmh {
 namespace {
 
-constexpr int kShThreads = 512;     // two union workgroups per CU (~58 KiB of LDS each for up to ~500 rows)
 constexpr int kShScanThreads = 1024;
-constexpr int kShCap = 4096;        // entries of one unit in LDS
-constexpr int kShBinBits = 12;
-constexpr int kShBins = 1 << kShBinBits;
 constexpr int kShBin = 64;          // entries of one bin sorted in place (more: fallback)
 constexpr int kShMaxRows = 4096;    // organisms of one shard (LDS piece table)
 constexpr int kShRoffCache = 1024;  // row offsets kept in LDS
-constexpr int kShTarget = 3072;     // entries per unit (units of one coarse cell share its entries)
 constexpr int kShCoarseBits = 16;   // coarse cells: at most 2^16
+// Two union shapes (k_shard_union<NT, CAP, ..>): units of up to CAP entries in LDS, ~3/4 CAP on
+// average.  Up to kShSmallRows rows, 256 threads and CAP 2048 (four workgroups per CU, ~29 KiB of
+// LDS each): a unit's barriers span 4 waves, not 8 (config 5 at N = 1, 16 rows: union passes
+// 59.5 -> 55.4 ms); with more rows a unit's row pieces would shrink to a few entries each, so 512
+// threads and CAP 4096 (two workgroups per CU, ~58 KiB of LDS each for up to ~500 rows).
+constexpr int kShSmallRows = 32;
 constexpr int kShSlotRows = 256;    // up to this many rows, an entry's row comes from the 64-entry slot
                                     // table (a u8 row per slot, then a few steps over row starts); beyond,
                                     // by binary search (R = 128, config 5's shard at N = 8: 3 vs 7 LDS
@@ -54,6 +57,49 @@ __device__ __forceinline__ uint32_t lower_in(const uint64_t* __restrict__ row, u
     return a;
 }
 
+// lower_in for a row piece [a, b) whose codes lie in [c0, c0 + w1]: starts at the entry where c
+// would sit if the piece's codes were spread evenly over that span and gallops from there (the
+// unit starts of k_shard_ustarts: sorted k-mer codes are close to uniform inside a coarse cell, so
+// the guess is a few entries off -- one or two cache lines, where a binary search over a piece of
+// ~500 entries touched ~6)
+__device__ __forceinline__ uint32_t lower_guess(const uint64_t* __restrict__ row, uint32_t a, uint32_t b, uint64_t c,
+                                                uint64_t c0, uint64_t w1) {
+    if (a >= b) return a;
+    const uint32_t n = b - a;
+    const double f = (double)(c - c0) / ((double)w1 + 1.0);   // in [0, 1)
+    const uint32_t g = a + min(n - 1u, (uint32_t)(f * (double)n));
+    uint32_t lo, hi;   // the answer lies in [lo, hi]
+    uint32_t step = 1u;
+    if (row[g] < c) {
+        lo = g + 1u;
+        hi = b;
+        while (lo + step - 1u < b) {
+            const uint32_t p = lo + step - 1u;
+            if (row[p] < c) {
+                lo = p + 1u;
+                step <<= 1;
+            } else {
+                hi = p;
+                break;
+            }
+        }
+    } else {
+        lo = a;
+        hi = g;
+        while (hi - a >= step) {
+            const uint32_t p = hi - step;
+            if (row[p] >= c) {
+                hi = p;
+                step <<= 1;
+            } else {
+                lo = p + 1u;
+                break;
+            }
+        }
+    }
+    return lower_in(row, lo, hi, c);
+}
+
 // cs[r * (Q + 1) + q] = the first entry of row r (relative to the row) whose code is >= the
 // start of coarse cell q, lo + q 2^CSH (q = Q: the row's length).  One thread per (q, r).
 __global__ __launch_bounds__(256) void k_shard_coarse(const uint64_t* __restrict__ codes,
@@ -67,18 +113,19 @@ __global__ __launch_bounds__(256) void k_shard_coarse(const uint64_t* __restrict
     cs[x] = q == Q ? n : lower_in(codes + a, 0u, n, lo + ((uint64_t)q << CSH));
 }
 
-// Units of coarse cell q: nu[q] = ceil(its entries (all rows) / kShTarget).
+// Units of coarse cell q: nu[q] = ceil(its entries (all rows) / target).
 __global__ __launch_bounds__(256) void k_shard_cells(const uint32_t* __restrict__ cs, int R, uint32_t Q,
-                                                     uint64_t lo, uint64_t hi_incl, int CSH,
+                                                     uint64_t lo, uint64_t hi_incl, int CSH, uint32_t target,
                                                      uint32_t* __restrict__ nu) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= Q) return;
     uint64_t e = 0;
     for (int r = 0; r < R; ++r) e += cs[(uint64_t)r * (Q + 1u) + q + 1u] - cs[(uint64_t)r * (Q + 1u) + q];
-    // at most one unit per code (a unit of one code holds <= R <= kShCap entries)
+    // at most one unit per code (a unit of one code holds R entries at most: past the union's
+    // LDS it goes to the fallback)
     const uint64_t c0 = lo + ((uint64_t)q << CSH);
     const uint64_t w1 = (q + 1u == Q ? hi_incl : c0 + ((1ull << CSH) - 1u)) - c0;   // width - 1
-    const uint64_t n = (e + kShTarget - 1) / kShTarget;
+    const uint64_t n = (e + target - 1) / target;
     nu[q] = (uint32_t)(n == 0u ? 0u : (n - 1u > w1 ? w1 + 1u : n));
 }
 
@@ -118,6 +165,7 @@ constexpr int kUsU = 64, kUsR = 64;
 __global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restrict__ codes,
                                                        const uint64_t* __restrict__ roff, int R,
                                                        const uint32_t* __restrict__ cs, uint32_t Q,
+                                                       uint64_t lo, uint64_t hi_incl, int CSH,
                                                        const uint64_t* __restrict__ ub,
                                                        const uint32_t* __restrict__ ucell, uint32_t U,
                                                        uint32_t* __restrict__ st) {
@@ -126,10 +174,10 @@ __global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restric
     const uint32_t nu = min((uint32_t)kUsU, U + 1u - u0);
     for (int r0 = 0; r0 < R; r0 += kUsR) {
         const int nr = min(kUsR, R - r0);
-        for (int idx = threadIdx.x; idx < kUsU * kUsR; idx += 256) {
+        for (int idx = threadIdx.x; idx < kUsU * nr; idx += 256) {   // (only the chunk's rows: R = 16 uses 16 of 64)
             const uint32_t uu = (uint32_t)(idx % kUsU);
             const int rr = idx / kUsU;
-            if (uu < nu && rr < nr) {
+            if (uu < nu) {
                 const uint32_t u = u0 + uu;
                 const int r = r0 + rr;
                 const uint64_t a = roff[r];
@@ -139,16 +187,18 @@ __global__ __launch_bounds__(256) void k_shard_ustarts(const uint64_t* __restric
                 } else {
                     const uint32_t q = ucell[u];
                     const uint32_t* c = cs + (uint64_t)r * (Q + 1u);
-                    v = lower_in(codes + a, c[q], c[q + 1u], ub[u]);
+                    const uint64_t c0 = lo + ((uint64_t)q << CSH);
+                    const uint64_t w1 = (q + 1u == Q ? hi_incl : c0 + ((1ull << CSH) - 1u)) - c0;
+                    v = lower_guess(codes + a, c[q], c[q + 1u], ub[u], c0, w1);
                 }
                 tile[uu][rr] = v;
             }
         }
         __syncthreads();
-        for (int idx = threadIdx.x; idx < kUsU * kUsR; idx += 256) {
-            const int rr = idx % kUsR;
-            const uint32_t uu = (uint32_t)(idx / kUsR);
-            if (uu < nu && rr < nr) st[(uint64_t)(u0 + uu) * (uint64_t)R + (uint64_t)(r0 + rr)] = tile[uu][rr];
+        for (int idx = threadIdx.x; idx < (int)nu * nr; idx += 256) {
+            const int rr = idx % nr;
+            const uint32_t uu = (uint32_t)(idx / nr);
+            st[(uint64_t)(u0 + uu) * (uint64_t)R + (uint64_t)(r0 + rr)] = tile[uu][rr];
         }
         __syncthreads();
     }
@@ -165,13 +215,14 @@ __device__ __forceinline__ uint32_t unit_of(const uint64_t* __restrict__ ub, uin
     return a;
 }
 
-// Block-wide exclusive scan of one u32 per thread (kShThreads); returns the thread's prefix,
-// *total = the sum.  ws: kShThreads / 64 words of LDS.
+// Block-wide exclusive scan of one u32 per thread (NT); returns the thread's prefix,
+// *total = the sum.  ws: NT / 64 words of LDS.
 //
 // Every barrier of the union is lds_barrier() (kmh_device.h): the kernel never reads back what it
 // stores, and __syncthreads() -- a workgroup release, s_waitcnt vmcnt(0) -- made each of a unit's
 // ~10 barriers wait for the stores of the previous unit and for the loads prefetched for the next
 // one (round 6: the software pipelining over units only works with LDS-only barriers).
+template <int NT>
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t incl = scan64(v);
@@ -179,7 +230,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
     lds_barrier();
     uint32_t pre = 0u, tot = 0u;
 #pragma unroll
-    for (int w = 0; w < kShThreads / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
         const uint32_t x = ws[w];
         pre += w < wave ? x : 0u;
         tot += x;
@@ -197,8 +248,8 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
 // pieces are scanned (into the other of two LDS tables) and its codes loaded right after this
 // unit's scatter, so they land during this unit's sort, heads and stores (one unit at a time per
 // workgroup waited for two global round trips per unit: latency-bound).
-template <bool WRITE, typename K, typename IX>
-__global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_shard_union(const uint64_t* __restrict__ codes,
+template <int NT, int CAP, bool WRITE, typename K, typename IX>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
                                                             const uint32_t* __restrict__ st, uint32_t S,
                                                             const uint64_t* __restrict__ ub,
@@ -207,11 +258,19 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                                                             const unsigned long long* __restrict__ colbase,
                                                             uint64_t* __restrict__ columns,
                                                             IX* __restrict__ indices) {
+    // NT threads, units of up to CAP entries in LDS, CAP bins of a unit's codes (kBB bits), and
+    // the sizes pass's hash set of 2 CAP slots
+    constexpr int kBB = CAP == 2048 ? 11 : 12, kHB = kBB + 1, kHS = 1 << kHB;
+    static_assert((1 << kBB) == CAP, "CAP is 2048 or 4096");
+    // sizes pass with u32 offsets: the union's size by LDS hash-set inserts, no sort (HASH)
+    constexpr bool HASH = !WRITE && sizeof(K) == 4;
     // the unit's codes as offsets from its first code: u32 whenever every unit spans < 2^32 codes
-    __shared__ __attribute__((aligned(16))) K scode[kShCap];
-    __shared__ __attribute__((aligned(16))) uint16_t sidx[kShCap];
-    __shared__ uint32_t hist[kShBins];
-    __shared__ uint32_t colrel[WRITE ? kShCap : 1];   // WRITE: column of gathered entry i - the unit's first
+    __shared__ __attribute__((aligned(16))) K scode[HASH ? 1 : CAP];
+    __shared__ __attribute__((aligned(16))) uint16_t sidx[HASH ? 1 : CAP];
+    __shared__ __attribute__((aligned(16))) uint32_t htab[HASH ? kHS : 1];   // HASH: offset + 1, 0 = empty
+    __shared__ uint32_t htop;   // HASH: the offset 2^32 - 1 (no room for + 1) occurs
+    __shared__ uint32_t hist[CAP];
+    __shared__ uint32_t colrel[WRITE ? CAP : 1];   // WRITE: column of gathered entry i - the unit's first
     // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), and two
     // piece tables (this unit's, the next unit's): the pieces' exclusive prefix of their sizes
     // (R + 1) and their first entries (relative to their rows)
@@ -226,14 +285,14 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     uint64_t* const dtab = reinterpret_cast<uint64_t*>(
         reinterpret_cast<char*>(ptab) + ((2u * (2u * (uint32_t)R + 1u)) * 4u + 15u) / 16u * 16u);
     auto dl_of = [&](int k) { return dtab + (uint32_t)k * (uint32_t)R; };
-    __shared__ uint32_t ws[kShThreads / 64];
+    __shared__ uint32_t ws[NT / 64];
     __shared__ uint32_t flag;
     // up to kShSlotRows rows: the row holding gathered entry 64 m of piece table k (rtab[k][m])
-    __shared__ uint8_t rtab[2][kShCap / 64];
-    constexpr int PER = kShCap / kShThreads;   // entries per thread
-    constexpr int BPT = kShBins / kShThreads;  // bins per thread
+    __shared__ uint8_t rtab[2][CAP / 64];
+    constexpr int PER = CAP / NT;   // entries per thread
+    constexpr int BPT = CAP / NT;  // bins per thread
     const int tid = threadIdx.x;
-    for (int r = tid; r < R && r < kShRoffCache; r += kShThreads) sroff[r] = roff[r];
+    for (int r = tid; r < R && r < kShRoffCache; r += NT) sroff[r] = roff[r];
     // (made visible by the first barriers)
     auto row_base = [&](int r) { return r < kShRoffCache ? sroff[r] : roff[r]; };
 
@@ -263,7 +322,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         }
     };
     // next unit's row starts: prefetched into registers when there is one row per thread
-    const bool pipe_st = R <= kShThreads;   // (uniform)
+    const bool pipe_st = R <= NT;   // (uniform)
     uint32_t sta = 0u, stb = 0u;
     auto issue_st = [&](uint32_t u) {
         if (pipe_st && tid < R) {
@@ -276,9 +335,9 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
     auto build = [&](uint32_t u, int k) -> uint32_t {
         uint32_t* const pfx = pfx_of(k);
         uint32_t* const pa = pa_of(k);
-        // (R > kShThreads: a contiguous run of rows per thread, so that the block scan of the
+        // (R > NT: a contiguous run of rows per thread, so that the block scan of the
         // threads' sums is the rows' prefix in row order)
-        const int rq = (R + kShThreads - 1) / kShThreads, r0 = min(R, tid * rq), r1 = min(R, r0 + rq);
+        const int rq = (R + NT - 1) / NT, r0 = min(R, tid * rq), r1 = min(R, r0 + rq);
         uint32_t mine = 0u;
         if (pipe_st) {
             if (tid < R) {
@@ -293,7 +352,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
         uint32_t T;
-        uint32_t pre = block_scan(mine, ws, &T);
+        uint32_t pre = block_scan<NT>(mine, ws, &T);
         if (pipe_st) {
             if (tid < R) pfx[tid] = pre;
         } else {
@@ -306,13 +365,13 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         if (tid == 0) pfx[R] = T;
         if (R <= kShSlotRows && tid < R) dl_of(k)[tid] = row_base(tid) + pa[tid] - pre;   // (pipe_st: one row per thread)
         if (R <= kShSlotRows && tid < R && mine) {   // (one row per thread) the 64-entry slots starting in this row
-            // (a unit over kShCap entries is not gathered: its slots past the table are skipped)
-            for (uint32_t m = (pre + 63u) >> 6; (m << 6) < pre + mine && m < (uint32_t)(kShCap / 64); ++m)
+            // (a unit over CAP entries is not gathered: its slots past the table are skipped)
+            for (uint32_t m = (pre + 63u) >> 6; (m << 6) < pre + mine && m < (uint32_t)(CAP / 64); ++m)
                 rtab[k][m] = (uint8_t)tid;
         }
         return T;
     };
-    // the codes of a unit of T (1 .. kShCap) entries, table k (visible), all loads in flight;
+    // the codes of a unit of T (1 .. CAP) entries, table k (visible), all loads in flight;
     // WRITE with up to kShSlotRows rows: the entries' rows packed a byte each into rk, for the index stores
     auto gather = [&](uint32_t T, int k, uint64_t (&cv)[PER], uint32_t (&rk)[2]) {
         const uint32_t* const pfx = pfx_of(k);
@@ -321,7 +380,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         int rv[PER];
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const uint32_t i = (uint32_t)(u * kShThreads + tid);
+            const uint32_t i = (uint32_t)(u * NT + tid);
             iv[u] = i < T ? i : T - 1u;
         }
         rows_of(pfx, rtab[k], iv, rv);
@@ -351,7 +410,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
     for (int u = 0; u < PER; ++u) cv[u] = 0ull;
     uint32_t rk[2] = {0u, 0u}, rk2[2] = {0u, 0u};   // (this unit's rows, the next unit's)
-    if (Tc >= 1u && Tc <= (uint32_t)kShCap) gather(Tc, 0, cv, rk);
+    if (Tc >= 1u && Tc <= (uint32_t)CAP) gather(Tc, 0, cv, rk);
     unsigned long long cb = WRITE ? colbase[s] : 0ull;
     int k = 0;
     for (;;) {
@@ -359,34 +418,74 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         const bool has2 = s2 < S;   // (uniform)
         if (has2) issue_st(s2);
         const unsigned long long cb2 = WRITE && has2 ? colbase[s2] : 0ull;
-        for (int q = 0; q < BPT; ++q) hist[q * kShThreads + tid] = 0u;
-        if (tid == 0) flag = 0u;
+        for (int q = 0; q < BPT; ++q) hist[q * NT + tid] = 0u;
+        if constexpr (HASH) {
+            uint4* const h4 = reinterpret_cast<uint4*>(htab);
+#pragma unroll
+            for (int q = 0; q < kHS / 4 / NT; ++q) h4[q * NT + tid] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (tid == 0) {
+            flag = 0u;
+            htop = 0u;
+        }
         lds_barrier();
         const uint32_t T = Tc;
-        const bool ok = T >= 1u && T <= (uint32_t)kShCap;   // (uniform)
+        const bool ok = T >= 1u && T <= (uint32_t)CAP;   // (uniform)
         if (!ok && !WRITE && tid == 0) {   // empty (a part of a coarse cell with no entries) or too big
             ucount[s] = 0u;
-            if (T > (uint32_t)kShCap) big[1 + atomicAdd(big, 1u)] = s;
+            if (T > (uint32_t)CAP) big[1 + atomicAdd(big, 1u)] = s;
         }
         bool sorted_ok = false;
         uint64_t base = 0ull;
         int bsh = 0;
+        uint32_t nf = 0u;   // HASH: this thread's first occurrences
         if (ok) {
             // 2. bins: 12 bits over the unit's span, counted
             base = ub[s];
             const uint64_t span1 = ue[s] - base;   // span - 1
             const int sbits = span1 ? 64 - __builtin_clzll(span1) : 0;
-            bsh = sbits > kShBinBits ? sbits - kShBinBits : 0;
+            bsh = sbits > kBB ? sbits - kBB : 0;
             uint32_t bv[PER];
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
-                const uint32_t i = (uint32_t)(u * kShThreads + tid);
-                bv[u] = (uint32_t)min((K)(cv[u] - base) >> bsh, (K)(kShBins - 1));
+                const uint32_t i = (uint32_t)(u * NT + tid);
+                bv[u] = (uint32_t)min((K)(cv[u] - base) >> bsh, (K)(CAP - 1));
                 if (i < T) atomicAdd(&hist[bv[u]], 1u);
+            }
+            if constexpr (HASH) {
+                // the union's size: inserts into an LDS hash set (linear probing, load <= 1/2); an
+                // entry counts iff its insert finds an empty slot -- no scan, scatter or sort
+#pragma unroll
+                for (int u = 0; u < PER; ++u) {
+                    const uint32_t i = (uint32_t)(u * NT + tid);
+                    if (i < T) {
+                        const uint32_t off = (uint32_t)(cv[u] - base);
+                        if (off == 0xFFFFFFFFu) {
+                            htop = 1u;
+                        } else {
+                            const uint32_t key = off + 1u;
+                            uint32_t h = (key * 0x9E3779B1u) >> (32 - kHB);
+                            for (;;) {
+                                const uint32_t old = atomicCAS(&htab[h], 0u, key);
+                                if (old == 0u) {
+                                    ++nf;
+                                    break;
+                                }
+                                if (old == key) break;
+                                h = (h + 1u) & (uint32_t)(kHS - 1);
+                            }
+                        }
+                    }
+                }
             }
             lds_barrier();
             // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
-            {
+            //    (HASH: only the check -- the write pass's sort holds the same bins)
+            if constexpr (HASH) {
+#pragma unroll
+                for (int q = 0; q < BPT; ++q)
+                    if (hist[BPT * tid + q] > (uint32_t)kShBin) flag = 1u;
+            } else {
                 uint32_t v[BPT], sum = 0u;
 #pragma unroll
                 for (int q = 0; q < BPT; ++q) {
@@ -395,7 +494,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     if (v[q] > (uint32_t)kShBin) flag = 1u;
                 }
                 uint32_t tot;
-                uint32_t o = block_scan(sum, ws, &tot);
+                uint32_t o = block_scan<NT>(sum, ws, &tot);
 #pragma unroll
                 for (int q = 0; q < BPT; ++q) {
                     hist[BPT * tid + q] = o * 0x10001u;
@@ -408,11 +507,11 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 ucount[s] = 0u;
                 big[1 + atomicAdd(big, 1u)] = s;
             }
-            if (sorted_ok) {
+            if (!HASH && sorted_ok) {
                 // 4. scatter by bin (hist ends as start | end << 16)
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                    const uint32_t i = (uint32_t)(u * NT + tid);
                     if (i < T) {
                         const uint32_t at = atomicAdd(&hist[bv[u]], 0x10000u) >> 16;
                         scode[at] = (K)(cv[u] - base);
@@ -426,16 +525,21 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
         uint32_t T2 = 0u;
         if (has2) T2 = build(s2, k ^ 1);   // (its barriers also order the scatter before the sort)
         lds_barrier();
-        if (has2 && T2 >= 1u && T2 <= (uint32_t)kShCap) gather(T2, k ^ 1, cv, rk2);
-        if (!WRITE && sorted_ok) {
+        if (has2 && T2 >= 1u && T2 <= (uint32_t)CAP) gather(T2, k ^ 1, cv, rk2);
+        if (HASH && sorted_ok) {
+            uint32_t U;
+            block_scan<NT>(nf + (tid == 0 ? htop : 0u), ws, &U);
+            if (tid == 0) ucount[s] = U;
+        }
+        if (!HASH && !WRITE && sorted_ok) {
             // the union's size needs no order: position p counts iff no earlier position of its
             // bin holds its code (bins of up to 4 entries: 4 reads clamped into the bin)
             uint32_t nf = 0u;
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
-                const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
+                const uint32_t p = (uint32_t)(u * NT + tid), pc = p < T ? p : 0u;
                 const K key = scode[pc];
-                const uint32_t b = (uint32_t)min(key >> bsh, (K)(kShBins - 1));
+                const uint32_t b = (uint32_t)min(key >> bsh, (K)(CAP - 1));
                 const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
                 bool first = true;
                 if (be - bs <= 4u) {
@@ -451,7 +555,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 nf += (p < T && first) ? 1u : 0u;
             }
             uint32_t U;
-            block_scan(nf, ws, &U);
+            block_scan<NT>(nf, ws, &U);
             if (tid == 0) ucount[s] = U;
         }
         if (WRITE && sorted_ok) {
@@ -470,14 +574,14 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 uint32_t dst[PER];
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
+                    const uint32_t p = (uint32_t)(u * NT + tid), pc = p < T ? p : 0u;
                     key[u] = scode[pc];
                     kix[u] = sidx[pc];
                 }
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    const uint32_t p = (uint32_t)(u * kShThreads + tid), pc = p < T ? p : 0u;
-                    const uint32_t b = (uint32_t)min(key[u] >> bsh, (K)(kShBins - 1));
+                    const uint32_t p = (uint32_t)(u * NT + tid), pc = p < T ? p : 0u;
+                    const uint32_t b = (uint32_t)min(key[u] >> bsh, (K)(CAP - 1));
                     const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
                     uint32_t rk = 0u;
                     if (be - bs <= 4u) {
@@ -535,7 +639,7 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                 nh += (uint32_t)h;
             }
             uint32_t U;
-            const uint32_t hp = block_scan(nh, ws, &U);
+            const uint32_t hp = block_scan<NT>(nh, ws, &U);
             {
                 // the columns from the heads; every entry's column (relative to the unit's
                 // first) into LDS by its gathered index, then stored in gathered order:
@@ -564,14 +668,14 @@ __global__ __launch_bounds__(kShThreads) __attribute__((amdgpu_waves_per_eu(4)))
                     uint32_t iv[PER];
 #pragma unroll
                     for (int u = 0; u < PER; ++u) {
-                        const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                        const uint32_t i = (uint32_t)(u * NT + tid);
                         iv[u] = i < T ? i : 0u;
                     }
                     rows_of(pfx, rtab[k], iv, rv);
                 }
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    const uint32_t i = (uint32_t)(u * kShThreads + tid);
+                    const uint32_t i = (uint32_t)(u * NT + tid);
                     if (i < T) {
                         const uint64_t at = R <= kShSlotRows ? dl_of(k)[rv[u]] + i
                                                              : row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]]);
@@ -761,9 +865,50 @@ int scan_u32_u64(Ctx* ctx, const uint32_t* in, uint32_t n, unsigned long long* o
     return KMH_OK;
 }
 
+// The union's arguments and its two launches (sizes pass, write pass) in one of the two shapes.
+struct UnionArgs {
+    const uint64_t* codes;
+    const uint64_t* roff;
+    int R;
+    const uint32_t* st;
+    uint32_t S;
+    const uint64_t *ub, *ue;
+    uint32_t *ucount, *big;
+    const unsigned long long* colbase;
+    uint64_t* columns;
+    uint32_t* ix32;
+    int64_t* ix64;
+    bool narrow;
+    unsigned grid;
+    size_t dyn;
+};
+template <int NT, int CAP>
+void launch_union(const UnionArgs& a, bool write, hipStream_t s) {
+    const dim3 g(a.grid), b(NT);
+    if (!write) {
+        if (a.narrow)
+            hipLaunchKernelGGL((k_shard_union<NT, CAP, false, uint32_t, uint32_t>), g, b, a.dyn, s, a.codes, a.roff, a.R,
+                               a.st, a.S, a.ub, a.ue, a.ucount, a.big, nullptr, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((k_shard_union<NT, CAP, false, uint64_t, uint32_t>), g, b, a.dyn, s, a.codes, a.roff, a.R,
+                               a.st, a.S, a.ub, a.ue, a.ucount, a.big, nullptr, nullptr, nullptr);
+    } else if (a.narrow && a.ix32) {
+        hipLaunchKernelGGL((k_shard_union<NT, CAP, true, uint32_t, uint32_t>), g, b, a.dyn, s, a.codes, a.roff, a.R, a.st,
+                           a.S, a.ub, a.ue, a.ucount, a.big, a.colbase, a.columns, a.ix32);
+    } else if (a.narrow) {
+        hipLaunchKernelGGL((k_shard_union<NT, CAP, true, uint32_t, int64_t>), g, b, a.dyn, s, a.codes, a.roff, a.R, a.st,
+                           a.S, a.ub, a.ue, a.ucount, a.big, a.colbase, a.columns, a.ix64);
+    } else if (a.ix32) {
+        hipLaunchKernelGGL((k_shard_union<NT, CAP, true, uint64_t, uint32_t>), g, b, a.dyn, s, a.codes, a.roff, a.R, a.st,
+                           a.S, a.ub, a.ue, a.ucount, a.big, a.colbase, a.columns, a.ix32);
+    } else {
+        hipLaunchKernelGGL((k_shard_union<NT, CAP, true, uint64_t, int64_t>), g, b, a.dyn, s, a.codes, a.roff, a.R, a.st,
+                           a.S, a.ub, a.ue, a.ucount, a.big, a.colbase, a.columns, a.ix64);
+    }
+}
+
 int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int R, uint64_t lo,
                 uint64_t hi_incl, uint64_t* d_columns, void* d_indices, bool idx32, uint64_t* ncols, hipStream_t s) {
-    static_assert(kShMaxRows <= kShCap, "a unit of one code fits the LDS");
     if (R < 1 || R > kShMaxRows) return fail(ctx, KMH_ERR_UNSUPPORTED, "a shard holds 1 to 4096 organism rows");
     if (!d_codes || !row_off || !ncols || hi_incl < lo) return fail(ctx, KMH_ERR_INVALID, "bad shard arguments");
     const uint64_t T = row_off[R] - row_off[0];
@@ -802,7 +947,9 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     hipLaunchKernelGGL(k_shard_coarse, dim3((unsigned)((ncs + 255) / 256)), dim3(256), 0, s, codes, d_roff, R, lo, CSH, Q,
                        d_cs);
     KMH_HIP(ctx, hipGetLastError());
-    hipLaunchKernelGGL(k_shard_cells, dim3((Q + 255) / 256), dim3(256), 0, s, d_cs, R, Q, lo, hi_incl, CSH, d_nu);
+    const bool small = R <= kShSmallRows;   // the union's shape
+    const uint32_t target = small ? 1792u : 3584u;
+    hipLaunchKernelGGL(k_shard_cells, dim3((Q + 255) / 256), dim3(256), 0, s, d_cs, R, Q, lo, hi_incl, CSH, target, d_nu);
     KMH_HIP(ctx, hipGetLastError());
     if ((rc = scan_u32_u64(ctx, d_nu, Q, d_ubase, s))) return rc;
     unsigned long long U64 = 0;
@@ -830,22 +977,23 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
                        d_ue, d_ucell);
     KMH_HIP(ctx, hipGetLastError());
     hipLaunchKernelGGL(k_shard_ustarts, dim3((unsigned)(((uint64_t)S + 1 + kUsU - 1) / kUsU)), dim3(256), 0, s, codes, d_roff, R, d_cs, Q,
-                       d_ub, d_ucell, S, d_st);
+                       lo, hi_incl, CSH, d_ub, d_ucell, S, d_st);
     KMH_HIP(ctx, hipGetLastError());
     KMH_HIP(ctx, hipMemsetAsync(d_big, 0, 4, s));
     time_end(ctx, s);
-    const unsigned ug = (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * 2);
+    const unsigned ug = (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * (small ? 4 : 2));
     const size_t dyn = (size_t)std::min(R, kShRoffCache) * 8 + ((2 * ((size_t)2 * R + 1)) * 4 + 15) / 16 * 16 +
                        (R <= kShSlotRows ? (size_t)2 * R * 8 : 0);
-    time_begin(ctx, s, "k_shard_union");
     // every unit lies inside one coarse cell of 2^CSH codes: u32 offsets when CSH <= 32
-    const bool narrow = CSH <= 32;
-    if (narrow)
-        hipLaunchKernelGGL((k_shard_union<false, uint32_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
-                           d_st, S, d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
-    else
-        hipLaunchKernelGGL((k_shard_union<false, uint64_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
-                           d_st, S, d_ub, d_ue, d_ucount, d_big, nullptr, nullptr, nullptr);
+    // (indices at the rows' own offsets: row_off[0] may be past the start of d_indices)
+    UnionArgs ua{codes, d_roff, R, d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns,
+                 idx32 ? static_cast<uint32_t*>(d_indices) + row_off[0] : nullptr,
+                 idx32 ? nullptr : static_cast<int64_t*>(d_indices) + row_off[0], CSH <= 32, ug, dyn};
+    uint32_t* const ix32 = ua.ix32;
+    int64_t* const ix64 = ua.ix64;
+    time_begin(ctx, s, "k_shard_union");
+    if (small) launch_union<256, 2048>(ua, false, s);
+    else launch_union<512, 4096>(ua, false, s);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     uint32_t nbig = 0;
@@ -907,21 +1055,8 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
     time_begin(ctx, s, "k_shard_union");
-    // (indices at the rows' own offsets: row_off[0] may be past the start of d_indices)
-    uint32_t* const ix32 = idx32 ? static_cast<uint32_t*>(d_indices) + row_off[0] : nullptr;
-    int64_t* const ix64 = idx32 ? nullptr : static_cast<int64_t*>(d_indices) + row_off[0];
-    if (narrow && idx32)
-        hipLaunchKernelGGL((k_shard_union<true, uint32_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
-                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix32);
-    else if (narrow)
-        hipLaunchKernelGGL((k_shard_union<true, uint32_t, int64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
-                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix64);
-    else if (idx32)
-        hipLaunchKernelGGL((k_shard_union<true, uint64_t, uint32_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
-                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix32);
-    else
-        hipLaunchKernelGGL((k_shard_union<true, uint64_t, int64_t>), dim3(ug), dim3(kShThreads), dyn, s, codes, d_roff, R,
-                           d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns, ix64);
+    if (small) launch_union<256, 2048>(ua, true, s);
+    else launch_union<512, 4096>(ua, true, s);
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (nbig) {
