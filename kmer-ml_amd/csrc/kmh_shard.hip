@@ -249,7 +249,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
 // unit's scatter, so they land during this unit's sort, heads and stores (one unit at a time per
 // workgroup waited for two global round trips per unit: latency-bound).
 template <int NT, int CAP, bool WRITE, typename K, typename IX>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_shard_union(const uint64_t* __restrict__ codes,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 && sizeof(K) == 4 && !WRITE ? 5 : 4))) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
                                                             const uint32_t* __restrict__ st, uint32_t S,
                                                             const uint64_t* __restrict__ ub,
@@ -879,12 +879,12 @@ struct UnionArgs {
     uint32_t* ix32;
     int64_t* ix64;
     bool narrow;
-    unsigned grid;
+    unsigned grid, grid_sizes;
     size_t dyn;
 };
 template <int NT, int CAP>
 void launch_union(const UnionArgs& a, bool write, hipStream_t s) {
-    const dim3 g(a.grid), b(NT);
+    const dim3 g(write ? a.grid : a.grid_sizes), b(NT);
     if (!write) {
         if (a.narrow)
             hipLaunchKernelGGL((k_shard_union<NT, CAP, false, uint32_t, uint32_t>), g, b, a.dyn, s, a.codes, a.roff, a.R,
@@ -988,7 +988,8 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     // (indices at the rows' own offsets: row_off[0] may be past the start of d_indices)
     UnionArgs ua{codes, d_roff, R, d_st, S, d_ub, d_ue, d_ucount, d_big, d_colbase, d_columns,
                  idx32 ? static_cast<uint32_t*>(d_indices) + row_off[0] : nullptr,
-                 idx32 ? nullptr : static_cast<int64_t*>(d_indices) + row_off[0], CSH <= 32, ug, dyn};
+                 idx32 ? nullptr : static_cast<int64_t*>(d_indices) + row_off[0], CSH <= 32, ug,
+                 (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * (small ? 5 : 2)), dyn};
     uint32_t* const ix32 = ua.ix32;
     int64_t* const ix64 = ua.ix64;
     time_begin(ctx, s, "k_shard_union");
