@@ -24,6 +24,7 @@
 // starts came from a pass over every code; the workgroups were latency-bound per unit, and a
 // uniform span must stay small enough for the densest part of the range.)
 #include <algorithm>
+#include <cstdio>
 #include <vector>
 
 #include "kmh_device.h"
@@ -248,6 +249,14 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* ws, uint32_
 // pieces are scanned (into the other of two LDS tables) and its codes loaded right after this
 // unit's scatter, so they land during this unit's sort, heads and stores (one unit at a time per
 // workgroup waited for two global round trips per unit: latency-bound).
+#ifdef KMH_EXPERIMENTS
+// KMH_EXPERIMENTS builds only: clocks of the union's phases, summed over workgroups (thread 0)
+__device__ unsigned long long g_shard_pt[2][16];
+#define KMH_SPT(i) if (tid == 0) { const unsigned long long t_ = clock64(); pt_[i] += t_ - tl_; tl_ = t_; }
+#else
+#define KMH_SPT(i)
+#endif
+
 template <int NT, int CAP, bool WRITE, typename K, typename IX>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 && sizeof(K) == 4 && !WRITE ? 5 : 4))) void k_shard_union(const uint64_t* __restrict__ codes,
                                                             const uint64_t* __restrict__ roff, int R,
@@ -258,10 +267,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                                                             const unsigned long long* __restrict__ colbase,
                                                             uint64_t* __restrict__ columns,
                                                             IX* __restrict__ indices) {
-    // NT threads, units of up to CAP entries in LDS, CAP bins of a unit's codes (kBB bits), and
-    // the sizes pass's hash set of 2 CAP slots
-    constexpr int kBB = CAP == 2048 ? 11 : 12, kHB = kBB + 1, kHS = 1 << kHB;
-    static_assert((1 << kBB) == CAP, "CAP is 2048 or 4096");
+    // NT threads, units of up to CAP entries in LDS, NB = CAP bins of a unit's codes (kBB bits;
+    // 2 CAP bins in the write pass, fewer entries sharing a bin, measured slower: 30.9 -> 33.2 ms
+    // at 16 rows, the larger histogram's clearing and scan outweigh the rank reads saved), and the
+    // sizes pass's hash set of 2 CAP slots
+    static_assert(CAP == 2048 || CAP == 4096, "CAP is 2048 or 4096");
+    constexpr int NB = CAP;
+    constexpr int kBB = CAP == 2048 ? 11 : 12;
+    constexpr int kHS = 2 * CAP, kHB = (CAP == 2048 ? 12 : 13);
     // sizes pass with u32 offsets: the union's size by LDS hash-set inserts, no sort (HASH)
     constexpr bool HASH = !WRITE && sizeof(K) == 4;
     // the unit's codes as offsets from its first code: u32 whenever every unit spans < 2^32 codes
@@ -269,7 +282,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
     __shared__ __attribute__((aligned(16))) uint16_t sidx[HASH ? 1 : CAP];
     __shared__ __attribute__((aligned(16))) uint32_t htab[HASH ? kHS : 1];   // HASH: offset + 1, 0 = empty
     __shared__ uint32_t htop;   // HASH: the offset 2^32 - 1 (no room for + 1) occurs
-    __shared__ uint32_t hist[CAP];
+    __shared__ uint32_t hist[NB];
     __shared__ uint32_t colrel[WRITE ? CAP : 1];   // WRITE: column of gathered entry i - the unit's first
     // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), and two
     // piece tables (this unit's, the next unit's): the pieces' exclusive prefix of their sizes
@@ -290,7 +303,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
     // up to kShSlotRows rows: the row holding gathered entry 64 m of piece table k (rtab[k][m])
     __shared__ uint8_t rtab[2][CAP / 64];
     constexpr int PER = CAP / NT;   // entries per thread
-    constexpr int BPT = CAP / NT;  // bins per thread
+    constexpr int BPT = NB / NT;   // bins per thread
     const int tid = threadIdx.x;
     for (int r = tid; r < R && r < kShRoffCache; r += NT) sroff[r] = roff[r];
     // (made visible by the first barriers)
@@ -373,7 +386,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
     };
     // the codes of a unit of T (1 .. CAP) entries, table k (visible), all loads in flight;
     // WRITE with up to kShSlotRows rows: the entries' rows packed a byte each into rk, for the index stores
-    auto gather = [&](uint32_t T, int k, uint64_t (&cv)[PER], uint32_t (&rk)[2]) {
+    auto gather = [&](uint32_t T, int k, K (&cv)[PER], uint32_t (&rk)[2]) {
         const uint32_t* const pfx = pfx_of(k);
         const uint32_t* const pa = pa_of(k);
         uint32_t iv[PER];
@@ -397,8 +410,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
 #pragma unroll
             for (int u = 0; u < PER; ++u) at[u] = row_base(rv[u]) + pa[rv[u]] + (iv[u] - pfx[rv[u]]);
         }
+        // (u32 offsets: only the codes' low words are loaded -- a u64 load whose high half the
+        // compiler knew to be dead had that half's register reused while the load was in flight,
+        // and the wait for it (vmcnt) drained the prefetch at the start of the sort)
+        if constexpr (sizeof(K) == 4) {
 #pragma unroll
-        for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
+            for (int u = 0; u < PER; ++u) cv[u] = reinterpret_cast<const uint32_t*>(codes)[2 * at[u]];
+        } else {
+#pragma unroll
+            for (int u = 0; u < PER; ++u) cv[u] = codes[at[u]];
+        }
     };
 
     uint32_t s = blockIdx.x;
@@ -406,13 +427,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
     issue_st(s);
     uint32_t Tc = build(s, 0);
     lds_barrier();
-    uint64_t cv[PER];
+    K cv[PER];   // a unit's codes (u32 offsets: their low words; the offsets wrap correctly)
 #pragma unroll
-    for (int u = 0; u < PER; ++u) cv[u] = 0ull;
+    for (int u = 0; u < PER; ++u) cv[u] = (K)0;
     uint32_t rk[2] = {0u, 0u}, rk2[2] = {0u, 0u};   // (this unit's rows, the next unit's)
     if (Tc >= 1u && Tc <= (uint32_t)CAP) gather(Tc, 0, cv, rk);
     unsigned long long cb = WRITE ? colbase[s] : 0ull;
     int k = 0;
+#ifdef KMH_EXPERIMENTS
+    unsigned long long pt_[16] = {}, tl_ = clock64();
+#endif
     for (;;) {
         const uint32_t s2 = s + gridDim.x;
         const bool has2 = s2 < S;   // (uniform)
@@ -429,6 +453,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
             htop = 0u;
         }
         lds_barrier();
+        KMH_SPT(0)
         const uint32_t T = Tc;
         const bool ok = T >= 1u && T <= (uint32_t)CAP;   // (uniform)
         if (!ok && !WRITE && tid == 0) {   // empty (a part of a coarse cell with no entries) or too big
@@ -449,7 +474,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const uint32_t i = (uint32_t)(u * NT + tid);
-                bv[u] = (uint32_t)min((K)(cv[u] - base) >> bsh, (K)(CAP - 1));
+                bv[u] = (uint32_t)min((K)(cv[u] - (K)base) >> bsh, (K)(NB - 1));
                 if (i < T) atomicAdd(&hist[bv[u]], 1u);
             }
             if constexpr (HASH) {
@@ -459,7 +484,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t i = (uint32_t)(u * NT + tid);
                     if (i < T) {
-                        const uint32_t off = (uint32_t)(cv[u] - base);
+                        const uint32_t off = (uint32_t)(cv[u] - (K)base);
                         if (off == 0xFFFFFFFFu) {
                             htop = 1u;
                         } else {
@@ -479,6 +504,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                 }
             }
             lds_barrier();
+            KMH_SPT(1)
             // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
             //    (HASH: only the check -- the write pass's sort holds the same bins)
             if constexpr (HASH) {
@@ -502,6 +528,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                 }
             }
             lds_barrier();
+            KMH_SPT(2)
             sorted_ok = flag == 0u;   // (uniform)
             if (!sorted_ok && !WRITE && tid == 0) {
                 ucount[s] = 0u;
@@ -514,7 +541,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                     const uint32_t i = (uint32_t)(u * NT + tid);
                     if (i < T) {
                         const uint32_t at = atomicAdd(&hist[bv[u]], 0x10000u) >> 16;
-                        scode[at] = (K)(cv[u] - base);
+                        scode[at] = (K)(cv[u] - (K)base);
                         sidx[at] = (uint16_t)i;
                     }
                 }
@@ -522,10 +549,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
         }
         // this unit's codes are dead: the next unit's pieces, then its loads (landing during
         // this unit's sort, heads and stores)
+        KMH_SPT(3)
         uint32_t T2 = 0u;
         if (has2) T2 = build(s2, k ^ 1);   // (its barriers also order the scatter before the sort)
         lds_barrier();
+        KMH_SPT(4)
         if (has2 && T2 >= 1u && T2 <= (uint32_t)CAP) gather(T2, k ^ 1, cv, rk2);
+        KMH_SPT(5)
         if (HASH && sorted_ok) {
             uint32_t U;
             block_scan<NT>(nf + (tid == 0 ? htop : 0u), ws, &U);
@@ -539,7 +569,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
             for (int u = 0; u < PER; ++u) {
                 const uint32_t p = (uint32_t)(u * NT + tid), pc = p < T ? p : 0u;
                 const K key = scode[pc];
-                const uint32_t b = (uint32_t)min(key >> bsh, (K)(CAP - 1));
+                const uint32_t b = (uint32_t)min(key >> bsh, (K)(NB - 1));
                 const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
                 bool first = true;
                 if (be - bs <= 4u) {
@@ -581,10 +611,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t p = (uint32_t)(u * NT + tid), pc = p < T ? p : 0u;
-                    const uint32_t b = (uint32_t)min(key[u] >> bsh, (K)(CAP - 1));
+                    const uint32_t b = (uint32_t)min(key[u] >> bsh, (K)(NB - 1));
                     const uint32_t h = hist[b], bs = h & 0xFFFFu, be = h >> 16;
                     uint32_t rk = 0u;
-                    if (be - bs <= 4u) {
+                    if (be - bs <= 1u) {
+                        // a bin of one entry stays in place (~40 % of the entries): no reads
+                    } else if (be - bs <= 4u) {
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
                             const uint32_t y = bs + (uint32_t)t;
@@ -609,6 +641,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                 }
             }
             lds_barrier();
+            KMH_SPT(6)
             // 6. run heads = the distinct codes; thread t owns positions PER t .. PER t + PER - 1,
             //    read as 16-byte vectors (PER single reads at a stride of PER words were 8-way bank
             //    conflicts); positions past T hold stale codes and are masked
@@ -640,6 +673,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
             }
             uint32_t U;
             const uint32_t hp = block_scan<NT>(nh, ws, &U);
+            KMH_SPT(7)
             {
                 // the columns from the heads; every entry's column (relative to the unit's
                 // first) into LDS by its gathered index, then stored in gathered order:
@@ -648,23 +682,39 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                 uint32_t run = hp;   // heads before this thread's positions
                 const uint4 ix = *reinterpret_cast<const uint4*>(sidx + PER * tid);
                 const uint32_t ixw[4] = {ix.x, ix.y, ix.z, ix.w};
+                // the heads compacted into scode[0, U) (every thread read its positions before the
+                // scan's barriers, and a head moves down only), then stored lane-consecutively:
+                // a thread's own heads, PER words apart across the lanes, made each store a
+                // separate 64-byte request per lane
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t p = (uint32_t)(PER * tid + u);
                     if (p < T) {
                         if ((hm >> u) & 1u) {
-                            columns[cb + run] = base + (uint64_t)kv[u];
+                            scode[run] = kv[u];
                             ++run;
                         }
                         colrel[(ixw[u >> 1] >> (16 * (u & 1))) & 0xFFFFu] = run - 1u;
                     }
                 }
                 lds_barrier();
-                int rv[PER];
-                if (R <= kShSlotRows) {   // (uniform) the rows found by the gather
+                for (uint32_t j = (uint32_t)tid; j < U; j += NT) columns[cb + j] = base + (uint64_t)scode[j];
+                KMH_SPT(8)
+                if (R <= kShSlotRows) {   // (uniform) the rows found by the gather; all LDS reads, then the stores
+                    const uint64_t* const dl = dl_of(k);
+                    uint64_t ad[PER];
+                    uint32_t cr[PER];
 #pragma unroll
-                    for (int u = 0; u < PER; ++u) rv[u] = (int)((rk[u >> 2] >> (8 * (u & 3))) & 0xFFu);
+                    for (int u = 0; u < PER; ++u) {
+                        const uint32_t i = (uint32_t)(u * NT + tid), ic = i < T ? i : 0u;
+                        ad[u] = dl[(rk[u >> 2] >> (8 * (u & 3))) & 0xFFu] + ic;
+                        cr[u] = colrel[ic];
+                    }
+#pragma unroll
+                    for (int u = 0; u < PER; ++u)
+                        if ((uint32_t)(u * NT + tid) < T) indices[ad[u]] = (IX)(cb + cr[u]);
                 } else {
+                    int rv[PER];
                     uint32_t iv[PER];
 #pragma unroll
                     for (int u = 0; u < PER; ++u) {
@@ -672,20 +722,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                         iv[u] = i < T ? i : 0u;
                     }
                     rows_of(pfx, rtab[k], iv, rv);
-                }
 #pragma unroll
-                for (int u = 0; u < PER; ++u) {
-                    const uint32_t i = (uint32_t)(u * NT + tid);
-                    if (i < T) {
-                        const uint64_t at = R <= kShSlotRows ? dl_of(k)[rv[u]] + i
-                                                             : row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]]);
-                        indices[at] = (IX)(cb + colrel[i]);
+                    for (int u = 0; u < PER; ++u) {
+                        const uint32_t i = (uint32_t)(u * NT + tid);
+                        if (i < T) indices[row_base(rv[u]) + pa[rv[u]] + (i - pfx[rv[u]])] = (IX)(cb + colrel[i]);
                     }
                 }
+                KMH_SPT(9)
             }
         }
         if (!has2) break;
         lds_barrier();   // the LDS tables are rewritten by the next unit
+        KMH_SPT(10)
         s = s2;
         Tc = T2;
         k ^= 1;
@@ -693,6 +741,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
         rk[0] = rk2[0];
         rk[1] = rk2[1];
     }
+#ifdef KMH_EXPERIMENTS
+    if (tid == 0) {
+        pt_[11] = 1u;
+        for (int i = 0; i < 12; ++i) atomicAdd(&g_shard_pt[WRITE ? 1 : 0][i], pt_[i]);
+    }
+#endif
 }
 
 // Exclusive u64 scan of n u32: out[i] = sum of in[0 .. i), out[n] = the total.  Blocks of 4096
@@ -1055,9 +1109,26 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     if ((rc = scan_u32_u64(ctx, d_ucount, S, d_colbase, s))) return rc;
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
+#ifdef KMH_EXPERIMENTS
+    {
+        unsigned long long z[2][16] = {};
+        KMH_HIP(ctx, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_shard_pt), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+    }
+#endif
     time_begin(ctx, s, "k_shard_union");
     if (small) launch_union<256, 2048>(ua, true, s);
     else launch_union<512, 4096>(ua, true, s);
+#ifdef KMH_EXPERIMENTS
+    {
+        unsigned long long z[2][16];
+        KMH_HIP(ctx, hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_shard_pt), sizeof(z), 0, hipMemcpyDeviceToHost, s));
+        KMH_HIP(ctx, hipStreamSynchronize(s));
+        const double wg = (double)std::max(1ull, z[1][11]);
+        std::fprintf(stderr, "[union write phases, Mcyc per workgroup]");
+        for (int i = 0; i < 11; ++i) std::fprintf(stderr, " %d:%.2f", i, z[1][i] / wg / 1e6);
+        std::fprintf(stderr, " (workgroups %.0f)\n", wg);
+    }
+#endif
     time_end(ctx, s);
     KMH_HIP(ctx, hipGetLastError());
     if (nbig) {
