@@ -282,7 +282,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
     __shared__ __attribute__((aligned(16))) uint16_t sidx[HASH ? 1 : CAP];
     __shared__ __attribute__((aligned(16))) uint32_t htab[HASH ? kHS : 1];   // HASH: offset + 1, 0 = empty
     __shared__ uint32_t htop;   // HASH: the offset 2^32 - 1 (no room for + 1) occurs
-    __shared__ uint32_t hist[NB];
+    __shared__ __attribute__((aligned(16))) uint32_t hist[NB];
     __shared__ uint32_t colrel[WRITE ? CAP : 1];   // WRITE: column of gathered entry i - the unit's first
     // dynamic: the rows' offsets (the first kShRoffCache; the rest read from memory), and two
     // piece tables (this unit's, the next unit's): the pieces' exclusive prefix of their sizes
@@ -304,6 +304,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
     __shared__ uint8_t rtab[2][CAP / 64];
     constexpr int PER = CAP / NT;   // entries per thread
     constexpr int BPT = NB / NT;   // bins per thread
+    static_assert(BPT % 4 == 0, "a thread's bins are cleared and checked as 16-byte words");
     const int tid = threadIdx.x;
     for (int r = tid; r < R && r < kShRoffCache; r += NT) sroff[r] = roff[r];
     // (made visible by the first barriers)
@@ -442,7 +443,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
         const bool has2 = s2 < S;   // (uniform)
         if (has2) issue_st(s2);
         const unsigned long long cb2 = WRITE && has2 ? colbase[s2] : 0ull;
-        for (int q = 0; q < BPT; ++q) hist[q * NT + tid] = 0u;
+        {
+            uint4* const hz = reinterpret_cast<uint4*>(hist);
+#pragma unroll
+            for (int q = 0; q < BPT / 4; ++q) hz[q * NT + tid] = make_uint4(0u, 0u, 0u, 0u);
+        }
         if constexpr (HASH) {
             uint4* const h4 = reinterpret_cast<uint4*>(htab);
 #pragma unroll
@@ -464,6 +469,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
         uint64_t base = 0ull;
         int bsh = 0;
         uint32_t nf = 0u;   // HASH: this thread's first occurrences
+        // the unit's codes have landed here on every path (an empty unit included): otherwise the
+        // next gather, writing the same registers, waited for them (vmcnt) behind this unit's
+        // stores -- the loads and stores share one in-order counter
+#pragma unroll
+        for (int u = 0; u < PER; ++u) asm volatile("" : "+v"(cv[u]));
         if (ok) {
             // 2. bins: 12 bits over the unit's span, counted
             base = ub[s];
@@ -508,9 +518,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
             // 3. bin starts (start | start << 16); a bin over kShBin entries sends s to the fallback
             //    (HASH: only the check -- the write pass's sort holds the same bins)
             if constexpr (HASH) {
+                const uint4* const hv = reinterpret_cast<const uint4*>(hist + BPT * tid);
+                uint32_t mx = 0u;
 #pragma unroll
-                for (int q = 0; q < BPT; ++q)
-                    if (hist[BPT * tid + q] > (uint32_t)kShBin) flag = 1u;
+                for (int q = 0; q < BPT / 4; ++q) {
+                    const uint4 v = hv[q];
+                    mx = max(max(mx, max(v.x, v.y)), max(v.z, v.w));
+                }
+                if (mx > (uint32_t)kShBin) flag = 1u;
             } else {
                 uint32_t v[BPT], sum = 0u;
 #pragma unroll
@@ -599,14 +614,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
             //    writes.  (An insertion sort per bin was a chain of dependent LDS round trips that
             //    the whole wave took for every bin slot in which one of its lanes had a bin to sort.)
             {
+                // (a position's destination and its gathered index packed in one register, dst |
+                // index << 16, 0xFFFF = stays: fewer live registers through the sort)
                 K key[PER];
-                uint16_t kix[PER];
-                uint32_t dst[PER];
+                uint32_t dk[PER];
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t p = (uint32_t)(u * NT + tid), pc = p < T ? p : 0u;
                     key[u] = scode[pc];
-                    kix[u] = sidx[pc];
+                    dk[u] = (uint32_t)sidx[pc] << 16;
                 }
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
@@ -624,19 +640,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
                             rk += (y < be && (o < key[u] || (o == key[u] && y < pc))) ? 1u : 0u;
                         }
                     } else {
-                        for (uint32_t y = bs; y < be; ++y) {
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+                        for (uint32_t y = bs; y < be; ++y) {   // (rare: kept small, no spills)
                             const K o = scode[y];
                             rk += (o < key[u] || (o == key[u] && y < pc)) ? 1u : 0u;
                         }
                     }
-                    dst[u] = p < T && be - bs > 1u ? bs + rk : 0xFFFFFFFFu;   // (single entries stay)
+                    dk[u] |= p < T && be - bs > 1u ? bs + rk : 0xFFFFu;   // (single entries stay)
                 }
                 lds_barrier();
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
-                    if (dst[u] != 0xFFFFFFFFu) {
-                        scode[dst[u]] = key[u];
-                        sidx[dst[u]] = kix[u];
+                    const uint32_t d = dk[u] & 0xFFFFu;
+                    if (d != 0xFFFFu) {
+                        scode[d] = key[u];
+                        sidx[d] = (uint16_t)(dk[u] >> 16);
                     }
                 }
             }
@@ -1046,6 +1064,12 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
                  (unsigned)std::min<uint64_t>(S, (uint64_t)std::max(1, ctx->num_cu) * (small ? 5 : 2)), dyn};
     uint32_t* const ix32 = ua.ix32;
     int64_t* const ix64 = ua.ix64;
+#ifdef KMH_EXPERIMENTS
+    {
+        unsigned long long z[2][16] = {};
+        KMH_HIP(ctx, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_shard_pt), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+    }
+#endif
     time_begin(ctx, s, "k_shard_union");
     if (small) launch_union<256, 2048>(ua, false, s);
     else launch_union<512, 4096>(ua, false, s);
@@ -1109,12 +1133,6 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
     if ((rc = scan_u32_u64(ctx, d_ucount, S, d_colbase, s))) return rc;
     unsigned long long total = 0;
     KMH_HIP(ctx, hipMemcpyAsync(&total, d_colbase + S, 8, hipMemcpyDeviceToHost, s));
-#ifdef KMH_EXPERIMENTS
-    {
-        unsigned long long z[2][16] = {};
-        KMH_HIP(ctx, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_shard_pt), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
-    }
-#endif
     time_begin(ctx, s, "k_shard_union");
     if (small) launch_union<256, 2048>(ua, true, s);
     else launch_union<512, 4096>(ua, true, s);
@@ -1127,6 +1145,10 @@ int shard_union(Ctx* ctx, const uint64_t* d_codes, const uint64_t* row_off, int 
         std::fprintf(stderr, "[union write phases, Mcyc per workgroup]");
         for (int i = 0; i < 11; ++i) std::fprintf(stderr, " %d:%.2f", i, z[1][i] / wg / 1e6);
         std::fprintf(stderr, " (workgroups %.0f)\n", wg);
+        const double wg0 = (double)std::max(1ull, z[0][11]);
+        std::fprintf(stderr, "[union sizes phases, Mcyc per workgroup]");
+        for (int i = 0; i < 11; ++i) std::fprintf(stderr, " %d:%.2f", i, z[0][i] / wg0 / 1e6);
+        std::fprintf(stderr, " (workgroups %.0f)\n", wg0);
     }
 #endif
     time_end(ctx, s);
