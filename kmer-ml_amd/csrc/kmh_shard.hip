@@ -489,13 +489,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 &&
             }
             if constexpr (HASH) {
                 // the union's size: inserts into an LDS hash set (linear probing, load <= 1/2); an
-                // entry counts iff its insert finds an empty slot -- no scan, scatter or sort
+                // entry counts iff its insert finds an empty slot -- no scan, scatter or sort.  An
+                // entry alone in its bin (~40 %) has no equal and counts without an insert.
+                lds_barrier();   // (the histogram complete)
 #pragma unroll
                 for (int u = 0; u < PER; ++u) {
                     const uint32_t i = (uint32_t)(u * NT + tid);
                     if (i < T) {
                         const uint32_t off = (uint32_t)(cv[u] - (K)base);
-                        if (off == 0xFFFFFFFFu) {
+                        if (hist[bv[u]] == 1u) {
+                            ++nf;
+                        } else if (off == 0xFFFFFFFFu) {
                             htop = 1u;
                         } else {
                             const uint32_t key = off + 1u;
