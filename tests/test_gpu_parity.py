@@ -1429,7 +1429,7 @@ def _shard_union(ctx, dev, rows, lo, hi_incl):
 
 
 @pytest.mark.parametrize("case", ["distinct", "shared", "identical", "mixed", "narrow", "wide", "many_rows", "dense_cell",
-                                  "max_rows", "slot_rows64", "rows200"])
+                                  "max_rows", "slot_rows64", "rows200", "cell_top"])
 def test_shard_union_vs_numpy(ctx, dev, case):
     """kmh_shard_union_dev (the column union and CSR indices of a shard) against numpy's
     union1d / searchsorted: rows of distinct codes (the LDS path), rows sharing half their codes,
@@ -1443,9 +1443,13 @@ def test_shard_union_vs_numpy(ctx, dev, case):
     through the 64-entry slot table, with one dense window cut into ~120 units whose row pieces
     range from ~20 entries (inside one slot) to ~500 (spanning 7-8 slots, starting at every offset
     of a slot) -- the shape of the only case (dense_cell) that failed the first slot-table build;
-    rows200: 200 rows sharing a pool of codes (the slot table beyond 64 rows, up to its 256)."""
+    rows200: 200 rows sharing a pool of codes (the slot table beyond 64 rows, up to its 256).
+    cell_top: a 2^48-code range (coarse cells of 2^32 codes, u32 offsets) whose sparse cells are
+    single units holding their last code, offset 2^32 - 1 -- the one offset the sizes pass's hash
+    set cannot store as offset + 1 (counted apart), shared by two rows."""
     rng = np.random.default_rng({"distinct": 1, "shared": 2, "identical": 3, "mixed": 4, "narrow": 5, "wide": 6,
-                                 "many_rows": 7, "dense_cell": 8, "max_rows": 9, "slot_rows64": 10, "rows200": 11}[case])
+                                 "many_rows": 7, "dense_cell": 8, "max_rows": 9, "slot_rows64": 10, "rows200": 11,
+                                 "cell_top": 12}[case])
     lo, hi = 1 << 40, (1 << 41) - 1
     if case == "distinct":
         rows = [np.unique(rng.integers(lo, hi, 200_000, dtype=np.uint64)) for _ in range(7)]
@@ -1478,6 +1482,11 @@ def test_shard_union_vs_numpy(ctx, dev, case):
     elif case == "rows200":   # R = 200: the slot table's rows past 64 (config 5's N = 8 shard has 128)
         pool = rng.integers(lo, hi, 3_000_000, dtype=np.uint64)
         rows = [np.unique(rng.choice(pool, 1_000 + 37 * r)) for r in range(200)]
+    elif case == "cell_top":
+        lo, hi = 0, (1 << 48) - 1
+        tops = np.array([(c << 32) - 1 for c in range(1, 40)], np.uint64)   # each cell's last code
+        rows = [np.unique(np.concatenate([tops[r::2], rng.integers(lo, hi, 3_000, dtype=np.uint64)])) for r in range(2)]
+        rows.append(np.unique(np.concatenate([tops, rng.integers(lo, hi, 2_000, dtype=np.uint64)])))
     elif case == "slot_rows64":
         win = lo + (1 << 39) + np.arange(1 << 22, dtype=np.uint64)
         sizes = [40_000 if r % 10 == 0 else 2_000 + 500 * (r % 9) for r in range(64)]
